@@ -1,0 +1,190 @@
+/*
+ * radhip.h — C ABI of libradhip.so, the hand-written HIP (gfx950 / MI355X) kernels of the
+ * Phase-6 audio-deepfake hot path (lux-liang/Robust-Audio-Deepfake-Evolution).
+ *
+ * Conventions ("C-ABI conventions"):
+ *   - extern "C", plain pointers and sizes, no torch types.
+ *   - Every entry point returns int: 0 = ok, > 0 = hipError_t of the failing launch,
+ *     < 0 = argument error (RDX_E*). rdx_strerror() names a code.
+ *   - All device pointers are caller-owned; no entry point allocates device memory
+ *     (workspace sizes are queried with the *_workspace / *_elems helpers).
+ *   - `stream` is a hipStream_t (0 = legacy default stream). Nothing synchronises the host,
+ *     so every launch function is graph-capturable.
+ *   - Tensors are row-major and contiguous unless a leading dimension (ld*) is given.
+ *   - dtype selects the storage type of the "activation" operands (RDX_F32 or RDX_BF16);
+ *     arithmetic is fp32 (fp64 for the RawBoost filters and reductions).
+ *   - No global state: thread-compatible, one process per GPU.
+ *
+ * Each function names the reference interface it replaces (file:line into the reference).
+ */
+#ifndef RADHIP_H
+#define RADHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDX_OK 0
+#define RDX_EINVAL (-1)        /* bad shape / pointer / argument */
+#define RDX_EUNSUPPORTED (-2)  /* shape outside what the kernel is built for */
+
+typedef enum { RDX_F32 = 0, RDX_BF16 = 1 } rdx_dtype;
+
+const char* rdx_version(void);
+const char* rdx_strerror(int code);
+
+/* ------------------------------------------------------------------------------------------
+ * SincConv front end.
+ * Replaces CONV.__init__ filter bank (src/models/DualStreamSEMamba.py:95-117), CONV.forward
+ * (:119-138) and the first step of SincNetEncoder.forward, `max_pool2d(abs(conv), (3,3))` (:251-253).
+ *   x       [batch, len] fp32 waveform
+ *   filters [channels, ksize] fp32 band-pass bank (unmasked)
+ *   channels in [mask_lo, mask_hi) are treated as zeroed filters (the Freq_aug band mask, :121-125)
+ *   out     [batch, channels/3, (len-ksize+1)/3] fp32  = max over 3x3 windows of |conv|
+ * ------------------------------------------------------------------------------------------ */
+int rdx_sincconv_absmaxpool_fwd(const float* x, int64_t batch, int64_t len, const float* filters,
+                                int channels, int ksize, int mask_lo, int mask_hi, float* out,
+                                void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Bidirectional Mamba (replaces mamba_ssm Mamba.forward -> mamba_inner_fn, called twice per
+ * PN_BiMambas_Encoder.forward with a flip, src/models/DualStreamSEMamba.py:467-486; semantics of
+ * the reference-owned MambaBlock, src/models/modules/mamba_block.py:41-122).
+ * Direction 0 scans t = 0..L-1; direction 1 scans the flipped sequence, with every tensor kept at
+ * ORIGINAL positions (no flip is ever materialised). `dirs` = 1 (plain Mamba) or 2 (Bi-Mamba).
+ * ------------------------------------------------------------------------------------------ */
+
+/* Depthwise causal conv (kernel K, bias) + SiLU, for both scan directions.
+ *   x  [B, L, D] with row stride ldx (the x half of in_proj's xz [B, L, 2D])
+ *   w  [D, K] fp32, bias [D] fp32
+ *   u  [dirs, B, L, D]   u[0] causal, u[1] anti-causal (= flip(conv(flip(x)))) */
+int rdx_dwconv_bidir_fwd(int dtype, const void* x, int64_t ldx, const float* w, const float* bias,
+                         void* u, int B, int L, int D, int K, int dirs, void* stream);
+/* Backward. du [dirs, B, L, D]; writes dx (row stride lddx, overwritten), and per-(batch)
+ * partial weight / bias gradients dw_part [B, D, K], db_part [B, D] (fp32; caller sums dim 0). */
+int rdx_dwconv_bidir_bwd(int dtype, const void* x, int64_t ldx, const float* w, const float* bias,
+                         const void* du, void* dx, int64_t lddx, float* dw_part, float* db_part,
+                         int B, int L, int D, int K, int dirs, void* stream);
+
+/* Selective scan, replaces selective_scan_cuda.fwd (mamba_ssm) / MambaBlock.ssm_step
+ * (mamba_block.py:65-122):  dt = softplus(delta + dt_bias);  h = exp(dt*A) h + dt*B*u;
+ * y = C.h + Dp*u, A = -exp(A_log).  N (d_state) must be 16; L <= 640.
+ *   u, delta  [dirs, B, L, D]
+ *   Bm, Cm    [dirs, B, L, N] with row stride ldbc (views into x_proj's [dirs, B, L, R+2N])
+ *   A_log [D, N], Dp [D], dt_bias [D] fp32
+ *   y     [dirs, B, L, D] fp32 out
+ *   ckpt  [dirs, B, nck-1, D, N] fp32 out (state checkpoints for bwd; see rdx_scan_ckpt_elems) */
+int64_t rdx_scan_ckpt_elems(int B, int L, int D, int N, int dirs);
+int rdx_scan_nblk_d(int D);
+int rdx_selective_scan_fwd(int dtype, const void* u, const void* delta, const float* A_log,
+                           const void* Bm, const void* Cm, int64_t ldbc, const float* Dp,
+                           const float* dt_bias, float* y, float* ckpt, int B, int L, int D, int N,
+                           int dirs, void* stream);
+/* Backward. dy [dirs, B, L, D] fp32 with direction stride dy_dir_stride (0 = both directions see
+ * the same dy, the Bi-Mamba case). Outputs:
+ *   du, ddelta [dirs, B, L, D] (dtype)           — overwritten
+ *   dBC_part   [rdx_scan_nblk_d(D), dirs, B, L, 2N] fp32 — partial dB|dC, caller sums dim 0
+ *   dA_part    [dirs*B, D, N] fp32 (d/dA_log)    — caller sums dim 0
+ *   dD_part, dbias_part [dirs*B, D] fp32         — caller sums dim 0 */
+int rdx_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A_log,
+                           const void* Bm, const void* Cm, int64_t ldbc, const float* Dp,
+                           const float* dt_bias, const float* ckpt, const float* dy,
+                           int64_t dy_dir_stride, void* du, void* ddelta, float* dBC_part,
+                           float* dA_part, float* dD_part, float* dbias_part, int B, int L, int D,
+                           int N, int dirs, void* stream);
+
+/* Gate shared by both directions: g = (sum_dir y[dir]) * silu(z);  ysum = sum_dir y[dir].
+ *   y [dirs, B, L, D] fp32, z [B, L, D] with row stride ldz, g [B, L, D] (dtype), ysum fp32. */
+int rdx_bigate_fwd(int dtype, const float* y, int dirs, const void* z, int64_t ldz, void* g,
+                   float* ysum, int B, int L, int D, void* stream);
+/* dy = dg * silu(z) (fp32, [B, L, D]);  dz = dg * ysum * silu'(z) (dtype, row stride lddz). */
+int rdx_bigate_bwd(int dtype, const void* dg, const void* z, int64_t ldz, const float* ysum,
+                   float* dy, void* dz, int64_t lddz, int B, int L, int D, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * WavLM layer-weighted sum, replaces WavLMFrontend.forward's stack + softmax-weighted sum
+ * (src/models/DualStreamSEMamba.py:427-437).  hs: host array of `nl` device pointers, each
+ * [n] elements; w: device [nl] fp32 raw layer weights (softmax taken in-kernel). nl <= 64.
+ * ------------------------------------------------------------------------------------------ */
+int rdx_layer_wsum_fwd(int dtype, int nl, const void* const* hs, const float* w, void* out,
+                       int64_t n, void* stream);
+/* Backward: dhs[l] = softmax(w)_l * g (dtype, overwritten), dot_part [nblk, nl] fp32 partial
+ * sums of <g, h_l>; nblk = rdx_layer_wsum_nblk(n). dw follows on the host side from the dots. */
+int rdx_layer_wsum_nblk(int64_t n);
+int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, const float* w, const void* g,
+                       void* const* dhs, float* dot_part, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * RawBoost, batched over utterances with host-drawn parameters. Replaces RawBoost.process and
+ * its three algorithms (src/rawboost.py:15-95) as called per utterance by
+ * Dataset_ASVspoof2019_train.__getitem__ (src/data_utils.py:169-174).
+ * One record per utterance; arithmetic in fp64.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int64_t offset;   /* first sample of this utterance in x / out (flat buffers)            */
+  int64_t len;      /* samples                                                             */
+  int32_t algo;     /* 0 copy, 1 LnL convolutive, 2 ISD impulsive, 3 SSI stationary, 4 = 1+2 */
+  int32_t n_a;      /* IIR order (1..5) for LnL                                            */
+  double b[6];      /* FIR numerator (product of five (1 + c z^-1))                        */
+  double a[6];      /* IIR denominator, a[0] = 1                                           */
+  double f;         /* non-linearity coefficient  y += f*y^2                               */
+  double beta;      /* ISD: impulse probability 1/beta                                     */
+  double snr_db;    /* SSI: target SNR (dB)                                                */
+  uint64_t seed;    /* Philox key for the per-sample noise of ISD / SSI                    */
+} rdx_rawboost_utt;
+
+/* Workspace: fp64 partial sums [nutt][ceil(total_samples/4096)][2]. */
+int64_t rdx_rawboost_workspace_bytes(int nutt, int64_t total_samples);
+/* noise_isd / noise_ssi: optional device fp64 arrays laid out like x that replace the in-kernel
+ * Philox draws (ISD: the product noise*mask; SSI: the Gaussian noise). Pass NULL in production;
+ * tests pass the reference's numpy draws to get exact parity. */
+int rdx_rawboost_batch(const float* x, float* out, const rdx_rawboost_utt* utts, int nutt,
+                       void* workspace, const double* noise_isd, const double* noise_ssi,
+                       void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * "Poor man's codec": windowed-sinc polyphase resampling, restating
+ * torchaudio.transforms.Resample (sinc_interp_hann, lowpass width 6, rolloff 0.99) as called by
+ * apply_codec_aug (src/data_utils.py:31-59).
+ * rdx_resample_kernel fills the [new_g, 2*width + orig_g] fp32 kernel on the HOST
+ * (orig_g/new_g = orig/new divided by their gcd); returns width via *width_out.
+ * rdx_resample_batch: one launch for all records; out_len = ceil(new_g * len / orig_g).
+ * ------------------------------------------------------------------------------------------ */
+int rdx_resample_kernel(int orig_freq, int new_freq, int lowpass_width, double rolloff,
+                        float* host_kernel, int host_kernel_cap, int* width_out, int* orig_g_out,
+                        int* new_g_out);
+typedef struct {
+  int64_t in_offset, in_len, out_offset, out_len;
+  int32_t orig_g, new_g, width, kern_offset; /* kern_offset into the packed kernel buffer */
+} rdx_resample_job;
+int rdx_resample_batch(const float* in, float* out, const float* kernels,
+                       const rdx_resample_job* jobs, int njobs, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * pad_random / pad + mixup gather: builds the model input batch [nutt, max_len] from
+ * variable-length signals. Replaces pad_random (src/data_utils.py:116-127) / pad (:107-113) and
+ * the mixup blend of train_epoch (src/main.py:1038-1042):
+ *   base[b][i] = sig_b[ start_b + i ]          if len_b >= max_len (crop at start_b)
+ *              = sig_b[ i mod len_b ]          otherwise (tile)
+ *   out[b] = lam * base[b] + (1 - lam) * base[perm[b]]   (perm = NULL -> out = base)
+ * offsets/lens/starts are host arrays of nutt entries; nutt <= 64.
+ * ------------------------------------------------------------------------------------------ */
+int rdx_pad_mixup(const float* sig, const int64_t* offsets, const int64_t* lens,
+                  const int64_t* starts, int nutt, int64_t max_len, const int* perm, float lam,
+                  float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * FGM attack, replaces FGM.attack (src/main.py:85-94): for each tensor i,
+ *   backup_i = p_i;  if (||g_i|| != 0 && !isnan(||g_i||))  p_i += eps * g_i / ||g_i||
+ * Host arrays of ntensors (<= 32) device pointers, fp32. workspace: fp64 [ntensors * 256].
+ * ------------------------------------------------------------------------------------------ */
+int rdx_fgm_attack(int ntensors, float* const* params, const float* const* grads,
+                   float* const* backup, const int64_t* numels, float eps, double* workspace,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RADHIP_H */

@@ -1,0 +1,62 @@
+// Shared helpers for the radhip HIP kernels (gfx950 only: wave64, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include "../../include/radhip.h"
+
+#define RDX_WAVE 64
+
+#define RDX_LAUNCH_CHECK()                          \
+  do {                                              \
+    hipError_t e_ = hipGetLastError();              \
+    if (e_ != hipSuccess) return (int)e_;           \
+  } while (0)
+
+#define RDX_REQUIRE(cond)                           \
+  do {                                              \
+    if (!(cond)) return RDX_EINVAL;                 \
+  } while (0)
+
+namespace rdx {
+
+// Storage-type adapters: all arithmetic is fp32.
+template <typename T> __device__ __forceinline__ float ld(const T* p, int64_t i);
+template <> __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }
+template <> __device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p, int64_t i) {
+  return __bfloat162float(p[i]);
+}
+template <typename T> __device__ __forceinline__ void st(T* p, int64_t i, float v);
+template <> __device__ __forceinline__ void st<float>(float* p, int64_t i, float v) { p[i] = v; }
+template <> __device__ __forceinline__ void st<__hip_bfloat16>(__hip_bfloat16* p, int64_t i, float v) {
+  p[i] = __float2bfloat16(v);
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// F.softplus(x) with the default threshold 20 (mamba_ssm: delta <= 20 ? log1p(exp(delta)) : delta)
+__device__ __forceinline__ float softplusf_(float x) { return x <= 20.f ? log1pf(expf(x)) : x; }
+
+// Sum over the 16 lanes of a DPP row (lanes 16r..16r+15); every lane of the row gets the sum.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xF, 0xF, false));  // row_ror:2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false));  // row_ror:1
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace rdx

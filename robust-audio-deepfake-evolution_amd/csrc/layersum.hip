@@ -1,0 +1,191 @@
+// WavLM layer-weighted sum (25 hidden states) for gfx950.
+//
+// Reference: WavLMFrontend.forward (src/models/DualStreamSEMamba.py:427-437):
+//   stacked = torch.stack(hidden_states)            # materialises 25 x [B, T, 1024]
+//   out = (softmax(layer_weights).view(-1,1,1,1) * stacked).sum(0)
+// Here the states are read in place through a pointer table (no stack copy), the softmax of the
+// 25 weights is taken in-kernel, and every lane streams 16 B per state per step (HBM-bound).
+#include "common.h"
+
+namespace rdx {
+
+constexpr int LWS_MAXL = 64;
+constexpr int LWS_THREADS = 256;
+constexpr int LWS_NBLK = 1024;  // fixed grid for the backward partial dots (grid-stride)
+
+struct PtrTable {
+  const void* p[LWS_MAXL];
+};
+struct MutPtrTable {
+  void* p[LWS_MAXL];
+};
+
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  using type = float4;
+  static __device__ __forceinline__ void load(const float* p, int64_t i, float v[4]) {
+    float4 q = *reinterpret_cast<const float4*>(p + i);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  static __device__ __forceinline__ void store(float* p, int64_t i, const float v[4]) {
+    *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct Vec4<__hip_bfloat16> {
+  static __device__ __forceinline__ void load(const __hip_bfloat16* p, int64_t i, float v[4]) {
+    uint2 q = *reinterpret_cast<const uint2*>(p + i);
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+  static __device__ __forceinline__ void store(__hip_bfloat16* p, int64_t i, const float v[4]) {
+    __hip_bfloat16 b0 = __float2bfloat16(v[0]), b1 = __float2bfloat16(v[1]);
+    __hip_bfloat16 b2 = __float2bfloat16(v[2]), b3 = __float2bfloat16(v[3]);
+    uint2 q;
+    q.x = (uint32_t)(*reinterpret_cast<uint16_t*>(&b0)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&b1)) << 16);
+    q.y = (uint32_t)(*reinterpret_cast<uint16_t*>(&b2)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&b3)) << 16);
+    *reinterpret_cast<uint2*>(p + i) = q;
+  }
+};
+
+__device__ __forceinline__ void softmax_into(const float* __restrict__ w, int nl, float* s_p) {
+  if (threadIdx.x < 64) {
+    float v = (threadIdx.x < nl) ? w[threadIdx.x] : -INFINITY;
+    float m = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float e = (threadIdx.x < nl) ? __expf(v - m) : 0.f;
+    float s = wave_sum(e);
+    if (threadIdx.x < nl) s_p[threadIdx.x] = e / s;
+  }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(LWS_THREADS) void lws_fwd_kernel(PtrTable hs, int nl, const float* __restrict__ w,
+                                                              T* __restrict__ out, int64_t n) {
+  __shared__ float s_p[LWS_MAXL];
+  softmax_into(w, nl, s_p);
+  const int64_t nv = n / 4;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < nl; ++l) {
+      float h[4];
+      Vec4<T>::load(reinterpret_cast<const T*>(hs.p[l]), v * 4, h);
+      const float p = s_p[l];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(p, h[j], acc[j]);
+    }
+    Vec4<T>::store(out, v * 4, acc);
+  }
+  // tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    int64_t i = (n & ~(int64_t)3) + threadIdx.x;
+    float acc = 0.f;
+    for (int l = 0; l < nl; ++l) acc = fmaf(s_p[l], ld(reinterpret_cast<const T*>(hs.p[l]), i), acc);
+    st(out, i, acc);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(LWS_THREADS) void lws_bwd_kernel(PtrTable hs, MutPtrTable dhs, int nl,
+                                                              const float* __restrict__ w,
+                                                              const T* __restrict__ g,
+                                                              float* __restrict__ dot_part, int64_t n) {
+  __shared__ float s_p[LWS_MAXL];
+  __shared__ float s_red[LWS_THREADS / 64][LWS_MAXL];
+  softmax_into(w, nl, s_p);
+  const int64_t nv = n / 4;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int l = 0; l < nl; ++l) {
+    const T* h = reinterpret_cast<const T*>(hs.p[l]);
+    T* dh = reinterpret_cast<T*>(dhs.p[l]);
+    const float p = s_p[l];
+    float dot = 0.f;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+      float gv[4], hv[4], o[4];
+      Vec4<T>::load(g, v * 4, gv);
+      Vec4<T>::load(h, v * 4, hv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { dot = fmaf(gv[j], hv[j], dot); o[j] = p * gv[j]; }
+      Vec4<T>::store(dh, v * 4, o);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+      int64_t i = (n & ~(int64_t)3) + threadIdx.x;
+      float gg = ld(g, i);
+      dot = fmaf(gg, ld(h, i), dot);
+      st(dh, i, p * gg);
+    }
+    dot = wave_sum(dot);
+    if (lane == 0) s_red[wid][l] = dot;
+  }
+  __syncthreads();
+  if (threadIdx.x < nl) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < LWS_THREADS / 64; ++k) s += s_red[k][threadIdx.x];
+    dot_part[(int64_t)blockIdx.x * nl + threadIdx.x] = s;
+  }
+}
+
+}  // namespace rdx
+
+using namespace rdx;
+
+#define LWS_DISPATCH(dtype, ...)                                    \
+  do {                                                              \
+    if ((dtype) == RDX_F32) {                                       \
+      using T = float;                                              \
+      __VA_ARGS__;                                                  \
+    } else if ((dtype) == RDX_BF16) {                               \
+      using T = __hip_bfloat16;                                     \
+      __VA_ARGS__;                                                  \
+    } else {                                                        \
+      return RDX_EINVAL;                                            \
+    }                                                               \
+  } while (0)
+
+extern "C" int rdx_layer_wsum_nblk(int64_t n) {
+  int64_t nv = (n / 4 + LWS_THREADS - 1) / LWS_THREADS;
+  if (nv < 1) nv = 1;
+  return (int)(nv < LWS_NBLK ? nv : LWS_NBLK);
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+extern "C" int rdx_layer_wsum_fwd(int dtype, int nl, const void* const* hs, const float* w, void* out,
+                                  int64_t n, void* stream) {
+  RDX_REQUIRE(hs && w && out && n > 0 && nl > 0);
+  if (nl > LWS_MAXL) return RDX_EUNSUPPORTED;
+  PtrTable t{};
+  for (int l = 0; l < nl; ++l) {
+    RDX_REQUIRE(hs[l] != nullptr);
+    if (!aligned16(hs[l])) return RDX_EUNSUPPORTED;
+    t.p[l] = hs[l];
+  }
+  if (!aligned16(out)) return RDX_EUNSUPPORTED;
+  int nblk = rdx_layer_wsum_nblk(n);
+  LWS_DISPATCH(dtype, hipLaunchKernelGGL(lws_fwd_kernel<T>, dim3(nblk), dim3(LWS_THREADS), 0,
+                                         as_stream(stream), t, nl, w, (T*)out, n));
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+extern "C" int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, const float* w, const void* g,
+                                  void* const* dhs, float* dot_part, int64_t n, void* stream) {
+  RDX_REQUIRE(hs && dhs && w && g && dot_part && n > 0 && nl > 0);
+  if (nl > LWS_MAXL) return RDX_EUNSUPPORTED;
+  PtrTable t{};
+  MutPtrTable dt{};
+  for (int l = 0; l < nl; ++l) {
+    RDX_REQUIRE(hs[l] != nullptr && dhs[l] != nullptr);
+    if (!aligned16(hs[l]) || !aligned16(dhs[l])) return RDX_EUNSUPPORTED;
+    t.p[l] = hs[l];
+    dt.p[l] = dhs[l];
+  }
+  if (!aligned16(g)) return RDX_EUNSUPPORTED;
+  int nblk = rdx_layer_wsum_nblk(n);
+  LWS_DISPATCH(dtype, hipLaunchKernelGGL(lws_bwd_kernel<T>, dim3(nblk), dim3(LWS_THREADS), 0,
+                                         as_stream(stream), t, dt, nl, w, (const T*)g, dot_part, n));
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}

@@ -1,0 +1,129 @@
+"""ctypes binding of libradhip.so (C ABI declared in include/radhip.h).
+
+The library is built in-tree (csrc/Makefile -> radhip/libradhip.so). There is no CPU fallback:
+if the library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RADHIP_LIB", os.path.join(_HERE, "libradhip.so"))
+
+RDX_F32 = 0
+RDX_BF16 = 1
+
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+c_vp = ctypes.c_void_p
+c_fp = ctypes.c_void_p  # float* passed as raw address
+
+
+class RawboostUtt(ctypes.Structure):
+    """Mirror of rdx_rawboost_utt (include/radhip.h)."""
+
+    _fields_ = [
+        ("offset", c_i64),
+        ("len", c_i64),
+        ("algo", ctypes.c_int32),
+        ("n_a", ctypes.c_int32),
+        ("b", c_f64 * 6),
+        ("a", c_f64 * 6),
+        ("f", c_f64),
+        ("beta", c_f64),
+        ("snr_db", c_f64),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class ResampleJob(ctypes.Structure):
+    """Mirror of rdx_resample_job (include/radhip.h)."""
+
+    _fields_ = [
+        ("in_offset", c_i64),
+        ("in_len", c_i64),
+        ("out_offset", c_i64),
+        ("out_len", c_i64),
+        ("orig_g", ctypes.c_int32),
+        ("new_g", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("kern_offset", ctypes.c_int32),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "rdx_version": (ctypes.c_char_p, []),
+    "rdx_strerror": (ctypes.c_char_p, [c_int]),
+    "rdx_sincconv_absmaxpool_fwd": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "rdx_dwconv_bidir_fwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_dwconv_bidir_bwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                     c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_scan_ckpt_elems": (c_i64, [c_int, c_int, c_int, c_int, c_int]),
+    "rdx_scan_nblk_d": (c_int, [c_int]),
+    "rdx_selective_scan_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                       c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_selective_scan_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_bigate_fwd": (c_int, [c_int, c_vp, c_int, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "rdx_bigate_bwd": (c_int, [c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
+    "rdx_layer_wsum_fwd": (c_int, [c_int, c_int, ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_vp]),
+    "rdx_layer_wsum_nblk": (c_int, [c_i64]),
+    "rdx_layer_wsum_bwd": (c_int, [c_int, c_int, ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.POINTER(c_vp), c_vp,
+                                   c_i64, c_vp]),
+    "rdx_rawboost_workspace_bytes": (c_i64, [c_int, c_i64]),
+    "rdx_rawboost_batch": (c_int, [c_vp, c_vp, ctypes.POINTER(RawboostUtt), c_int, c_vp, c_vp, c_vp, c_vp]),
+    "rdx_resample_kernel": (c_int, [c_int, c_int, c_int, c_f64, ctypes.POINTER(c_f32), c_int,
+                                    ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "rdx_resample_batch": (c_int, [c_vp, c_vp, c_vp, ctypes.POINTER(ResampleJob), c_int, c_vp]),
+    "rdx_pad_mixup": (c_int, [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_int,
+                              c_i64, ctypes.POINTER(c_int), c_f32, c_vp, c_vp]),
+    "rdx_fgm_attack": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                               ctypes.POINTER(c_i64), c_f32, c_vp, c_vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def header_symbols():
+    """Function names declared in include/radhip.h (used by the export test)."""
+    import re
+    hdr = os.path.join(_HERE, "..", "..", "include", "radhip.h")
+    text = open(hdr).read()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int64_t|int)\s+(rdx_\w+)\s*\(", text, re.M)))
+
+
+def lib():
+    """Load libradhip.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"libradhip.so not found at {LIB_PATH}: build it with `make -C csrc` "
+                    "(or __graft_entry__.build()); there is no CPU fallback for the HIP path")
+            L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(code, what=""):
+    if code != 0:
+        msg = lib().rdx_strerror(int(code)).decode()
+        raise RuntimeError(f"radhip {what} failed: code {code} ({msg})")
+
+
+def ptr_array(ptrs):
+    arr = (c_vp * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr

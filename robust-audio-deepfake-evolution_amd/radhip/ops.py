@@ -1,0 +1,282 @@
+"""PyTorch-facing wrappers of the libradhip.so C ABI (device memory, streams and autograd only).
+
+Every op here runs the hand-written HIP kernel on the tensor's current HIP stream; there is no CPU
+path. Tensors must live on a ROCm device.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr_array
+
+_DT = {torch.float32: _lib.RDX_F32, torch.bfloat16: _lib.RDX_BF16}
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _dtype_code(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"radhip: unsupported dtype {t.dtype} (float32 / bfloat16 only)")
+
+
+def _require_gpu(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError("radhip ops run on the GPU only (tensor on %s)" % t.device)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# --------------------------------------------------------------------------------- SincConv ----
+def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0):
+    """|conv1d(x, filters)| max-pooled 3x3 over (channel, time): [B, L] -> [B, C//3, (L-K+1)//3].
+
+    Replaces CONV.forward + F.max_pool2d(torch.abs(.), (3, 3))
+    (reference src/models/DualStreamSEMamba.py:119-138, :250-253).
+    """
+    _require_gpu(x, filters)
+    x = x.contiguous().float()
+    filters = filters.contiguous().float()
+    B, L = x.shape
+    C, K = filters.shape
+    out = torch.empty(B, C // 3, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
+    check(lib().rdx_sincconv_absmaxpool_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi), _p(out),
+                                            _stream(x)), "sincconv_absmaxpool_fwd")
+    return out
+
+
+# ------------------------------------------------------------------------------ Bi-Mamba -------
+def _rowview_ld(x):
+    """x: [B, L, D] view with unit inner stride and rows of stride ld; returns ld."""
+    B, L, D = x.shape
+    if x.stride(2) != 1 or x.stride(0) != L * x.stride(1):
+        raise ValueError("radhip: expected a [B, L, D] row view (inner stride 1, batch stride L*ld)")
+    return x.stride(1)
+
+
+class DWConvBidir(torch.autograd.Function):
+    """Depthwise causal conv + SiLU for both scan directions (mamba causal_conv1d stage)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, dirs):
+        _require_gpu(x)
+        B, L, D = x.shape
+        ldx = _rowview_ld(x)
+        w = weight.reshape(D, -1).contiguous().float()
+        b = bias.contiguous().float()
+        K = w.shape[1]
+        u = torch.empty(dirs, B, L, D, device=x.device, dtype=x.dtype)
+        check(lib().rdx_dwconv_bidir_fwd(_dtype_code(x), _p(x), ldx, _p(w), _p(b), _p(u), B, L, D, K, dirs,
+                                         _stream(x)), "dwconv_bidir_fwd")
+        ctx.save_for_backward(x, w, b)
+        ctx.dirs = dirs
+        ctx.wshape = weight.shape
+        return u
+
+    @staticmethod
+    def backward(ctx, du):
+        x, w, b = ctx.saved_tensors
+        B, L, D = x.shape
+        K = w.shape[1]
+        du = du.contiguous().to(x.dtype)
+        dx = torch.empty(B, L, D, device=x.device, dtype=x.dtype)
+        dw_part = torch.empty(B, D, K, device=x.device, dtype=torch.float32)
+        db_part = torch.empty(B, D, device=x.device, dtype=torch.float32)
+        check(lib().rdx_dwconv_bidir_bwd(_dtype_code(x), _p(x), _rowview_ld(x), _p(w), _p(b), _p(du), _p(dx), D,
+                                         _p(dw_part), _p(db_part), B, L, D, K, ctx.dirs, _stream(x)),
+              "dwconv_bidir_bwd")
+        return dx, dw_part.sum(0).view(ctx.wshape), db_part.sum(0), None
+
+
+class SelectiveScan(torch.autograd.Function):
+    """y[dir] = scan(u[dir], softplus(delta[dir] + dt_bias), A = -exp(A_log), B, C) + D*u[dir]."""
+
+    @staticmethod
+    def forward(ctx, u, delta, A_log, Bm, Cm, Dp, dt_bias):
+        _require_gpu(u)
+        dirs, B, L, D = u.shape
+        N = A_log.shape[1]
+        dt = u.dtype
+        u = u.contiguous()
+        delta = delta.contiguous().to(dt)
+        if Bm.dtype != dt:
+            Bm, Cm = Bm.to(dt), Cm.to(dt)
+        ldbc = Bm.stride(2)
+        if Bm.stride(3) != 1 or Cm.stride(2) != ldbc or Bm.stride(1) != L * ldbc or Bm.stride(0) != B * L * ldbc:
+            raise ValueError("radhip: B / C must be column slices of one [dirs, B, L, R+2N] tensor")
+        A_log = A_log.contiguous().float()
+        Dp = Dp.contiguous().float()
+        dt_bias = dt_bias.contiguous().float()
+        y = torch.empty(dirs, B, L, D, device=u.device, dtype=torch.float32)
+        ck = torch.empty(lib().rdx_scan_ckpt_elems(B, L, D, N, dirs), device=u.device, dtype=torch.float32)
+        check(lib().rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc, _p(Dp),
+                                           _p(dt_bias), _p(y), _p(ck), B, L, D, N, dirs, _stream(u)),
+              "selective_scan_fwd")
+        ctx.save_for_backward(u, delta, A_log, Bm, Cm, Dp, dt_bias, ck)
+        ctx.ldbc = ldbc
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        u, delta, A_log, Bm, Cm, Dp, dt_bias, ck = ctx.saved_tensors
+        dirs, B, L, D = u.shape
+        N = A_log.shape[1]
+        dy = dy.float()
+        if dirs > 1 and dy.stride(0) == 0 and dy[0].is_contiguous():
+            dy_stride = 0
+        else:
+            dy = dy.contiguous()
+            dy_stride = B * L * D
+        du = torch.empty_like(u)
+        ddelta = torch.empty_like(u)
+        nblk = lib().rdx_scan_nblk_d(D)
+        dBC = torch.empty(nblk, dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)
+        dA = torch.empty(dirs * B, D, N, device=u.device, dtype=torch.float32)
+        dD = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
+        dbias = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
+        check(lib().rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ctx.ldbc,
+                                           _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du), _p(ddelta),
+                                           _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs, _stream(u)),
+              "selective_scan_bwd")
+        dBC = dBC.sum(0).to(Bm.dtype)
+        return du, ddelta, dA.sum(0), dBC[..., :N], dBC[..., N:], dD.sum(0), dbias.sum(0)
+
+
+class BiGate(torch.autograd.Function):
+    """g = (sum over directions of y) * silu(z)."""
+
+    @staticmethod
+    def forward(ctx, y, z):
+        _require_gpu(y, z)
+        dirs, B, L, D = y.shape
+        y = y.contiguous()
+        ldz = _rowview_ld(z)
+        g = torch.empty(B, L, D, device=z.device, dtype=z.dtype)
+        ysum = torch.empty(B, L, D, device=z.device, dtype=torch.float32)
+        check(lib().rdx_bigate_fwd(_dtype_code(z), _p(y), dirs, _p(z), ldz, _p(g), _p(ysum), B, L, D, _stream(z)),
+              "bigate_fwd")
+        ctx.save_for_backward(z, ysum)
+        ctx.dirs = dirs
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        z, ysum = ctx.saved_tensors
+        B, L, D = z.shape
+        dg = dg.contiguous().to(z.dtype)
+        dy = torch.empty(B, L, D, device=z.device, dtype=torch.float32)
+        dz = torch.empty(B, L, D, device=z.device, dtype=z.dtype)
+        check(lib().rdx_bigate_bwd(_dtype_code(z), _p(dg), _p(z), _rowview_ld(z), _p(ysum), _p(dy), _p(dz), D, B, L,
+                                   D, _stream(z)), "bigate_bwd")
+        return dy.unsqueeze(0).expand(ctx.dirs, B, L, D), dz
+
+
+# ------------------------------------------------------------------- layer-weighted sum ------
+class LayerWeightedSum(torch.autograd.Function):
+    """sum_l softmax(w)_l * h_l over the WavLM hidden states, without stacking them."""
+
+    @staticmethod
+    def forward(ctx, w, *hs):
+        _require_gpu(w, *hs)
+        h0 = hs[0]
+        dt = h0.dtype
+        hs = tuple(h if (h.dtype == dt and h.is_contiguous()) else h.to(dt).contiguous() for h in hs)
+        wf = w.detach().contiguous().float()
+        out = torch.empty_like(hs[0])
+        check(lib().rdx_layer_wsum_fwd(_dtype_code(h0), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
+                                       _p(out), out.numel(), _stream(out)), "layer_wsum_fwd")
+        ctx.save_for_backward(wf, *hs)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        wf, *hs = ctx.saved_tensors
+        g = g.contiguous().to(hs[0].dtype)
+        dhs = [torch.empty_like(h) for h in hs]
+        n = g.numel()
+        nblk = lib().rdx_layer_wsum_nblk(n)
+        dots = torch.empty(nblk, len(hs), device=g.device, dtype=torch.float32)
+        check(lib().rdx_layer_wsum_bwd(_dtype_code(g), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf), _p(g),
+                                       ptr_array([d.data_ptr() for d in dhs]), _p(dots), n, _stream(g)),
+              "layer_wsum_bwd")
+        dots = dots.sum(0)
+        p = torch.softmax(wf, 0)
+        dw = p * (dots - (p * dots).sum())
+        return (dw, *dhs)
+
+
+def layer_weighted_sum(hidden_states, layer_weights):
+    return LayerWeightedSum.apply(layer_weights, *hidden_states)
+
+
+# ------------------------------------------------------------------------------------ FGM ----
+def fgm_attack(params, grads, backups, eps):
+    """backup <- p; p += eps * g / ||g|| per tensor (skip when the norm is 0 or NaN). fp32 tensors."""
+    assert len(params) == len(grads) == len(backups) and len(params) > 0
+    _require_gpu(*params)
+    for p, g, b in zip(params, grads, backups):
+        assert p.dtype == g.dtype == b.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous()
+    ws = torch.empty(len(params) * 256, device=params[0].device, dtype=torch.float64)
+    n = len(params)
+    numels = (ctypes.c_int64 * n)(*[p.numel() for p in params])
+    check(lib().rdx_fgm_attack(n, ptr_array([p.data_ptr() for p in params]), ptr_array([g.data_ptr() for g in grads]),
+                               ptr_array([b.data_ptr() for b in backups]), numels, float(eps), _p(ws),
+                               _stream(params[0])), "fgm_attack")
+
+
+# ---------------------------------------------------------------------------- augmentation ----
+def rawboost_batch(x_flat, records, noise_isd=None, noise_ssi=None):
+    """Apply RawBoost to every utterance of a flat fp32 buffer; records: list of RawboostUtt."""
+    _require_gpu(x_flat)
+    x_flat = x_flat.contiguous().float()
+    out = torch.empty_like(x_flat)
+    n = len(records)
+    arr = (_lib.RawboostUtt * n)(*records)
+    total = int(sum(r.len for r in records))
+    wsb = lib().rdx_rawboost_workspace_bytes(n, max(total, 1))
+    ws = torch.empty(max(wsb, 8), device=x_flat.device, dtype=torch.uint8)
+    ni = _p(noise_isd) if noise_isd is not None else None
+    ns = _p(noise_ssi) if noise_ssi is not None else None
+    check(lib().rdx_rawboost_batch(_p(x_flat), _p(out), arr, n, _p(ws), ni, ns, _stream(x_flat)), "rawboost_batch")
+    return out
+
+
+def resample_kernel(orig_freq, new_freq, lowpass_width=6, rolloff=0.99):
+    """Host fp32 kernel [new_g, 2*width+orig_g] (torchaudio sinc_interp_hann restatement)."""
+    w = ctypes.c_int()
+    og = ctypes.c_int()
+    ng = ctypes.c_int()
+    check(lib().rdx_resample_kernel(orig_freq, new_freq, lowpass_width, rolloff, None, 0, ctypes.byref(w),
+                                    ctypes.byref(og), ctypes.byref(ng)), "resample_kernel")
+    kw = 2 * w.value + og.value
+    buf = (ctypes.c_float * (ng.value * kw))()
+    check(lib().rdx_resample_kernel(orig_freq, new_freq, lowpass_width, rolloff, buf, len(buf), ctypes.byref(w),
+                                    ctypes.byref(og), ctypes.byref(ng)), "resample_kernel")
+    t = torch.tensor(list(buf), dtype=torch.float32).view(ng.value, kw)
+    return t, w.value, og.value, ng.value
+
+
+def resample_batch(x_flat, out_flat, kernels_dev, jobs):
+    _require_gpu(x_flat, out_flat, kernels_dev)
+    arr = (_lib.ResampleJob * len(jobs))(*jobs)
+    check(lib().rdx_resample_batch(_p(x_flat), _p(out_flat), _p(kernels_dev), arr, len(jobs), _stream(x_flat)),
+          "resample_batch")
+
+
+def pad_mixup(sig_flat, offsets, lens, starts, max_len, perm=None, lam=1.0):
+    """[nutt, max_len] batch: crop (len >= max_len, at starts[b]) or tile, then mixup with perm."""
+    _require_gpu(sig_flat)
+    n = len(offsets)
+    out = torch.empty(n, max_len, device=sig_flat.device, dtype=torch.float32)
+    I64 = ctypes.c_int64 * n
+    pa = (ctypes.c_int * n)(*perm) if perm is not None else None
+    check(lib().rdx_pad_mixup(_p(sig_flat), I64(*offsets), I64(*lens), I64(*starts), n, int(max_len), pa, float(lam),
+                              _p(out), _stream(sig_flat)), "pad_mixup")
+    return out

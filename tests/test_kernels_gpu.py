@@ -1,0 +1,262 @@
+"""Parity of every HIP kernel (through the C ABI) with the oracle on the same seeded inputs."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from seeded import seeded_array, seeded_fill_
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+# ------------------------------------------------------------------------------- SincConv ----
+@pytest.mark.parametrize("mask", [(0, 0), (12, 31), (60, 70)])
+def test_sincconv_absmaxpool_full_length(mask):
+    from oracle.sinc import sinc_filterbank, sincconv_absmaxpool
+    from radhip.ops import sincconv_absmaxpool as hip_sinc
+    bank = sinc_filterbank()
+    x = seeded_array("k.sinc", (2, 64600), scale=0.1).astype(np.float32)
+    out = hip_sinc(torch.from_numpy(x).to(DEV), bank.to(DEV), *mask).cpu().numpy()
+    ref = sincconv_absmaxpool(x, bank.numpy(), *mask)
+    assert out.shape == ref.shape == (2, 23, 21490)
+    np.testing.assert_allclose(out, ref, rtol=1e-4, atol=2e-6)
+
+
+def test_sincconv_golden(golden):
+    from radhip.ops import sincconv_absmaxpool as hip_sinc
+    g = golden("sinc_conv.npz")
+    out = hip_sinc(torch.from_numpy(g["x"][:, 0]).to(DEV), torch.from_numpy(g["band_pass"]).to(DEV),
+                   int(g["mask_lo"]), int(g["mask_hi"])).cpu().numpy()
+    np.testing.assert_allclose(out, g["pooled_masked"], rtol=1e-4, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------- Bi-Mamba -----
+def _mamba_pair(d_model, seed):
+    from oracle.mamba import MambaRef
+    from radhip.mamba import Mamba
+    ref = MambaRef(d_model, 16)
+    seeded_fill_(ref, seed=seed)
+    hip = Mamba(d_model, 16)
+    hip.load_state_dict(ref.state_dict())
+    return ref.double(), hip.to(DEV)
+
+
+@pytest.mark.parametrize("dirs,d_model,L,B", [(1, 16, 23, 2), (2, 16, 19, 2), (2, 144, 201, 2), (1, 144, 201, 3)])
+def test_mamba_fwd_bwd_fp32(dirs, d_model, L, B):
+    from oracle.mamba import bimamba_ref
+    ref, hip = _mamba_pair(d_model, 100 + d_model)
+    x = seeded_array(f"k.mamba.{d_model}.{L}", (B, L, d_model))
+    r = seeded_array(f"k.mamba.r.{d_model}.{L}", (B, L, d_model))
+    xr = torch.from_numpy(x).requires_grad_(True)
+    yr = bimamba_ref(ref, xr) if dirs == 2 else ref(xr)
+    (yr * torch.from_numpy(r)).sum().backward()
+    xh = torch.from_numpy(x).float().to(DEV).requires_grad_(True)
+    yh = hip.bidirectional(xh) if dirs == 2 else hip(xh)
+    (yh * torch.from_numpy(r).float().to(DEV)).sum().backward()
+    assert _rel(yh.detach().cpu(), yr.detach()) < 2e-5
+    assert _rel(xh.grad.cpu(), xr.grad) < 1e-4
+    for (k, pr), (k2, ph) in zip(ref.named_parameters(), hip.named_parameters()):
+        assert k == k2
+        assert _rel(ph.grad.cpu(), pr.grad) < 2e-4, k
+
+
+def test_mamba_golden_reference_block(golden):
+    """Product Mamba on the reference MambaBlock's own fixture (fp32)."""
+    from radhip.mamba import Mamba
+    g = golden("mamba_block.npz")
+    m = Mamba(16, 16)
+    seeded_fill_(m, seed=21)
+    m = m.to(DEV)
+    x = torch.from_numpy(g["x"]).to(DEV).requires_grad_(True)
+    y = m(x)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), g["y"], rtol=1e-4, atol=1e-5)
+    (y * torch.from_numpy(g["r"]).to(DEV)).sum().backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), g["dx"], rtol=1e-3, atol=1e-5)
+    for k, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), g[f"grad:{k}"], rtol=2e-3, atol=1e-5, err_msg=k)
+
+
+def test_mamba_bf16_autocast():
+    from oracle.mamba import bimamba_ref
+    ref, hip = _mamba_pair(144, 7)
+    x = seeded_array("k.mamba.bf16", (4, 201, 144))
+    with torch.no_grad():
+        yr = bimamba_ref(ref, torch.from_numpy(x)).numpy()
+    xh = torch.from_numpy(x).float().to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yh = hip.bidirectional(xh)
+    yh.float().sum().backward()
+    assert torch.isfinite(xh.grad).all()
+    assert _rel(yh.float().detach().cpu(), yr) < 3e-2
+
+
+def test_dwconv_both_directions_vs_torch():
+    from radhip.ops import DWConvBidir
+    B, L, D = 3, 57, 40
+    xz = torch.randn(B, L, 2 * D, device=DEV, dtype=torch.float64).float().requires_grad_(True)
+    w = torch.randn(D, 1, 4, device=DEV).requires_grad_(True)
+    b = torch.randn(D, device=DEV).requires_grad_(True)
+    u = DWConvBidir.apply(xz[..., :D], w, b, 2)
+    xt = xz[..., :D].transpose(1, 2)
+    u0 = F.silu(F.conv1d(xt, w, b, padding=3, groups=D)[..., :L]).transpose(1, 2)
+    u1 = torch.flip(F.silu(F.conv1d(torch.flip(xt, [2]), w, b, padding=3, groups=D)[..., :L]), [2]).transpose(1, 2)
+    torch.testing.assert_close(u[0], u0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(u[1], u1, rtol=1e-5, atol=1e-6)
+    r = torch.randn_like(u)
+    g_h = torch.autograd.grad((u * r).sum(), (xz, w, b))
+    g_t = torch.autograd.grad((torch.stack([u0, u1]) * r).sum(), (xz, w, b))
+    for a, c in zip(g_h, g_t):
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-5)
+
+
+# -------------------------------------------------------------------- layer-weighted sum -----
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layer_weighted_sum(dtype):
+    from radhip.ops import layer_weighted_sum
+    hs = [torch.randn(2, 201, 1024, device=DEV).to(dtype).requires_grad_(True) for _ in range(25)]
+    w = torch.randn(25, device=DEV).requires_grad_(True)
+    out = layer_weighted_sum(hs, w)
+    ref = (F.softmax(w, 0).view(-1, 1, 1, 1) * torch.stack([h.float() for h in hs])).sum(0)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+    g = torch.randn_like(ref)
+    gh = torch.autograd.grad((out.float() * g).sum(), [w] + hs)
+    gr = torch.autograd.grad((ref * g).sum(), [w] + hs)
+    torch.testing.assert_close(gh[0], gr[0], rtol=1e-3 if dtype == torch.float32 else 5e-2, atol=1e-3)
+    for a, c in zip(gh[1:], gr[1:]):
+        torch.testing.assert_close(a.float(), c.float(), rtol=tol, atol=tol)
+
+
+# ------------------------------------------------------------------------------- RawBoost -----
+def _records_from_draws(draws, lens, seed=0):
+    from radhip._lib import RawboostUtt
+    recs, off = [], 0
+    for d, n in zip(draws, lens):
+        r = RawboostUtt()
+        r.offset, r.len, r.algo, r.seed = off, n, d["algo"], seed
+        if "lnl" in d:
+            b = np.zeros(6)
+            b[:len(d["lnl"]["b"])] = d["lnl"]["b"]
+            a = np.zeros(6)
+            a[:len(d["lnl"]["a"])] = d["lnl"]["a"]
+            r.b[:] = list(b)
+            r.a[:] = list(a)
+            r.n_a = len(d["lnl"]["a"]) - 1
+            r.f = d["lnl"]["f"]
+        if "isd" in d:
+            r.beta = d["isd"]["beta"]
+        if "ssi" in d:
+            r.snr_db = d["ssi"]["snr"]
+        recs.append(r)
+        off += n
+    return recs
+
+
+def test_rawboost_batch_exact_with_reference_draws():
+    from oracle import rawboost as orb
+    from radhip.ops import rawboost_batch
+    lens = [64000, 64000, 37000, 64000, 5000, 64000, 64000, 64000]
+    algos = [1, 2, 3, 4, 1, 4, 0, 3]
+    rng = np.random.RandomState(42)
+    xs = [(0.1 * rng.randn(n)).astype(np.float32) for n in lens]
+    draws, refs = [], []
+    for x, a in zip(xs, algos):
+        d = orb.draw_process(len(x), [a], rng) if a else {"algo": 0}
+        draws.append(d)
+        refs.append(orb.apply_process(x.astype(np.float64), d))
+    isd = np.concatenate([d["isd"]["nm"] if "isd" in d else np.zeros(n) for d, n in zip(draws, lens)])
+    ssi = np.concatenate([d["ssi"]["noise"] if "ssi" in d else np.zeros(n) for d, n in zip(draws, lens)])
+    flat = torch.from_numpy(np.concatenate(xs)).to(DEV)
+    out = rawboost_batch(flat, _records_from_draws(draws, lens), torch.from_numpy(isd).to(DEV),
+                         torch.from_numpy(ssi).to(DEV)).cpu().numpy()
+    off = 0
+    for n, ref, a in zip(lens, refs, algos):
+        np.testing.assert_allclose(out[off:off + n], ref.astype(np.float32), rtol=2e-6, atol=2e-7,
+                                   err_msg=f"algo {a}")
+        off += n
+
+
+def test_rawboost_philox_statistics():
+    from radhip.ops import rawboost_batch
+    n = 64000
+    x = torch.full((3 * n,), 0.1, device=DEV)
+    draws = [{"algo": 2, "isd": {"beta": 5}}, {"algo": 2, "isd": {"beta": 9}}, {"algo": 3, "ssi": {"snr": 20.0}}]
+    out = rawboost_batch(x, _records_from_draws(draws, [n] * 3, seed=1234)).cpu().numpy().astype(np.float64)
+    for i, beta in enumerate([5, 9]):
+        seg = out[i * n:(i + 1) * n]
+        frac = np.mean(seg != np.float32(0.1))
+        assert abs(frac - 1 / beta) < 0.01
+        nz = (seg[seg != np.float32(0.1)] - 0.1) / 0.2      # = noise samples
+        assert abs(nz.mean()) < 0.05 and abs(nz.std() - 1) < 0.05
+    seg = out[2 * n:]
+    noise = seg - 0.1
+    snr = 10 * np.log10(np.sum(np.full(n, 0.1) ** 2) / np.sum(noise ** 2))
+    assert abs(snr - 20.0) < 0.01
+
+
+# ---------------------------------------------------------------------- codec resampling ----
+@pytest.mark.parametrize("sr", [8000, 6000, 4000])
+def test_resample_roundtrip(sr):
+    from oracle.resample import resample
+    from radhip._lib import ResampleJob
+    from radhip.ops import resample_batch, resample_kernel
+    x = seeded_array(f"k.rs.{sr}", (30011,), scale=0.1)
+    kd, wd, ogd, ngd = resample_kernel(16000, sr)
+    ku, wu, ogu, ngu = resample_kernel(sr, 16000)
+    kern = torch.cat([kd.reshape(-1), ku.reshape(-1)]).to(DEV)
+    n_down = -(-ngd * len(x) // ogd)
+    n_up = -(-ngu * n_down // ogu)
+    xin = torch.from_numpy(x).float().to(DEV)
+    mid = torch.empty(n_down, device=DEV)
+    out = torch.empty(n_up, device=DEV)
+    resample_batch(xin, mid, kern, [ResampleJob(0, len(x), 0, n_down, ogd, ngd, wd, 0)])
+    resample_batch(mid, out, kern, [ResampleJob(0, n_down, 0, n_up, ogu, ngu, wu, kd.numel())])
+    ref_mid = resample(x.astype(np.float32).astype(np.float64), 16000, sr)
+    ref = resample(ref_mid, sr, 16000)
+    np.testing.assert_allclose(mid.cpu().numpy(), ref_mid, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=0, atol=4e-6)
+
+
+# ----------------------------------------------------------------------- pad + mixup ---------
+def test_pad_mixup_gather():
+    from oracle.data import pad
+    from radhip.ops import pad_mixup
+    lens = [1000, 64600, 70000, 64000]
+    sig = [seeded_array(f"k.pad.{n}", (n,)).astype(np.float32) for n in lens]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    starts = [0, 0, 3333, 0]
+    flat = torch.from_numpy(np.concatenate(sig)).to(DEV)
+    perm = [2, 0, 3, 1]
+    lam = 0.3
+    out = pad_mixup(flat, offs, lens, starts, 64600, perm, lam).cpu().numpy()
+    base = [pad(s) if n < 64600 else s[st:st + 64600] for s, n, st in zip(sig, lens, starts)]
+    for b in range(4):
+        np.testing.assert_allclose(out[b], lam * base[b] + (1 - lam) * base[perm[b]], rtol=1e-6, atol=1e-7)
+    plain = pad_mixup(flat, offs, lens, starts, 64600).cpu().numpy()
+    for b in range(4):
+        np.testing.assert_array_equal(plain[b], base[b])
+
+
+# ------------------------------------------------------------------------------------ FGM ----
+def test_fgm_attack_matches_reference_fixture(golden):
+    from radhip.ops import fgm_attack
+    g = golden("train_toy.npz")
+    keys = [k.split(":", 1)[1] for k in g if k.startswith("fgm_before:") and "feature_projection" in k]
+    ps = [torch.from_numpy(g[f"fgm_before:{k}"]).to(DEV).contiguous() for k in keys]
+    gs = [torch.from_numpy(g[f"fgm_grad:{k}"]).to(DEV).contiguous() for k in keys]
+    bk = [torch.empty_like(p) for p in ps]
+    fgm_attack(ps, gs, bk, 0.5)
+    for k, p, b in zip(keys, ps, bk):
+        np.testing.assert_allclose(p.cpu().numpy(), g[f"fgm_attacked:{k}"], rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(b.cpu().numpy(), g[f"fgm_before:{k}"])
+    # zero gradient: untouched
+    p = torch.ones(10, device=DEV)
+    fgm_attack([p], [torch.zeros(10, device=DEV)], [torch.empty(10, device=DEV)], 0.5)
+    assert torch.equal(p, torch.ones(10, device=DEV))
