@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""Phase-6 training throughput on MI355X (BASELINE.json metric: train utts/sec).
+
+One step = one optimizer step of the Phase-6 recipe on every rank: `accum` (4) micro-batches of
+`micro_batch` (8) synthetic utterances, each micro-batch = GPU RawBoost (algo 5, p 0.8) + codec
+resampling (p 0.3 x 0.5) + pad_random/tile to 64 600 + mixup, bf16-autocast forward of the full
+DualStreamSEMamba (random-init WavLM-Large + LoRA r8 q/v, SincNet, 4 Bi-Mamba layers), focal loss,
+backward, FGM attack (eps 0.5 on feature_projection) + adversarial forward/backward + restore; then
+all-reduce (RCCL, N > 1), clip 3.0, AdamW, EMA, LR schedule. An utterance counts once per step.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line. `roofline` is for the dominant hand-written HIP kernel of the step
+(largest total time), timed live with HIP events on its stream over the timed region;
+`cpu_baseline` times the oracle (CPU restatement, fp32) on a bounded sample on the host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "robust-audio-deepfake-evolution_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAKS = {"hbm": 8000.0, "fp32": 157.3}      # GB/s ; TFLOP/s  (MI355X_MICROARCH.md, dense, no sparsity)
+KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "selective_scan_fwd": ("hbm", None),
+                "selective_scan_bwd": ("hbm", None), "layer_wsum_fwd": ("hbm", None),
+                "layer_wsum_bwd": ("hbm", None), "rawboost_batch": ("hbm", None)}
+TRAIN_FLOP_PER_UTT = 0.72e12                # SURVEY.md §8d (algorithmic, FGM step)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--accum", type=int, default=4)
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--layerdrop", type=float, default=0.0,
+                    help="WavLM LayerDrop during the bench (0 = every layer runs; never less work)")
+    ap.add_argument("--pool", type=int, default=64, help="synthetic utterances resident in HBM per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-microsteps", type=int, default=1)
+    ap.add_argument("--config", default="Phase6_Proposed.conf")
+    return ap.parse_args()
+
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def synthetic_pool(n, length, seed, device):
+    """16 kHz utterances x = clip(0.1 N(0,1), -1, 1), labels Bernoulli(0.102)."""
+    rng = np.random.default_rng(seed)
+    x = np.clip(0.1 * rng.standard_normal((n, length)), -1, 1).astype(np.float32)
+    y = (rng.random(n) < 0.102).astype(np.int64)
+    return torch.from_numpy(x.reshape(-1)).to(device), torch.from_numpy(y)
+
+
+def build(config, device, layerdrop):
+    from radhip.build import apply_lora_to_wavlm, get_model
+    torch.manual_seed(1234)
+    model = get_model(config["model_config"], device)
+    model = apply_lora_to_wavlm(model, config["training_config"])
+    core = model.wavlm_stream._core()
+    core.config.layerdrop = layerdrop
+    return model
+
+
+def roofline_from_timing(timing):
+    rows = {}
+    for name, evs in timing.items():
+        ms = [s.elapsed_time(e) for s, e, _ in evs]
+        work = [w for _, _, w in evs]
+        rows[name] = {"launches": len(ms), "total_ms": float(sum(ms)), "avg_ms": float(np.mean(ms)),
+                      "avg_work": float(np.mean(work))}
+    if not rows:
+        return None, rows
+    dom = max(rows, key=lambda k: rows[k]["total_ms"])
+    r = rows[dom]
+    bound, kind = KERNEL_BOUND.get(dom, ("hbm", None))
+    if bound == "mfma":
+        achieved = r["avg_work"] / (r["avg_ms"] * 1e-3) / 1e12
+        peak, unit = PEAKS[kind], "TFLOP/s"
+    else:
+        achieved = r["avg_work"] / (r["avg_ms"] * 1e-3) / 1e9
+        peak, unit = PEAKS["hbm"], "GB/s"
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": dom,
+            "avg_launch_ms": round(r["avg_ms"], 5), "work_per_launch": r["avg_work"],
+            "work_unit": "FLOP" if bound == "mfma" else "bytes"}
+    return roof, rows
+
+
+def cpu_baseline(config, threads, microsteps):
+    """Oracle (CPU restatement, fp32) Phase-6 FGM micro-batch at B=2: RawBoost/codec (numpy), full
+    WavLM-Large (transformers, random init) + SincNet + sequential Bi-Mamba, focal loss, backward,
+    FGM attack + adversarial fwd/bwd + restore, AdamW step."""
+    from oracle import rawboost as orb
+    from oracle.data import pad_random
+    from oracle.model import OracleModel
+    from oracle.resample import codec_roundtrip
+    import random as pyrandom
+    from radhip.wavlm import WAVLM_LARGE
+    torch.set_num_threads(threads)
+    cfg = {k: v for k, v in WAVLM_LARGE.items()}
+    cfg["layerdrop"] = 0.0
+    cfg["conv_dim"] = tuple(cfg["conv_dim"])
+    torch.manual_seed(0)
+    m = OracleModel(cfg)
+    for n, p in m.named_parameters():
+        p.requires_grad_(not n.startswith("wavlm_stream.model.") or "feature_projection" in n)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.eval()
+    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5)
+    rng = np.random.default_rng(7)
+    B = 2
+    xs = [np.clip(0.1 * rng.standard_normal(64000), -1, 1) for _ in range(B)]
+    ys = torch.tensor([0, 1])
+
+    def focal(logits, y, a=0.9, g=2.5):
+        lp = torch.log_softmax(logits, 1).gather(1, y[:, None]).squeeze(1)
+        return (-torch.where(y == 0, 1 - a, a) * (1 - lp.exp()) ** g * lp).mean()
+
+    def one():
+        batch = []
+        for x in xs:
+            if pyrandom.random() < 0.8:
+                x = orb.process(x, [1, 2, 3, 4])
+            if pyrandom.random() < 0.3 and pyrandom.random() < 0.5:
+                x = codec_roundtrip(x, pyrandom.choice([8000, 6000, 4000]))
+            batch.append(pad_random(x))
+        xb = torch.tensor(np.stack(batch), dtype=torch.float32)
+        lam = float(np.random.beta(1, 1))
+        perm = torch.randperm(B)
+        xb = lam * xb + (1 - lam) * xb[perm]
+        _, out = m(xb)
+        loss = lam * focal(out, ys) + (1 - lam) * focal(out, ys[perm])
+        loss.backward()
+        fp = [p for n, p in m.named_parameters() if "feature_projection" in n]
+        bk = [p.data.clone() for p in fp]
+        with torch.no_grad():
+            for p in fp:
+                nrm = p.grad.norm()
+                if nrm != 0 and not torch.isnan(nrm):
+                    p.add_(0.5 * p.grad / nrm)
+        _, out = m(xb)
+        (lam * focal(out, ys) + (1 - lam) * focal(out, ys[perm])).backward()
+        with torch.no_grad():
+            for p, b in zip(fp, bk):
+                p.copy_(b)
+        torch.nn.utils.clip_grad_norm_([p for p in m.parameters() if p.requires_grad], 3.0)
+        opt.step()
+        opt.zero_grad()
+    t0 = time.perf_counter()
+    for _ in range(microsteps):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * microsteps / dt, 4), "unit": "utt/s", "cores": threads, "kind": "port",
+            "sample": f"{microsteps} Phase-6 FGM micro-batch(es) of B={B} (RawBoost/codec numpy, fwd+bwd x2, "
+                      f"AdamW) through the fp32 CPU oracle, {dt:.1f} s on {threads} threads"}
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_setup()
+    dev = torch.device("cuda", local)
+    from radhip import ops
+    from radhip.build import load_config
+    from radhip.train import Augmenter, Trainer, total_optimizer_steps
+    config = load_config(args.config)
+    tc = config["training_config"]
+    tc["accumulation_steps"] = args.accum
+    config["batch_size"] = args.micro_batch
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.amp]
+    model = build(config, dev, args.layerdrop)
+    total_steps = args.steps + args.warmup
+    trainer = Trainer(model, config, dev, total_optimizer_steps(1, total_steps * args.accum, args.accum), amp)
+    dc = config["data_config"]
+    aug = Augmenter(dev, algo=dc.get("rawboost_algo", 0), rawboost_p=dc.get("rawboost_p", 1.0),
+                    use_codec=dc.get("use_codec_aug", False), codec_p=dc.get("codec_p", 0.5))
+    L_RAW = 64000
+    pool_x, pool_y = synthetic_pool(args.pool, L_RAW, 1234 + rank, dev)
+    np.random.seed(1234 + rank)
+    import random as pyrandom
+    pyrandom.seed(1234 + rank)
+    B = args.micro_batch
+
+    def micro(i, last):
+        idx = np.random.randint(0, args.pool, size=B)
+        offs = [int(j) * L_RAW for j in idx]
+        lens = [L_RAW] * B
+        plan = aug.draw(lens)
+        lam, perm = trainer.mixup_draw(B)
+        x = aug.run(pool_x, offs, lens, plan, perm, lam)
+        trainer.micro_step(x, pool_y[idx], lam, perm, last_in_epoch=last)
+
+    def step():
+        for i in range(args.accum):
+            micro(i, i == args.accum - 1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.TIMING = {}
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    timing, ops.TIMING = ops.TIMING, None
+    t = torch.tensor([wall], device=dev, dtype=torch.float64)
+    if ws > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    loss = trainer.epoch_loss()
+    roof, rows = roofline_from_timing(timing)
+    utts = ws * args.steps * args.accum * B
+    value = utts / wall_max
+    if rank == 0:
+        line = {
+            "metric": "Phase-6 train throughput (utterances/sec), DualStreamSEMamba + LoRA + RawBoost/codec + FGM",
+            "value": round(value, 3), "unit": "utt/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000 * wall_max / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.amp, "data": "synthetic (16 kHz, 64000 samples, clip(0.1 N(0,1)))",
+            "config": {"workload": "Phase6_Proposed.conf train step on ASVspoof19-LA-shaped utterances",
+                       "model": "DualStreamSEMamba (WavLM-Large random init + LoRA r8 q/v, SincNet, 4x PN-BiMamba)",
+                       "micro_batch": B, "accumulation": args.accum, "global_batch": ws * B * args.accum,
+                       "seq_len": 64600, "parallelism": f"dp{ws}", "fgm": True, "mixup": True,
+                       "rawboost_algo": dc.get("rawboost_algo"), "codec_p": dc.get("codec_p"),
+                       "wavlm_layerdrop": args.layerdrop},
+            "roofline": roof,
+            "step_mfma_frac": round(value / ws * TRAIN_FLOP_PER_UTT / 2.5e15, 4),
+            "kernels": {k: {kk: round(vv, 5) if isinstance(vv, float) else vv for kk, vv in v.items()}
+                        for k, v in rows.items()},
+            "final_loss": round(loss, 6),
+        }
+        if ws == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 8)
+            line["cpu_baseline"] = cpu_baseline(config, threads, args.cpu_microsteps)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+"""CPU restatement of the reference Model (src/models/DualStreamSEMamba.py:49-769).
+
+WavLM stream = transformers' WavLMModel (the reference's own dependency, installed in the image)
+with the reference's softmax layer weighting; SincNet / fusion / Bi-Mamba / head restated with the
+sequential Mamba of oracle.mamba. State-dict keys equal the reference's (and the product's).
+Pinned by tests/golden/model_tiny.npz (reference forward + gradients on seeded weights).
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .mamba import PNBiMambaRef
+from .sinc import sinc_filterbank
+
+
+class OWavLM(nn.Module):
+    def __init__(self, cfg_dict):
+        super().__init__()
+        from transformers import WavLMConfig, WavLMModel
+        self.model = WavLMModel(WavLMConfig(**cfg_dict))
+        self.layer_weights = nn.Parameter(torch.zeros(self.model.config.num_hidden_layers + 1))
+
+    def forward(self, x):
+        hs = self.model(x, output_hidden_states=True).hidden_states
+        w = F.softmax(self.layer_weights, dim=0)
+        return (w.view(-1, 1, 1, 1) * torch.stack(hs)).sum(0)
+
+
+class OConv(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.band_pass = sinc_filterbank(70, 128, 16000)
+
+    def forward(self, x, mask=None):
+        w = self.band_pass.clone().to(x.dtype)
+        if mask is not None:
+            w[mask[0]:mask[1]] = 0
+        return F.conv1d(x, w.view(70, 1, 129))
+
+
+class ORes(nn.Module):
+    """Residual_block (:144-200) incl. the dead bn1/selu branch."""
+
+    def __init__(self, nb, first=False):
+        super().__init__()
+        self.first = first
+        if not first:
+            self.bn1 = nn.BatchNorm2d(nb[0])
+        self.conv1 = nn.Conv2d(nb[0], nb[1], (2, 3), padding=(1, 1))
+        self.selu = nn.SELU()
+        self.bn2 = nn.BatchNorm2d(nb[1])
+        self.conv2 = nn.Conv2d(nb[1], nb[1], (2, 3), padding=(0, 1))
+        self.downsample = nb[0] != nb[1]
+        if self.downsample:
+            self.conv_downsample = nn.Conv2d(nb[0], nb[1], (1, 3), padding=(0, 1))
+        self.mp = nn.MaxPool2d((1, 3))
+
+    def forward(self, x):
+        if not self.first:
+            self.selu(self.bn1(x))   # computed and discarded, as in the reference (:185-189)
+        out = self.conv2(self.selu(self.bn2(self.conv1(x))))
+        idn = self.conv_downsample(x) if self.downsample else x
+        return self.mp(out + idn)
+
+
+class OSinc(nn.Module):
+    def __init__(self):
+        super().__init__()
+        f = [70, [1, 32], [32, 32], [32, 64], [64, 64]]
+        self.conv_time = OConv()
+        self.first_bn = nn.BatchNorm2d(1)
+        self.selu = nn.SELU()
+        self.encoder = nn.Sequential(*[nn.Sequential(ORes(nb, first=(i == 0)))
+                                       for i, nb in enumerate([f[1], f[2], f[3], f[4], f[4], f[4]])])
+
+    def forward(self, x, mask=None):
+        x = self.conv_time(x.unsqueeze(1), mask).unsqueeze(1)
+        x = self.selu(self.first_bn(F.max_pool2d(torch.abs(x), (3, 3))))
+        e = self.encoder(x)
+        return torch.max(torch.abs(e), dim=2)[0].transpose(1, 2)
+
+
+class OSE(nn.Module):
+    def __init__(self, c, r):
+        super().__init__()
+        self.fc = nn.Sequential(nn.Linear(c, c // r, bias=False), nn.ReLU(), nn.Linear(c // r, c, bias=False),
+                                nn.Sigmoid())
+
+    def forward(self, x):
+        return x * self.fc(x.mean(1)).unsqueeze(1)
+
+
+class OFusion(nn.Module):
+    def __init__(self, wd, sd, od, red):
+        super().__init__()
+        self.ln_wavlm, self.ln_sinc = nn.LayerNorm(wd), nn.LayerNorm(sd)
+        self.wavlm_proj, self.sinc_proj = nn.Linear(wd, od), nn.Linear(sd, od)
+        self.fusion_proj = nn.Linear(2 * od, od)
+        self.se_layer = OSE(od, red)
+        self.norm = nn.LayerNorm(od)
+        self.dropout = nn.Dropout(0.1)
+
+    def forward(self, fw, fs):
+        fw = self.wavlm_proj(self.ln_wavlm(fw))
+        fs = self.sinc_proj(self.ln_sinc(fs))
+        T1, T2 = fw.shape[1], fs.shape[1]
+        if T1 != T2:
+            if T1 / T2 > 4.0:      # nearest: source index floor(i * T2 / T1)
+                idx = torch.floor(torch.arange(T1, dtype=torch.float64) * (T2 / T1)).long()
+                fs = fs[:, idx]
+            else:
+                fs = F.interpolate(fs.transpose(1, 2), size=T1, mode="linear", align_corners=False).transpose(1, 2)
+        f = self.se_layer(self.fusion_proj(torch.cat([fw, fs], -1)))
+        return self.dropout(self.norm(f))
+
+
+class OracleModel(nn.Module):
+    def __init__(self, wavlm_cfg, emb_size=144, num_encoders=4, d_state=16):
+        super().__init__()
+        self.wavlm_stream = OWavLM(wavlm_cfg)
+        self.sinc_stream = OSinc()
+        self.fusion = OFusion(1024, 64, emb_size, 16)
+        self.backbone_layers = nn.ModuleList([PNBiMambaRef(emb_size, d_state) for _ in range(num_encoders)])
+        self.norm_f = nn.LayerNorm(emb_size)
+        self.attention_pool = nn.Linear(emb_size, 1)
+        self.dropout = nn.Dropout(0.1)
+        self.classifier = nn.Linear(emb_size, 2)
+
+    def forward(self, x, mask=None):
+        f = self.fusion(self.wavlm_stream(x), self.sinc_stream(x, mask))
+        for layer in self.backbone_layers:
+            f = layer(f)
+        f = self.norm_f(f)
+        a = F.softmax(self.attention_pool(f), dim=1)
+        feats = self.dropout(torch.matmul(a.transpose(1, 2), f).squeeze(1))
+        return feats, self.classifier(feats)
+
+
+def tiny_wavlm_config(js):
+    import json
+    d = json.loads(str(js)) if not isinstance(js, dict) else dict(js)
+    d["conv_dim"] = tuple(d["conv_dim"])
+    return d
+
+
+def np_seed_everything(seed):
+    np.random.seed(seed)
+    torch.manual_seed(seed)

@@ -25,14 +25,14 @@ def sinc_filterbank(out_channels=70, kernel_size=128, sample_rate=16000):
     f = int(sample_rate / 2) * np.linspace(0, 1, int(512 / 2) + 1)
     fm = _mel(f)
     edges = _hz(np.linspace(np.min(fm), np.max(fm), out_channels + 1))
-    taps = torch.arange(-(K - 1) / 2, (K - 1) / 2 + 1)   # float32 tensor, as in the reference
-    bank = torch.zeros(out_channels, K)
-    win = torch.Tensor(np.hamming(K))
+    taps = torch.arange(-(K - 1) / 2, (K - 1) / 2 + 1, device="cpu")   # float32, as in the reference
+    bank = torch.zeros(out_channels, K, device="cpu")
+    win = torch.from_numpy(np.hamming(K)).float()
     for i in range(out_channels):
         lo, hi = edges[i], edges[i + 1]
         ideal = (2 * hi / sample_rate) * np.sinc(2 * hi * taps / sample_rate) - \
                 (2 * lo / sample_rate) * np.sinc(2 * lo * taps / sample_rate)
-        bank[i, :] = win * torch.Tensor(ideal)
+        bank[i, :] = win * torch.from_numpy(np.asarray(ideal)).float()
     return bank
 
 

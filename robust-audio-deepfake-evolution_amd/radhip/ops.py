@@ -12,6 +12,36 @@ from ._lib import check, lib, ptr_array
 
 _DT = {torch.float32: _lib.RDX_F32, torch.bfloat16: _lib.RDX_BF16}
 
+# Optional live timing: when TIMING is a dict, every C-ABI launch below is bracketed by two HIP events
+# recorded on the stream it is launched on; TIMING[name] collects (start, end, work) tuples, where
+# `work` is the launch's algorithmic bytes or FLOPs (bench.py turns these into the roofline line).
+TIMING = None
+
+
+class _timed:
+    __slots__ = ("name", "t", "work", "ev")
+
+    def __init__(self, name, t, work=0.0):
+        self.name, self.t, self.work = name, t, work
+
+    def __enter__(self):
+        if TIMING is not None:
+            s = torch.cuda.current_stream(self.t.device)
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record(s)
+        return self
+
+    def __exit__(self, *exc):
+        if TIMING is not None:
+            self.ev[1].record(torch.cuda.current_stream(self.t.device))
+            TIMING.setdefault(self.name, []).append((self.ev[0], self.ev[1], self.work))
+        return False
+
+
+def sinc_flops(B, C, K, L):
+    """Algorithmic FLOPs of one fused SincConv launch: 2*K MACs for every conv output the 3x3 pool reads."""
+    return 2.0 * K * B * (3 * (C // 3)) * (3 * ((L - K + 1) // 3))
+
 
 def _stream(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
@@ -47,8 +77,9 @@ def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0):
     B, L = x.shape
     C, K = filters.shape
     out = torch.empty(B, C // 3, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
-    check(lib().rdx_sincconv_absmaxpool_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi), _p(out),
-                                            _stream(x)), "sincconv_absmaxpool_fwd")
+    with _timed("sincconv_absmaxpool", x, sinc_flops(B, C, K, L)):
+        check(lib().rdx_sincconv_absmaxpool_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi),
+                                                _p(out), _stream(x)), "sincconv_absmaxpool_fwd")
     return out
 
 
@@ -116,9 +147,11 @@ class SelectiveScan(torch.autograd.Function):
         dt_bias = dt_bias.contiguous().float()
         y = torch.empty(dirs, B, L, D, device=u.device, dtype=torch.float32)
         ck = torch.empty(lib().rdx_scan_ckpt_elems(B, L, D, N, dirs), device=u.device, dtype=torch.float32)
-        check(lib().rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc, _p(Dp),
-                                           _p(dt_bias), _p(y), _p(ck), B, L, D, N, dirs, _stream(u)),
-              "selective_scan_fwd")
+        es = u.element_size()
+        with _timed("selective_scan_fwd", u, dirs * B * L * (D * (2 * es + 4) + 2 * N * es)):
+            check(lib().rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc,
+                                               _p(Dp), _p(dt_bias), _p(y), _p(ck), B, L, D, N, dirs, _stream(u)),
+                  "selective_scan_fwd")
         ctx.save_for_backward(u, delta, A_log, Bm, Cm, Dp, dt_bias, ck)
         ctx.ldbc = ldbc
         return y
@@ -141,10 +174,12 @@ class SelectiveScan(torch.autograd.Function):
         dA = torch.empty(dirs * B, D, N, device=u.device, dtype=torch.float32)
         dD = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
         dbias = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
-        check(lib().rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ctx.ldbc,
-                                           _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du), _p(ddelta),
-                                           _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs, _stream(u)),
-              "selective_scan_bwd")
+        es = u.element_size()
+        with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
+            check(lib().rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
+                                               ctx.ldbc, _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du),
+                                               _p(ddelta), _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs,
+                                               _stream(u)), "selective_scan_bwd")
         dBC = dBC.sum(0).to(Bm.dtype)
         return du, ddelta, dA.sum(0), dBC[..., :N], dBC[..., N:], dD.sum(0), dbias.sum(0)
 
@@ -190,8 +225,9 @@ class LayerWeightedSum(torch.autograd.Function):
         hs = tuple(h if (h.dtype == dt and h.is_contiguous()) else h.to(dt).contiguous() for h in hs)
         wf = w.detach().contiguous().float()
         out = torch.empty_like(hs[0])
-        check(lib().rdx_layer_wsum_fwd(_dtype_code(h0), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
-                                       _p(out), out.numel(), _stream(out)), "layer_wsum_fwd")
+        with _timed("layer_wsum_fwd", out, (len(hs) + 1) * out.numel() * out.element_size()):
+            check(lib().rdx_layer_wsum_fwd(_dtype_code(h0), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
+                                           _p(out), out.numel(), _stream(out)), "layer_wsum_fwd")
         ctx.save_for_backward(wf, *hs)
         return out
 
@@ -203,9 +239,10 @@ class LayerWeightedSum(torch.autograd.Function):
         n = g.numel()
         nblk = lib().rdx_layer_wsum_nblk(n)
         dots = torch.empty(nblk, len(hs), device=g.device, dtype=torch.float32)
-        check(lib().rdx_layer_wsum_bwd(_dtype_code(g), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf), _p(g),
-                                       ptr_array([d.data_ptr() for d in dhs]), _p(dots), n, _stream(g)),
-              "layer_wsum_bwd")
+        with _timed("layer_wsum_bwd", g, (2 * len(hs) + 1) * n * g.element_size()):
+            check(lib().rdx_layer_wsum_bwd(_dtype_code(g), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
+                                           _p(g), ptr_array([d.data_ptr() for d in dhs]), _p(dots), n, _stream(g)),
+                  "layer_wsum_bwd")
         dots = dots.sum(0)
         p = torch.softmax(wf, 0)
         dw = p * (dots - (p * dots).sum())
@@ -244,7 +281,9 @@ def rawboost_batch(x_flat, records, noise_isd=None, noise_ssi=None):
     ws = torch.empty(max(wsb, 8), device=x_flat.device, dtype=torch.uint8)
     ni = _p(noise_isd) if noise_isd is not None else None
     ns = _p(noise_ssi) if noise_ssi is not None else None
-    check(lib().rdx_rawboost_batch(_p(x_flat), _p(out), arr, n, _p(ws), ni, ns, _stream(x_flat)), "rawboost_batch")
+    with _timed("rawboost_batch", x_flat, 8.0 * total):
+        check(lib().rdx_rawboost_batch(_p(x_flat), _p(out), arr, n, _p(ws), ni, ns, _stream(x_flat)),
+              "rawboost_batch")
     return out
 
 

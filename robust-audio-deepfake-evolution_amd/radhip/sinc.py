@@ -1,0 +1,132 @@
+"""SincNet stream: SincConv front end on the HIP kernel + the residual 2-D encoder.
+
+Reference: CONV (src/models/DualStreamSEMamba.py:49-138), Residual_block (:144-200) and
+SincNetEncoder (:206-270), themselves taken from AASIST (models/AASIST.py:325-466).
+"""
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .ops import sincconv_absmaxpool
+
+
+def mel_edges(out_channels, sample_rate, nfft=512):
+    """Band edges equally spaced on the mel scale over 0..fs/2 (CONV.__init__ :95-101)."""
+    f = int(sample_rate / 2) * np.linspace(0, 1, int(nfft / 2) + 1)
+    mel = 2595 * np.log10(1 + f / 700)
+    m = np.linspace(np.min(mel), np.max(mel), out_channels + 1)
+    return 700 * (10 ** (m / 2595) - 1)
+
+
+def sinc_bank(out_channels=70, kernel_size=129, sample_rate=16000):
+    """[C, K] float32 Hamming-windowed band-pass bank. Follows the reference's numeric path exactly
+    (float32 tap grid, numpy sinc on it, float32 window x float32 ideal response; :104-117) so the
+    bank is bit-identical to the reference's `band_pass` (checked against tests/golden)."""
+    K = kernel_size
+    edges = mel_edges(out_channels, sample_rate)
+    n = torch.arange(-(K - 1) / 2, (K - 1) / 2 + 1, device="cpu")   # float32 grid, as the reference
+    win = torch.from_numpy(np.hamming(K)).float()
+    rows = []
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        h = (2 * hi / sample_rate) * np.sinc(2 * hi * n / sample_rate)
+        l = (2 * lo / sample_rate) * np.sinc(2 * lo * n / sample_rate)
+        rows.append(win * torch.from_numpy(np.asarray(h - l)).float())
+    return torch.stack(rows)
+
+
+class CONV(nn.Module):
+    """Drop-in of the reference CONV: fixed (non-learnable) sinc filter bank. `forward` keeps the
+    reference's API (x [B,1,T] -> [B,C,T-K+1]) for callers that need the raw conv; SincNetEncoder uses
+    `absmaxpool`, the fused HIP path that never materialises the [B, 70, 64472] conv output."""
+
+    def __init__(self, out_channels, kernel_size, sample_rate=16000, in_channels=1, stride=1, padding=0,
+                 dilation=1, bias=False, groups=1, mask=False):
+        super().__init__()
+        if in_channels != 1:
+            raise ValueError("SincConv only support one input channel (here, in_channels = {%i})" % in_channels)
+        if bias:
+            raise ValueError("SincConv does not support bias.")
+        if groups > 1:
+            raise ValueError("SincConv does not support groups.")
+        self.out_channels = out_channels
+        self.kernel_size = kernel_size + 1 if kernel_size % 2 == 0 else kernel_size
+        self.sample_rate = sample_rate
+        self.stride, self.padding, self.dilation, self.mask = stride, padding, dilation, mask
+        self.register_buffer("band_pass", sinc_bank(out_channels, self.kernel_size, sample_rate), persistent=False)
+
+    def draw_mask(self):
+        """Freq_aug: zero A = int(U(0,20)) consecutive filters at A0 = randint(0, C-A) (:121-125),
+        numpy then python RNG, exactly as the reference draws them."""
+        A = int(np.random.uniform(0, 20))
+        A0 = random.randint(0, self.out_channels - A)
+        return A0, A0 + A
+
+    def forward(self, x, mask=False):
+        w = self.band_pass.clone()
+        if mask:
+            lo, hi = self.draw_mask()
+            w[lo:hi] = 0
+        return torch.nn.functional.conv1d(x, w.view(self.out_channels, 1, self.kernel_size), stride=self.stride,
+                                          padding=self.padding, dilation=self.dilation)
+
+    def absmaxpool(self, x, mask=False):
+        """max_pool2d(|conv(x)|, (3,3)) on the HIP kernel: x [B, T] -> [B, C//3, (T-K+1)//3]."""
+        lo, hi = self.draw_mask() if mask else (0, 0)
+        return sincconv_absmaxpool(x, self.band_pass, lo, hi)
+
+
+class Residual_block(nn.Module):
+    """Same parameters and forward as the reference block. The reference computes bn1+selu and then
+    discards them (`out = self.conv1(x)`, :189); here only bn1's running-stat side effect is kept
+    (when bn1 is in training mode), without the dead activation."""
+
+    def __init__(self, nb_filts, first=False):
+        super().__init__()
+        self.first = first
+        if not self.first:
+            self.bn1 = nn.BatchNorm2d(num_features=nb_filts[0])
+        self.conv1 = nn.Conv2d(nb_filts[0], nb_filts[1], kernel_size=(2, 3), padding=(1, 1), stride=1)
+        self.selu = nn.SELU(inplace=True)
+        self.bn2 = nn.BatchNorm2d(num_features=nb_filts[1])
+        self.conv2 = nn.Conv2d(nb_filts[1], nb_filts[1], kernel_size=(2, 3), padding=(0, 1), stride=1)
+        self.downsample = nb_filts[0] != nb_filts[1]
+        if self.downsample:
+            self.conv_downsample = nn.Conv2d(nb_filts[0], nb_filts[1], padding=(0, 1), kernel_size=(1, 3), stride=1)
+        self.mp = nn.MaxPool2d((1, 3))
+
+    def forward(self, x):
+        if not self.first and self.bn1.training:
+            with torch.no_grad():
+                self.bn1(x)
+        out = self.conv1(x)
+        out = self.selu(self.bn2(out))
+        out = self.conv2(out)
+        identity = self.conv_downsample(x) if self.downsample else x
+        return self.mp(out + identity)
+
+
+class SincNetEncoder(nn.Module):
+    def __init__(self, sinc_channels=70, sinc_kernel=128):
+        super().__init__()
+        filts = [sinc_channels, [1, 32], [32, 32], [32, 64], [64, 64]]
+        self.conv_time = CONV(out_channels=filts[0], kernel_size=sinc_kernel, in_channels=1)
+        self.first_bn = nn.BatchNorm2d(num_features=1)
+        self.selu = nn.SELU(inplace=True)
+        self.encoder = nn.Sequential(
+            nn.Sequential(Residual_block(nb_filts=filts[1], first=True)),
+            nn.Sequential(Residual_block(nb_filts=filts[2])),
+            nn.Sequential(Residual_block(nb_filts=filts[3])),
+            nn.Sequential(Residual_block(nb_filts=filts[4])),
+            nn.Sequential(Residual_block(nb_filts=filts[4])),
+            nn.Sequential(Residual_block(nb_filts=filts[4])))
+        self.out_dim = filts[-1][-1]
+
+    def forward(self, x, freq_aug=False):
+        """x [B, T] -> e_T [B, T', 64] (SincNetEncoder.forward :238-270)."""
+        x = self.conv_time.absmaxpool(x.float(), mask=freq_aug).unsqueeze(1)    # [B, 1, 23, T/3]
+        x = self.selu(self.first_bn(x))
+        e = self.encoder(x)
+        e_T, _ = torch.max(torch.abs(e), dim=2)
+        return e_T.transpose(1, 2)

@@ -1,0 +1,433 @@
+"""Phase-6 training engine on MI355X: GPU augmentation, FGM, focal loss, EMA, DDP gradient reducer,
+and the micro-batch / optimizer-step loop.
+
+Reference semantics (src/main.py):
+  train_epoch :998-1126  mixup -> autocast fwd -> loss/accum -> bwd -> [FGM attack -> fwd -> bwd ->
+                         restore] -> every `accum` micro-batches: unscale, clip 3.0, step, zero_grad,
+                         EMA update, scheduler step
+  FGM :74-100, focal loss :297-305 (kornia), AdamW groups :416-457, schedule :460-483,
+  EMA :491-496, FGM group :514-544; per-utterance augmentation data_utils.py:163-184.
+Design differences (same math): augmentation runs batched on the GPU from utterances resident in
+HBM; the loss is accumulated on the device (no per-micro-batch .item() sync); gradients of all
+trainable tensors live in ONE flat fp32 buffer so a data-parallel step is one RCCL all-reduce.
+"""
+import math
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .ops import fgm_attack, pad_mixup, rawboost_batch, resample_batch, resample_kernel
+
+MAX_LEN = 64600
+CODEC_RATES = (8000, 6000, 4000)
+
+
+# ------------------------------------------------------------------------------- losses ------
+class FocalLoss(nn.Module):
+    """kornia.losses.FocalLoss(alpha, gamma, reduction='mean') for 2-class logits.
+
+    alpha_mode 'per_class' (kornia >= 0.7: weight [1-alpha, alpha, ...] by target class) or 'scalar'
+    (older kornia: alpha for every class). kornia is absent from the image and the reference pins no
+    version: parity unpinned; default per_class."""
+
+    def __init__(self, alpha=0.25, gamma=2.0, alpha_mode="per_class"):
+        super().__init__()
+        self.alpha, self.gamma, self.alpha_mode = alpha, gamma, alpha_mode
+
+    def forward(self, logits, target):
+        logp = F.log_softmax(logits.float(), dim=1)
+        lp = logp.gather(1, target[:, None]).squeeze(1)
+        w = torch.pow(1.0 - lp.exp(), self.gamma)
+        if self.alpha is None:
+            a = 1.0
+        elif self.alpha_mode == "per_class":
+            a = torch.where(target == 0, 1.0 - self.alpha, self.alpha).to(lp.dtype)
+        else:
+            a = self.alpha
+        return (-a * w * lp).mean()
+
+
+def build_criterion(config, device):
+    """Loss selection of main.py:270-312 (focal when loss == 'Focal' or use_focal_loss, else weighted CE)."""
+    tc = config.get("training_config", {})
+    if config.get("loss") == "Focal" or tc.get("use_focal_loss", False):
+        return FocalLoss(tc.get("focal_alpha", 0.25), tc.get("focal_gamma", 2.0),
+                         tc.get("focal_alpha_mode", "per_class"))
+    w = torch.tensor([0.1, 0.9], device=device)
+    return nn.CrossEntropyLoss(weight=w, label_smoothing=tc.get("label_smoothing", 0.0))
+
+
+# --------------------------------------------------------------------------------- FGM -------
+class FGM:
+    """FGM on parameters whose name contains `emb_name` (main.py:74-100), on the HIP kernel.
+    `grad_hook(list_of_grads) -> list_of_grads` lets DDP hand in the globally reduced gradient."""
+
+    def __init__(self, model, emb_name="feature_projection", epsilon=1.0, grad_hook=None):
+        self.model, self.emb_name, self.epsilon = model, emb_name, epsilon
+        self.grad_hook = grad_hook
+        self.backup = {}
+
+    def _targets(self):
+        return [(n, p) for n, p in self.model.named_parameters() if p.requires_grad and self.emb_name in n]
+
+    def attack(self):
+        tg = self._targets()
+        with_grad = [(n, p) for n, p in tg if p.grad is not None]
+        for n, p in tg:
+            if p.grad is None:
+                self.backup[n] = p.data.clone()
+        if not with_grad:
+            return
+        ps = [p.data for _, p in with_grad]
+        gs = [p.grad.contiguous() for _, p in with_grad]
+        if self.grad_hook is not None:
+            gs = self.grad_hook(gs)
+        bks = [torch.empty_like(p) for p in ps]
+        fgm_attack(ps, gs, bks, self.epsilon)
+        for (n, _), b in zip(with_grad, bks):
+            self.backup[n] = b
+
+    def restore(self):
+        for n, p in self.model.named_parameters():
+            if p.requires_grad and self.emb_name in n and n in self.backup:
+                p.data.copy_(self.backup[n])
+        self.backup = {}
+
+
+# --------------------------------------------------------------------------------- EMA -------
+class EMA:
+    """AveragedModel(model, multi_avg_fn=get_ema_multi_avg_fn(decay)) restricted to the tensors that
+    can change (lerp(a, a, w) == a, so frozen tensors are unaffected in the reference as well).
+    First update copies; buffers are not averaged (use_buffers=False)."""
+
+    def __init__(self, model, decay=0.999):
+        self.model, self.decay = model, decay
+        self.names = [n for n, p in model.named_parameters() if p.requires_grad]
+        self.shadow = None
+        self.n_averaged = 0
+
+    def refresh_names(self):
+        self.names = [n for n, p in self.model.named_parameters() if p.requires_grad]
+        self.shadow = None if self.n_averaged == 0 else self.shadow
+
+    @torch.no_grad()
+    def update(self):
+        params = dict(self.model.named_parameters())
+        cur = [params[n].detach() for n in self.names]
+        if self.shadow is None or self.n_averaged == 0:
+            self.shadow = [c.clone() for c in cur]
+        else:
+            torch._foreach_lerp_(self.shadow, cur, 1.0 - self.decay)
+        self.n_averaged += 1
+
+    @torch.no_grad()
+    def swap(self):
+        """Exchange live and EMA values (call twice to restore)."""
+        if self.shadow is None:
+            return
+        params = dict(self.model.named_parameters())
+        for n, s in zip(self.names, self.shadow):
+            tmp = params[n].data.clone()
+            params[n].data.copy_(s)
+            s.copy_(tmp)
+
+    def state_dict(self):
+        """Full model state dict with EMA values (the reference saves ema_model.state_dict())."""
+        sd = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+        if self.shadow is not None:
+            for n, s in zip(self.names, self.shadow):
+                sd[n] = s.detach().clone()
+        return sd
+
+
+# ---------------------------------------------------------------------- flat gradients -------
+class FlatGrads:
+    """Every trainable tensor's .grad is a view into one contiguous fp32 buffer: zero_grad is one
+    memset, clipping one norm, and a data-parallel step one all-reduce (11.9 MB for Phase 6)."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        total = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            assert p.dtype == torch.float32
+            p.grad = self.flat[off:off + n].view_as(p)
+            off += n
+
+    def zero(self):
+        self.flat.zero_()
+
+    def all_reduce_mean(self, group=None):
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            self.flat.div_(dist.get_world_size(group))
+
+
+def fgm_global_grads(grads):
+    """DDP: FGM direction from the globally accumulated gradient (sum over ranks; the direction is
+    scale-invariant). One small all-reduce of the feature_projection grads per attack."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return grads
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat)
+    out, off = [], 0
+    for g in grads:
+        out.append(flat[off:off + g.numel()].view_as(g))
+        off += g.numel()
+    return out
+
+
+# ------------------------------------------------------------------------- augmentation -------
+class Augmenter:
+    """Per-utterance RawBoost + codec decisions drawn on the host in the reference's order
+    (Dataset_ASVspoof2019_train.__getitem__, data_utils.py:163-184), executed as one batched kernel
+    per stage on the GPU, then pad_random/tile + mixup gather into the [B, 64600] model input."""
+
+    def __init__(self, device, algo=0, rawboost_p=1.0, use_codec=False, codec_p=0.5, max_len=MAX_LEN):
+        self.device = torch.device(device)
+        self.algo, self.rawboost_p = int(algo), float(rawboost_p)
+        self.use_codec, self.codec_p = bool(use_codec), float(codec_p)
+        self.max_len = max_len
+        self.algo_ids = [1, 2, 3, 4] if self.algo == 5 else [self.algo]
+        kerns, self.kinfo, off = [], {}, 0
+        for sr in CODEC_RATES:
+            for a, b in ((16000, sr), (sr, 16000)):
+                k, w, og, ng = resample_kernel(a, b)
+                self.kinfo[(a, b)] = (off, w, og, ng)
+                kerns.append(k.reshape(-1))
+                off += k.numel()
+        self.kernels = torch.cat(kerns).to(self.device)
+
+    # --- host draws (mirror rawboost.py / data_utils.py draw order; per-sample noise -> Philox seed)
+    def _draw_rawboost(self, n):
+        r = _lib.RawboostUtt()
+        r.len = n
+        algo = self.algo_ids[np.random.randint(0, len(self.algo_ids))]
+        r.algo = algo
+        if algo in (1, 4):
+            n_a = [1, 2, 3, 4, 5][np.random.randint(0, 5)]
+            np.random.randint(0, 90)                          # the unused `a` draw (rawboost.py:40)
+            b = np.array([1.0])
+            for _ in range(5):
+                b = np.convolve(b, [1.0, np.random.uniform(-1, 1)])
+            a = np.array([1.0])
+            for _ in range(n_a):
+                a = np.convolve(a, [1.0, np.random.uniform(-0.1, 0.1)])
+            r.n_a = n_a
+            r.b[:] = list(b)
+            aa = np.zeros(6)
+            aa[:len(a)] = a
+            r.a[:] = list(aa)
+            r.f = float(np.random.randn())
+        if algo in (2, 4):
+            r.beta = float(list(range(5, 10))[np.random.randint(0, 5)])
+        if algo == 3:
+            r.snr_db = float(np.random.uniform(10, 40))
+        if algo in (2, 3, 4):
+            r.seed = int(np.random.randint(0, 2 ** 62, dtype=np.int64))
+        return r
+
+    def codec_len(self, n, sr):
+        _, _, ogd, ngd = self.kinfo[(16000, sr)]
+        _, _, ogu, ngu = self.kinfo[(sr, 16000)]
+        nd = -(-ngd * n // ogd)
+        return -(-ngu * nd // ogu)
+
+    def draw(self, lens):
+        """Host decisions for a batch, per utterance in the reference's order: RawBoost gate + draws,
+        codec gates + rate, then the pad_random crop start (on the post-codec length)."""
+        plan = []
+        for n in lens:
+            rec = None
+            if self.algo != 0 and random.random() < self.rawboost_p:
+                rec = self._draw_rawboost(n)
+            sr = None
+            if self.use_codec and random.random() < self.codec_p:
+                if random.random() < 0.5:                       # apply_codec_aug's inner gate (:35)
+                    sr = random.choice(list(CODEC_RATES))
+            m = self.codec_len(n, sr) if sr is not None else n
+            # pad_random: crop at randint(len - max_len) (a length of exactly max_len, which makes the
+            # reference's randint(0) raise, is taken whole)
+            start = int(np.random.randint(m - self.max_len)) if m > self.max_len else 0
+            plan.append((rec, sr, start))
+        return plan
+
+    def run(self, raw, offsets, lens, plan, perm=None, lam=1.0):
+        """raw: flat fp32 device buffer; returns x [B, max_len]."""
+        B = len(lens)
+        total = int(sum(lens))
+        work = raw
+        offs = list(offsets)
+        cur_lens = list(lens)
+        recs = []
+        for b, (rec, _, _) in enumerate(plan):
+            r = rec if rec is not None else _lib.RawboostUtt()
+            r.offset, r.len = int(offsets[b]), int(lens[b])
+            if rec is None:
+                r.algo = 0
+            recs.append(r)
+        if any(r.algo != 0 for r in recs):
+            work = rawboost_batch(raw, recs)
+        codec = [(b, sr) for b, (_, sr, _) in enumerate(plan) if sr is not None]
+        if codec:
+            jobs_d, jobs_u, mid_off, out_off = [], [], 0, 0
+            outs = []
+            for b, sr in codec:
+                kd, wd, ogd, ngd = self.kinfo[(16000, sr)]
+                ku, wu, ogu, ngu = self.kinfo[(sr, 16000)]
+                n = cur_lens[b]
+                nd = -(-ngd * n // ogd)
+                nu = -(-ngu * nd // ogu)
+                jobs_d.append(_lib.ResampleJob(int(offs[b]), n, mid_off, nd, ogd, ngd, wd, kd))
+                jobs_u.append(_lib.ResampleJob(mid_off, nd, total + out_off, nu, ogu, ngu, wu, ku))
+                outs.append((b, total + out_off, nu))
+                mid_off += nd
+                out_off += nu
+            mid = torch.empty(mid_off, device=self.device)
+            ext = torch.empty(total + out_off, device=self.device)
+            ext[:total].copy_(work[:total])
+            for i in range(0, len(jobs_d), 64):
+                resample_batch(work, mid, self.kernels, jobs_d[i:i + 64])
+            for i in range(0, len(jobs_u), 64):
+                resample_batch(mid, ext, self.kernels, jobs_u[i:i + 64])
+            work = ext
+            for b, o, nu in outs:
+                offs[b], cur_lens[b] = o, nu
+        starts = [st for (_, _, st) in plan]
+        return pad_mixup(work, offs, cur_lens, starts, self.max_len, perm, lam)
+
+
+# --------------------------------------------------------------------------- trainer ---------
+class Trainer:
+    """One Phase-6 training process (one GPU). Mirrors main.py's optimizer/scheduler construction and
+    train_epoch ordering."""
+
+    def __init__(self, model, config, device, total_steps, amp_dtype=torch.bfloat16, world_group=None,
+                 criterion=None, param_groups=None):
+        self.model, self.config, self.device = model, config, torch.device(device)
+        tc = config.get("training_config", {})
+        oc = config["optim_config"]
+        self.accum = max(1, int(tc.get("accumulation_steps", 1)))
+        self.use_mixup = bool(tc.get("use_mixup", False))
+        self.mixup_alpha = float(tc.get("mixup_alpha", 1.0))
+        self.freq_aug = str(config.get("freq_aug", "False")).lower() in ("true", "1", "yes", "y", "t", "on")
+        self.freeze_bn = bool(tc.get("freeze_bn", False))
+        self.amp_dtype = amp_dtype
+        self.criterion = criterion if criterion is not None else build_criterion(config, device)
+        self.group = world_group
+        # --- parameter groups (main.py:416-457): wavlm_stream* at wavlm_lr, the rest at base_lr
+        wl, bb = [], []
+        for n, p in model.named_parameters():
+            if p.requires_grad:
+                (wl if "wavlm_stream" in n else bb).append(p)
+        wavlm_lr = oc.get("wavlm_lr", 1e-6)
+        groups = [{"params": wl, "lr": wavlm_lr}, {"params": bb, "lr": oc["base_lr"]},
+                  {"params": [], "lr": oc["base_lr"]}]
+        if param_groups is not None:
+            groups = param_groups
+        try:
+            self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"], fused=True)
+        except (RuntimeError, TypeError):
+            self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"])
+        warm = int(tc.get("warmup_steps", max(1, int(total_steps * float(tc.get("warmup_ratio", 0.05))))))
+        warm = min(max(1, warm), max(1, total_steps - 1))
+        eta_min = oc.get("scheduler_config", {}).get("eta_min", 1e-6)
+        w_sched = torch.optim.lr_scheduler.LinearLR(self.opt, start_factor=float(tc.get("warmup_init_factor", 0.1)),
+                                                    end_factor=1.0, total_iters=warm)
+        c_sched = torch.optim.lr_scheduler.CosineAnnealingLR(self.opt, T_max=max(1, total_steps - warm),
+                                                             eta_min=eta_min)
+        self.sched = torch.optim.lr_scheduler.SequentialLR(self.opt, [w_sched, c_sched], milestones=[warm])
+        self.sched_on = oc.get("scheduler", "cosine") in ("cosine", "keras_decay")
+        self.scaler = torch.amp.GradScaler("cuda", enabled=(amp_dtype == torch.float16))
+        self.ema = EMA(model, tc.get("ema_decay", 0.999)) if tc.get("use_ema", False) else None
+        # --- FGM (main.py:514-544): unfreeze feature_projection, add it as its own group at wavlm_lr
+        self.fgm = None
+        if tc.get("use_fgm", False):
+            emb = tc.get("fgm_emb_name", "feature_projection")
+            if "feature_projection" in emb and hasattr(model, "wavlm_stream"):
+                fp = model.wavlm_stream._core().feature_projection
+                fp.requires_grad_(True)
+                in_opt = any(p is fp.projection.weight for g in self.opt.param_groups for p in g["params"])
+                if not in_opt:
+                    self.opt.add_param_group({"params": list(fp.parameters()), "lr": wavlm_lr})
+            self.fgm = FGM(model, emb, tc.get("fgm_epsilon", 1.0), grad_hook=fgm_global_grads)
+            if self.ema is not None:
+                self.ema.refresh_names()
+        self.grads = FlatGrads(model.parameters())
+        self.params = self.grads.params
+        self.micro = 0
+        self.loss_sum = torch.zeros((), device=self.device, dtype=torch.float64)
+        self.n_seen = 0
+
+    def _loss(self, out, ya, yb, lam):
+        if ya is yb or lam == 1.0:
+            return self.criterion(out, ya)
+        return lam * self.criterion(out, ya) + (1 - lam) * self.criterion(out, yb)
+
+    def _fwd_loss(self, x, ya, yb, lam):
+        with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype != torch.float32):
+            _, out = self.model(x, Freq_aug=self.freq_aug)
+            return self._loss(out, ya, yb, lam) / self.accum
+
+    def mixup_draw(self, B):
+        """lam ~ Beta(alpha, alpha) (numpy), perm = torch.randperm(B) (CPU generator) — main.py:1038-1046."""
+        if self.use_mixup and B > 1:
+            lam = float(np.random.beta(self.mixup_alpha, self.mixup_alpha))
+            perm = torch.randperm(B).tolist()
+            return lam, perm
+        return 1.0, None
+
+    def micro_step(self, x, y, lam=1.0, perm=None, last_in_epoch=False):
+        """One micro-batch: x [B, 64600] already mixed (perm/lam are those used for the mix)."""
+        self.model.train()
+        if self.freeze_bn:
+            for m in self.model.modules():
+                if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
+                    m.eval()
+        y = y.view(-1).long().to(self.device, non_blocking=True)
+        ya = y
+        yb = y[torch.tensor(perm, device=self.device)] if perm is not None else y
+        loss = self._fwd_loss(x, ya, yb, lam)
+        self.scaler.scale(loss).backward()
+        if self.fgm is not None:
+            self.fgm.attack()
+            adv = self._fwd_loss(x, ya, yb, lam)
+            self.scaler.scale(adv).backward()
+            self.fgm.restore()
+        self.micro += 1
+        B = x.shape[0]
+        self.loss_sum += loss.detach().double() * self.accum * B
+        self.n_seen += B
+        if self.micro % self.accum == 0 or last_in_epoch:
+            self.optimizer_step()
+        return loss
+
+    def optimizer_step(self):
+        self.grads.all_reduce_mean(self.group)
+        self.scaler.unscale_(self.opt)
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=3.0, foreach=True)
+        self.scaler.step(self.opt)
+        self.scaler.update()
+        self.grads.zero()
+        if self.ema is not None:
+            self.ema.update()
+        if self.sched_on:
+            self.sched.step()
+
+    def epoch_loss(self):
+        v = float(self.loss_sum.item()) / max(self.n_seen, 1)
+        self.loss_sum.zero_()
+        self.n_seen = 0
+        return v
+
+
+def total_optimizer_steps(num_epochs, micro_batches_per_epoch, accum):
+    return num_epochs * math.ceil(micro_batches_per_epoch / accum)

@@ -126,7 +126,7 @@ def test_layer_weighted_sum(dtype):
     ref = (F.softmax(w, 0).view(-1, 1, 1, 1) * torch.stack([h.float() for h in hs])).sum(0)
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
-    g = torch.randn_like(ref)
+    g = torch.randn_like(ref).to(dtype).float()   # the incoming gradient has the states' dtype
     gh = torch.autograd.grad((out.float() * g).sum(), [w] + hs)
     gr = torch.autograd.grad((ref * g).sum(), [w] + hs)
     torch.testing.assert_close(gh[0], gr[0], rtol=1e-3 if dtype == torch.float32 else 5e-2, atol=1e-3)

@@ -1,0 +1,139 @@
+"""Product model / training engine on the GPU against the reference's golden vectors and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from seeded import seeded_fill_
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tiny_product(golden, num_encoders=2):
+    import json
+    import models.DualStreamSEMamba as DS
+    g = golden("model_tiny.npz")
+    cfg = json.loads(str(g["wavlm_config"]))
+
+    class Args:
+        emb_size, d_state, sinc_channels, wavlm_freeze_layers = 144, 16, 70, -1
+    Args.num_encoders = num_encoders
+    Args.wavlm_config = cfg
+    torch.manual_seed(0)
+    m = DS.Model(Args(), device=DEV)
+    seeded_fill_(m, seed=41)
+    return m.to(DEV), g
+
+
+def test_product_model_matches_reference_golden(golden):
+    m, g = _tiny_product(golden)
+    m.eval()
+    x = torch.from_numpy(g["x"]).to(DEV)
+    feats, logits = m(x, Freq_aug=False)
+    np.testing.assert_allclose(logits.detach().cpu().numpy(), g["logits"], rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(feats.detach().cpu().numpy(), g["feats"], rtol=1e-3, atol=1e-3)
+    (logits[:, 1].sum() - logits[:, 0].sum()).backward()
+    n = 0
+    for k, p in m.named_parameters():
+        if f"grad:{k}" in g and p.grad is not None:
+            np.testing.assert_allclose(p.grad.cpu().numpy(), g[f"grad:{k}"], rtol=5e-3, atol=1e-4, err_msg=k)
+            n += 1
+        elif f"gradsum:{k}" in g and p.grad is not None:
+            gg = p.grad.cpu().numpy().astype(np.float64)
+            np.testing.assert_allclose([gg.sum(), (gg * gg).sum()], g[f"gradsum:{k}"], rtol=2e-2, atol=1e-6,
+                                       err_msg=k)
+            n += 1
+    assert n >= 7
+
+
+def test_product_model_vs_oracle_full_length(golden):
+    """Full 64 600-sample utterances, full WavLM depth (reduced widths), 4 Bi-Mamba layers: logits
+    within 1e-3 of the fp64 CPU oracle (north-star tolerance)."""
+    from oracle.model import OracleModel, tiny_wavlm_config
+    m, g = _tiny_product(golden, num_encoders=4)
+    m.eval()
+    o = OracleModel(tiny_wavlm_config(g["wavlm_config"]), emb_size=144, num_encoders=4)
+    o.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=True)
+    o = o.double().eval()
+    rng = np.random.default_rng(3)
+    x = np.clip(0.1 * rng.standard_normal((2, 64600)), -1, 1).astype(np.float32)
+    with torch.no_grad():
+        _, lh = m(torch.from_numpy(x).to(DEV))
+        _, lo = o(torch.from_numpy(x).double())
+    np.testing.assert_allclose(lh.cpu().numpy(), lo.numpy(), rtol=0, atol=1e-3)
+
+
+def test_phase6_train_micro_step_bf16(golden):
+    """One Phase-6 micro-batch (GPU aug, mixup, bf16 fwd/bwd, FGM) + optimizer step on the tiny model."""
+    from radhip.build import apply_lora_to_wavlm, load_config
+    from radhip.train import Augmenter, Trainer
+    m, _ = _tiny_product(golden)
+    cfg = load_config("Phase6_Proposed.conf")
+    cfg["training_config"]["accumulation_steps"] = 1
+    m = apply_lora_to_wavlm(m, cfg["training_config"])
+    before = {n: p.detach().clone() for n, p in m.named_parameters() if p.requires_grad}
+    tr = Trainer(m, cfg, DEV, total_steps=10)
+    assert tr.fgm is not None and tr.ema is not None
+    aug = Augmenter(DEV, algo=5, rawboost_p=0.8, use_codec=True, codec_p=1.0)
+    rng = np.random.default_rng(0)
+    raw = torch.from_numpy(np.clip(0.1 * rng.standard_normal(4 * 64000), -1, 1).astype(np.float32)).to(DEV)
+    np.random.seed(0)
+    plan = aug.draw([64000] * 4)
+    lam, perm = tr.mixup_draw(4)
+    x = aug.run(raw, [0, 64000, 128000, 192000], [64000] * 4, plan, perm, lam)
+    assert x.shape == (4, 64600) and torch.isfinite(x).all()
+    tr.micro_step(x, torch.tensor([0, 1, 0, 0]), lam, perm, last_in_epoch=True)
+    torch.cuda.synchronize()
+    assert np.isfinite(tr.epoch_loss())
+    changed = [n for n, p in m.named_parameters() if n in before and not torch.equal(p, before[n])]
+    assert any("lora_A" in n for n in changed) and any("backbone_layers" in n for n in changed)
+    assert any("feature_projection" in n for n, p in m.named_parameters() if p.requires_grad)
+
+
+def test_train_trajectory_matches_reference_driver(golden):
+    """Toy model through the product Trainer == the reference train_epoch (mixup, accumulation, FGM on
+    the accumulated grad, clip, AdamW, EMA, warmup+cosine) on identical RNG streams."""
+    from radhip.train import Trainer
+    g = golden("train_toy.npz")
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.feature_projection = torch.nn.Linear(6, 5)
+            self.body = torch.nn.Linear(5, 4)
+            self.classifier = torch.nn.Linear(4, 2)
+
+        def forward(self, x, Freq_aug=False):
+            h = torch.tanh(self.body(torch.tanh(self.feature_projection(x))))
+            return h, self.classifier(h)
+
+    toy = Toy()
+    for k, p in toy.named_parameters():
+        p.data.copy_(torch.from_numpy(g[f"train_init:{k}"]))
+    toy = toy.to(DEV)
+    cfg = {"loss": "CE", "freq_aug": "False",
+           "optim_config": {"base_lr": 5e-3, "wavlm_lr": 1e-2, "weight_decay": 1e-4, "scheduler": "cosine",
+                            "scheduler_config": {"eta_min": 1e-6}},
+           "training_config": {"use_mixup": True, "mixup_alpha": 1.0, "accumulation_steps": 2, "use_ema": True,
+                               "ema_decay": 0.999, "use_fgm": True, "fgm_epsilon": 0.5, "warmup_steps": 1,
+                               "warmup_init_factor": 0.1, "freeze_bn": True}}
+    groups = [{"params": [toy.feature_projection.weight, toy.feature_projection.bias], "lr": 1e-2},
+              {"params": list(toy.body.parameters()) + list(toy.classifier.parameters()), "lr": 5e-3}]
+    tr = Trainer(toy, cfg, DEV, total_steps=3, amp_dtype=torch.float32, param_groups=groups)
+    np.random.seed(61)
+    torch.manual_seed(61)
+    xs, ys = g["train_x"], g["train_y"]
+    for i in range(xs.shape[0]):
+        x = torch.from_numpy(xs[i]).to(DEV)
+        lam, perm = tr.mixup_draw(x.shape[0])
+        xm = lam * x + (1 - lam) * x[torch.tensor(perm, device=DEV)]
+        tr.micro_step(xm, torch.from_numpy(ys[i]), lam, perm, last_in_epoch=(i == xs.shape[0] - 1))
+    assert tr.epoch_loss() == pytest.approx(float(g["train_loss"]), rel=1e-5)
+    np.testing.assert_allclose([pg["lr"] for pg in tr.opt.param_groups], g["train_lr_final"], rtol=1e-6)
+    for k, p in toy.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), g[f"train_final:{k}"], rtol=1e-5, atol=1e-6,
+                                   err_msg=k)
+    tr.ema.swap()
+    for k, p in toy.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), g[f"train_ema:{k}"], rtol=1e-5, atol=1e-6,
+                                   err_msg=k)
