@@ -275,6 +275,13 @@ def rawboost_batch(x_flat, records, noise_isd=None, noise_ssi=None):
     x_flat = x_flat.contiguous().float()
     out = torch.empty_like(x_flat)
     n = len(records)
+    for r in records:
+        if r.offset < 0 or r.len <= 0 or r.offset + r.len > x_flat.numel():
+            raise ValueError(f"rawboost record [{r.offset}, +{r.len}) outside the {x_flat.numel()}-sample buffer")
+        if noise_isd is not None and r.offset + r.len > noise_isd.numel():
+            raise ValueError("noise_isd shorter than the records")
+        if noise_ssi is not None and r.offset + r.len > noise_ssi.numel():
+            raise ValueError("noise_ssi shorter than the records")
     arr = (_lib.RawboostUtt * n)(*records)
     total = int(sum(r.len for r in records))
     wsb = lib().rdx_rawboost_workspace_bytes(n, max(total, 1))
@@ -304,6 +311,12 @@ def resample_kernel(orig_freq, new_freq, lowpass_width=6, rolloff=0.99):
 
 def resample_batch(x_flat, out_flat, kernels_dev, jobs):
     _require_gpu(x_flat, out_flat, kernels_dev)
+    for j in jobs:
+        kw = 2 * j.width + j.orig_g
+        if (j.in_offset < 0 or j.in_offset + j.in_len > x_flat.numel() or j.out_offset < 0
+                or j.out_offset + j.out_len > out_flat.numel() or j.kern_offset + j.new_g * kw > kernels_dev.numel()
+                or j.out_len > -(-j.new_g * j.in_len // j.orig_g)):
+            raise ValueError("resample job outside its buffers")
     arr = (_lib.ResampleJob * len(jobs))(*jobs)
     check(lib().rdx_resample_batch(_p(x_flat), _p(out_flat), _p(kernels_dev), arr, len(jobs), _stream(x_flat)),
           "resample_batch")
@@ -313,6 +326,13 @@ def pad_mixup(sig_flat, offsets, lens, starts, max_len, perm=None, lam=1.0):
     """[nutt, max_len] batch: crop (len >= max_len, at starts[b]) or tile, then mixup with perm."""
     _require_gpu(sig_flat)
     n = len(offsets)
+    for o, L, st in zip(offsets, lens, starts):
+        if o < 0 or L <= 0 or o + L > sig_flat.numel():
+            raise ValueError(f"pad_mixup: utterance [{o}, +{L}) outside the {sig_flat.numel()}-sample buffer")
+        if L >= max_len and (st < 0 or st + max_len > L):
+            raise ValueError("pad_mixup: crop start outside the utterance")
+    if perm is not None and sorted(perm) != list(range(n)):
+        raise ValueError("pad_mixup: perm is not a permutation")
     out = torch.empty(n, max_len, device=sig_flat.device, dtype=torch.float32)
     I64 = ctypes.c_int64 * n
     pa = (ctypes.c_int * n)(*perm) if perm is not None else None

@@ -261,21 +261,27 @@ class Augmenter:
         return plan
 
     def run(self, raw, offsets, lens, plan, perm=None, lam=1.0):
-        """raw: flat fp32 device buffer; returns x [B, max_len]."""
+        """raw: flat fp32 device buffer holding the utterances at `offsets`; returns x [B, max_len].
+        The batch is first packed contiguously (one gather launch), so every later stage addresses a
+        compact [sum(lens)] buffer whatever the layout of the resident corpus."""
         B = len(lens)
         total = int(sum(lens))
-        work = raw
-        offs = list(offsets)
+        work = torch.cat([raw[int(o):int(o) + int(n)] for o, n in zip(offsets, lens)])
+        offs, acc = [], 0
+        for n in lens:
+            offs.append(acc)
+            acc += int(n)
         cur_lens = list(lens)
+        packed = work
         recs = []
         for b, (rec, _, _) in enumerate(plan):
             r = rec if rec is not None else _lib.RawboostUtt()
-            r.offset, r.len = int(offsets[b]), int(lens[b])
+            r.offset, r.len = int(offs[b]), int(lens[b])
             if rec is None:
                 r.algo = 0
             recs.append(r)
         if any(r.algo != 0 for r in recs):
-            work = rawboost_batch(raw, recs)
+            work = rawboost_batch(packed, recs)
         codec = [(b, sr) for b, (_, sr, _) in enumerate(plan) if sr is not None]
         if codec:
             jobs_d, jobs_u, mid_off, out_off = [], [], 0, 0
@@ -337,6 +343,21 @@ class Trainer:
             self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"], fused=True)
         except (RuntimeError, TypeError):
             self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"])
+        # --- FGM (main.py:514-544): unfreeze feature_projection, add it as its own group at wavlm_lr.
+        # The reference adds this group AFTER building its LR schedulers; on torch >= 2.x that makes
+        # SequentialLR's milestone step fail (strict zip over param groups), and on older torch the
+        # group silently escaped the warmup. Here the group is added first, so it follows the same
+        # warmup + cosine schedule as the other groups.
+        self.fgm = None
+        if tc.get("use_fgm", False):
+            emb = tc.get("fgm_emb_name", "feature_projection")
+            if "feature_projection" in emb and hasattr(model, "wavlm_stream"):
+                fp = model.wavlm_stream._core().feature_projection
+                fp.requires_grad_(True)
+                in_opt = any(p is fp.projection.weight for g in self.opt.param_groups for p in g["params"])
+                if not in_opt:
+                    self.opt.add_param_group({"params": list(fp.parameters()), "lr": wavlm_lr})
+            self.fgm = FGM(model, emb, tc.get("fgm_epsilon", 1.0), grad_hook=fgm_global_grads)
         warm = int(tc.get("warmup_steps", max(1, int(total_steps * float(tc.get("warmup_ratio", 0.05))))))
         warm = min(max(1, warm), max(1, total_steps - 1))
         eta_min = oc.get("scheduler_config", {}).get("eta_min", 1e-6)
@@ -348,19 +369,6 @@ class Trainer:
         self.sched_on = oc.get("scheduler", "cosine") in ("cosine", "keras_decay")
         self.scaler = torch.amp.GradScaler("cuda", enabled=(amp_dtype == torch.float16))
         self.ema = EMA(model, tc.get("ema_decay", 0.999)) if tc.get("use_ema", False) else None
-        # --- FGM (main.py:514-544): unfreeze feature_projection, add it as its own group at wavlm_lr
-        self.fgm = None
-        if tc.get("use_fgm", False):
-            emb = tc.get("fgm_emb_name", "feature_projection")
-            if "feature_projection" in emb and hasattr(model, "wavlm_stream"):
-                fp = model.wavlm_stream._core().feature_projection
-                fp.requires_grad_(True)
-                in_opt = any(p is fp.projection.weight for g in self.opt.param_groups for p in g["params"])
-                if not in_opt:
-                    self.opt.add_param_group({"params": list(fp.parameters()), "lr": wavlm_lr})
-            self.fgm = FGM(model, emb, tc.get("fgm_epsilon", 1.0), grad_hook=fgm_global_grads)
-            if self.ema is not None:
-                self.ema.refresh_names()
         self.grads = FlatGrads(model.parameters())
         self.params = self.grads.params
         self.micro = 0
