@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-microsteps", type=int, default=1)
     ap.add_argument("--config", default="Phase6_Proposed.conf")
+    ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the micro-step")
     return ap.parse_args()
 
 
@@ -197,7 +198,7 @@ def main():
     dev = torch.device("cuda", local)
     from radhip import ops
     from radhip.build import load_config
-    from radhip.train import Augmenter, Trainer, total_optimizer_steps
+    from radhip.train import Augmenter, GraphedMicroStep, Trainer, total_optimizer_steps
     config = load_config(args.config)
     tc = config["training_config"]
     tc["accumulation_steps"] = args.accum
@@ -215,6 +216,10 @@ def main():
     import random as pyrandom
     pyrandom.seed(1234 + rank)
     B = args.micro_batch
+    graph = None
+    if not args.eager:
+        graph = GraphedMicroStep(trainer, B)
+        graph.capture()
 
     def micro(i, last):
         idx = np.random.randint(0, args.pool, size=B)
@@ -222,8 +227,12 @@ def main():
         lens = [L_RAW] * B
         plan = aug.draw(lens)
         lam, perm = trainer.mixup_draw(B)
-        x = aug.run(pool_x, offs, lens, plan, perm, lam)
-        trainer.micro_step(x, pool_y[idx], lam, perm, last_in_epoch=last)
+        if graph is not None:
+            aug.run(pool_x, offs, lens, plan, perm, lam, out=graph.x)
+            graph.run(pool_y[idx].numpy(), lam, perm, last_in_epoch=last)
+        else:
+            x = aug.run(pool_x, offs, lens, plan, perm, lam)
+            trainer.micro_step(x, pool_y[idx], lam, perm, last_in_epoch=last)
 
     def step():
         for i in range(args.accum):
@@ -268,7 +277,7 @@ def main():
                        "micro_batch": B, "accumulation": args.accum, "global_batch": ws * B * args.accum,
                        "seq_len": 64600, "parallelism": f"dp{ws}", "fgm": True, "mixup": True,
                        "rawboost_algo": dc.get("rawboost_algo"), "codec_p": dc.get("codec_p"),
-                       "wavlm_layerdrop": args.layerdrop},
+                       "wavlm_layerdrop": args.layerdrop, "hip_graphs": graph is not None},
             "roofline": roof,
             "step_mfma_frac": round(value / ws * TRAIN_FLOP_PER_UTT / 2.5e15, 4),
             "kernels": {k: {kk: round(vv, 5) if isinstance(vv, float) else vv for kk, vv in v.items()}

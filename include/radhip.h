@@ -47,6 +47,11 @@ const char* rdx_strerror(int code);
 int rdx_sincconv_absmaxpool_fwd(const float* x, int64_t batch, int64_t len, const float* filters,
                                 int channels, int ksize, int mask_lo, int mask_hi, float* out,
                                 void* stream);
+/* Same, with the band mask [lo, hi) read from device memory (int32[2]) at execution time, so a
+ * captured HIP graph can be replayed with a fresh mask per call. */
+int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch, int64_t len,
+                                        const float* filters, int channels, int ksize,
+                                        const int32_t* mask_dev, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Bidirectional Mamba (replaces mamba_ssm Mamba.forward -> mamba_inner_fn, called twice per

@@ -65,7 +65,7 @@ def _p(t):
 
 
 # --------------------------------------------------------------------------------- SincConv ----
-def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0):
+def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
     """|conv1d(x, filters)| max-pooled 3x3 over (channel, time): [B, L] -> [B, C//3, (L-K+1)//3].
 
     Replaces CONV.forward + F.max_pool2d(torch.abs(.), (3, 3))
@@ -78,8 +78,13 @@ def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0):
     C, K = filters.shape
     out = torch.empty(B, C // 3, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
     with _timed("sincconv_absmaxpool", x, sinc_flops(B, C, K, L)):
-        check(lib().rdx_sincconv_absmaxpool_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi),
-                                                _p(out), _stream(x)), "sincconv_absmaxpool_fwd")
+        if mask_dev is not None:
+            assert mask_dev.dtype == torch.int32 and mask_dev.numel() >= 2 and mask_dev.is_cuda
+            check(lib().rdx_sincconv_absmaxpool_fwd_devmask(_p(x), B, L, _p(filters), C, K, _p(mask_dev), _p(out),
+                                                            _stream(x)), "sincconv_absmaxpool_fwd_devmask")
+        else:
+            check(lib().rdx_sincconv_absmaxpool_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi),
+                                                    _p(out), _stream(x)), "sincconv_absmaxpool_fwd")
     return out
 
 
@@ -322,7 +327,7 @@ def resample_batch(x_flat, out_flat, kernels_dev, jobs):
           "resample_batch")
 
 
-def pad_mixup(sig_flat, offsets, lens, starts, max_len, perm=None, lam=1.0):
+def pad_mixup(sig_flat, offsets, lens, starts, max_len, perm=None, lam=1.0, out=None):
     """[nutt, max_len] batch: crop (len >= max_len, at starts[b]) or tile, then mixup with perm."""
     _require_gpu(sig_flat)
     n = len(offsets)
@@ -333,7 +338,9 @@ def pad_mixup(sig_flat, offsets, lens, starts, max_len, perm=None, lam=1.0):
             raise ValueError("pad_mixup: crop start outside the utterance")
     if perm is not None and sorted(perm) != list(range(n)):
         raise ValueError("pad_mixup: perm is not a permutation")
-    out = torch.empty(n, max_len, device=sig_flat.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty(n, max_len, device=sig_flat.device, dtype=torch.float32)
+    assert out.shape == (n, max_len) and out.dtype == torch.float32 and out.is_contiguous()
     I64 = ctypes.c_int64 * n
     pa = (ctypes.c_int * n)(*perm) if perm is not None else None
     check(lib().rdx_pad_mixup(_p(sig_flat), I64(*offsets), I64(*lens), I64(*starts), n, int(max_len), pa, float(lam),

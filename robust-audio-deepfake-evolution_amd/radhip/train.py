@@ -22,6 +22,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .ops import fgm_attack, pad_mixup, rawboost_batch, resample_batch, resample_kernel
+from .wavlm import compute_time_mask
 
 MAX_LEN = 64600
 CODEC_RATES = (8000, 6000, 4000)
@@ -260,7 +261,7 @@ class Augmenter:
             plan.append((rec, sr, start))
         return plan
 
-    def run(self, raw, offsets, lens, plan, perm=None, lam=1.0):
+    def run(self, raw, offsets, lens, plan, perm=None, lam=1.0, out=None):
         """raw: flat fp32 device buffer holding the utterances at `offsets`; returns x [B, max_len].
         The batch is first packed contiguously (one gather launch), so every later stage addresses a
         compact [sum(lens)] buffer whatever the layout of the resident corpus."""
@@ -308,7 +309,7 @@ class Augmenter:
             for b, o, nu in outs:
                 offs[b], cur_lens[b] = o, nu
         starts = [st for (_, _, st) in plan]
-        return pad_mixup(work, offs, cur_lens, starts, self.max_len, perm, lam)
+        return pad_mixup(work, offs, cur_lens, starts, self.max_len, perm, lam, out=out)
 
 
 # --------------------------------------------------------------------------- trainer ---------
@@ -435,6 +436,174 @@ class Trainer:
         self.loss_sum.zero_()
         self.n_seen = 0
         return v
+
+
+class _PinnedRing:
+    """Small ring of pinned host slots for H2D copies of per-replay inputs (non_blocking, stream-ordered;
+    a slot is reused only after the copy that read it has executed)."""
+
+    def __init__(self, nbytes, slots=4):
+        self.bufs = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(slots)]
+        self.events = [None] * slots
+        self.i = 0
+
+    def stage(self, arrays):
+        """arrays: list of (numpy array, device tensor); packs them into one slot and copies."""
+        k = self.i
+        self.i = (self.i + 1) % len(self.bufs)
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        buf = self.bufs[k]
+        off = 0
+        views = []
+        for a, dst in arrays:
+            a = np.ascontiguousarray(a)
+            nb = a.nbytes
+            off = (off + 15) & ~15
+            buf[off:off + nb].numpy()[:] = a.view(np.uint8).reshape(-1)
+            views.append((buf[off:off + nb].view(dst.dtype).view(dst.shape), dst))
+            off += nb
+        for src, dst in views:
+            dst.copy_(src, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+
+
+class GraphedMicroStep:
+    """The Phase-6 micro-batch as two replayed HIP graphs: G0 = clean forward + loss + backward,
+    G1 = adversarial forward + backward; the FGM attack (and its DDP all-reduce) and the restore run
+    eagerly between them, so no collective is captured. Every per-call random decision (SincConv band
+    mask, SpecAugment time mask, LayerDrop, mixup lambda/permutation) is drawn on the host in the
+    reference's order and staged into static device buffers before each replay; the model reads them
+    through its *_dev hooks. ~9k kernel launches per micro-batch become 2 graph launches."""
+
+    def __init__(self, trainer, batch, max_len=MAX_LEN):
+        self.tr = trainer
+        m = trainer.model
+        dev = trainer.device
+        self.B = batch
+        self.x = torch.zeros(batch, max_len, device=dev)
+        self.ya = torch.zeros(batch, dtype=torch.long, device=dev)
+        self.yb = torch.zeros(batch, dtype=torch.long, device=dev)
+        self.lam = torch.ones((), device=dev)
+        self.conv = m.sinc_stream.conv_time
+        self.core = m.wavlm_stream._core()
+        cfg = self.core.config
+        nl = len(self.core.encoder.layers)
+        # frames after the WavLM feature extractor
+        T = max_len
+        for k, st in zip(cfg.conv_kernel, cfg.conv_stride):
+            T = (T - k) // st + 1
+        self.T = T
+        self.mask = [torch.zeros(2, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.tmask = [torch.zeros(batch, T, dtype=torch.bool, device=dev) for _ in range(2)]
+        self.keep = [torch.ones(nl, dtype=torch.bool, device=dev) for _ in range(2)]
+        self.spec_on = bool(getattr(cfg, "apply_spec_augment", True)) and cfg.mask_time_prob > 0
+        self.nl = nl
+        self.ring = _PinnedRing(4096 + 2 * batch * (T + 16) + 64 * nl)
+        self.graphs = None
+        self.pool = None
+
+    # -- host draws, in the reference's per-forward order: SpecAugment (numpy), LayerDrop (torch CPU),
+    #    SincConv band mask (numpy + python random)
+    def _draw_pass(self):
+        c = self.core.config
+        tm = (compute_time_mask(self.B, self.T, c.mask_time_prob, c.mask_time_length, c.mask_time_min_masks)
+              if self.spec_on else np.zeros((self.B, self.T), dtype=bool))
+        p = c.layerdrop
+        keep = np.ones(self.nl, dtype=bool)
+        r = np.array([float(torch.rand([])) for _ in range(self.nl)])   # one CPU draw per layer, as HF
+        if p > 0:
+            keep[1:] = ~(r[1:] < p)
+        lo, hi = self.conv.draw_mask() if self.tr.freq_aug else (0, 0)
+        return tm, keep, np.array([lo, hi], dtype=np.int32)
+
+    def _bind(self, k):
+        self.conv.mask_dev = self.mask[k]
+        self.core.time_mask_dev = self.tmask[k]
+        self.core.encoder.keep_dev = self.keep[k]
+
+    def _unbind(self):
+        self.conv.mask_dev = None
+        self.core.time_mask_dev = None
+        self.core.encoder.keep_dev = None
+
+    def _pass(self, k):
+        tr = self.tr
+        self._bind(k)
+        with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32, cache_enabled=False):
+            _, out = tr.model(self.x, Freq_aug=tr.freq_aug)
+            loss = (self.lam * tr.criterion(out, self.ya) + (1.0 - self.lam) * tr.criterion(out, self.yb)) / tr.accum
+        loss.backward()
+        if k == 0:
+            tr.loss_sum.add_(loss.detach().double() * (tr.accum * self.B))
+
+    def _stage(self, y, lam, perm):
+        y = np.asarray(y, dtype=np.int64).reshape(-1)
+        yb = y[np.asarray(perm)] if perm is not None else y
+        d0 = self._draw_pass()
+        d1 = self._draw_pass()
+        arrs = [(y, self.ya), (yb, self.yb), (np.array(lam, dtype=np.float32), self.lam)]
+        for k, (tm, keep, mk) in enumerate((d0, d1)):
+            arrs += [(tm, self.tmask[k]), (keep, self.keep[k]), (mk, self.mask[k])]
+        self.ring.stage(arrs)
+
+    def _fgm(self):
+        fgm = self.tr.fgm
+        if fgm is not None:
+            fgm.attack()
+
+    def _restore(self):
+        if self.tr.fgm is not None:
+            self.tr.fgm.restore()
+
+    def capture(self, warmup=2):
+        tr = self.tr
+        tr.model.train()
+        if tr.freeze_bn:
+            for m in tr.model.modules():
+                if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
+                    m.eval()
+        saved_loss = tr.loss_sum.clone()
+        side = torch.cuda.Stream(device=tr.device)
+        side.wait_stream(torch.cuda.current_stream(tr.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._pass(0)
+                self._fgm()
+                self._pass(1)
+                self._restore()
+        torch.cuda.current_stream(tr.device).wait_stream(side)
+        torch.cuda.synchronize(tr.device)
+        self.pool = torch.cuda.graph_pool_handle()
+        gs = []
+        for k in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool):
+                self._pass(k)
+            gs.append(g)
+            if k == 0:
+                self._fgm()
+        self._restore()
+        torch.cuda.synchronize(tr.device)
+        self._unbind()
+        tr.grads.zero()
+        tr.loss_sum.copy_(saved_loss)
+        self.graphs = gs
+
+    def run(self, y, lam=1.0, perm=None, last_in_epoch=False):
+        """self.x must already hold the mixed batch (Augmenter.run(..., out=self.x))."""
+        tr = self.tr
+        self._stage(y, lam, perm)
+        self.graphs[0].replay()
+        self._fgm()
+        self.graphs[1].replay()
+        self._restore()
+        tr.micro += 1
+        tr.n_seen += self.B
+        if tr.micro % tr.accum == 0 or last_in_epoch:
+            tr.optimizer_step()
 
 
 def total_optimizer_steps(num_epochs, micro_batches_per_epoch, accum):

@@ -329,6 +329,9 @@ class Encoder(nn.Module):
         self.layer_norm = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
         self.dropout = nn.Dropout(cfg.hidden_dropout)
         self.layers = nn.ModuleList([EncoderLayer(cfg, i == 0, self.stable) for i in range(cfg.num_hidden_layers)])
+        # HIP-graph mode: LayerDrop decisions come from this device bool [num_layers] (True = run the
+        # layer); the layer is computed and torch.where selects, which is exact in value and gradient.
+        self.keep_dev = None
 
     def forward(self, h, layerdrop=None):
         p = self.cfg.layerdrop if layerdrop is None else layerdrop
@@ -340,7 +343,14 @@ class Encoder(nn.Module):
         pos = None
         for i, layer in enumerate(self.layers):
             states.append(h)
-            skip = self.training and i > 0 and p > 0 and bool(torch.rand([]) < p)
+            if self.training and self.keep_dev is not None and i > 0:
+                hn, pos = layer(h, pos)
+                h = torch.where(self.keep_dev[i], hn, h)
+                continue
+            # HF draws torch.rand([]) for EVERY layer (train or eval) and skips when training, i > 0 and
+            # draw < layerdrop; the same CPU-RNG consumption is kept here
+            r = float(torch.rand([])) if self.keep_dev is None else 1.0
+            skip = self.training and i > 0 and p > 0 and r < p
             if not skip:
                 h, pos = layer(h, pos)
         if self.stable:
@@ -384,6 +394,7 @@ class WavLMEncoderModel(nn.Module):
         if c.mask_time_prob > 0 or c.mask_feature_prob > 0:
             self.masked_spec_embed = nn.Parameter(torch.Tensor(c.hidden_size).uniform_())
         self.encoder = Encoder(c)
+        self.time_mask_dev = None   # HIP-graph mode: SpecAugment time mask [B, T] bool on the device
 
     def forward(self, input_values, output_hidden_states=True, layerdrop=None):
         x = input_values
@@ -397,8 +408,11 @@ class WavLMEncoderModel(nn.Module):
         c = self.config
         if self.training and getattr(c, "apply_spec_augment", True) and c.mask_time_prob > 0:
             B, T, _ = h.shape
-            m = torch.from_numpy(compute_time_mask(B, T, c.mask_time_prob, c.mask_time_length,
-                                                   c.mask_time_min_masks)).to(h.device, non_blocking=True)
+            if self.time_mask_dev is not None:
+                m = self.time_mask_dev
+            else:
+                m = torch.from_numpy(compute_time_mask(B, T, c.mask_time_prob, c.mask_time_length,
+                                                       c.mask_time_min_masks)).to(h.device, non_blocking=True)
             h = torch.where(m[..., None], self.masked_spec_embed.to(h.dtype), h)
         last, states = self.encoder(h, layerdrop=layerdrop)
         return last, states
