@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-microsteps", type=int, default=1)
     ap.add_argument("--config", default="Phase6_Proposed.conf")
-    ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the micro-step")
+    ap.add_argument("--graphs", action="store_true",
+                    help="replay the micro-step as HIP graphs (experimental: torch's captured bias-grad "
+                         "reductions are not replay-idempotent on this stack, see DESIGN.md)")
     return ap.parse_args()
 
 
@@ -217,7 +219,7 @@ def main():
     pyrandom.seed(1234 + rank)
     B = args.micro_batch
     graph = None
-    if not args.eager:
+    if args.graphs:
         graph = GraphedMicroStep(trainer, B)
         graph.capture()
 

@@ -394,13 +394,17 @@ class Trainer:
             return lam, perm
         return 1.0, None
 
-    def micro_step(self, x, y, lam=1.0, perm=None, last_in_epoch=False):
-        """One micro-batch: x [B, 64600] already mixed (perm/lam are those used for the mix)."""
+    def train_mode(self):
+        """model.train() + freeze_batch_norm_stats (main.py:44-51,1016-1018)."""
         self.model.train()
         if self.freeze_bn:
             for m in self.model.modules():
                 if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
                     m.eval()
+
+    def micro_step(self, x, y, lam=1.0, perm=None, last_in_epoch=False):
+        """One micro-batch: x [B, 64600] already mixed (perm/lam are those used for the mix)."""
+        self.train_mode()
         y = y.view(-1).long().to(self.device, non_blocking=True)
         ya = y
         yb = y[torch.tensor(perm, device=self.device)] if perm is not None else y
@@ -502,6 +506,7 @@ class GraphedMicroStep:
         self.spec_on = bool(getattr(cfg, "apply_spec_augment", True)) and cfg.mask_time_prob > 0
         self.nl = nl
         self.ring = _PinnedRing(4096 + 2 * batch * (T + 16) + 64 * nl)
+        self.adv = trainer.fgm is not None     # the adversarial pass exists only with FGM
         self.graphs = None
         self.pool = None
 
@@ -542,10 +547,9 @@ class GraphedMicroStep:
     def _stage(self, y, lam, perm):
         y = np.asarray(y, dtype=np.int64).reshape(-1)
         yb = y[np.asarray(perm)] if perm is not None else y
-        d0 = self._draw_pass()
-        d1 = self._draw_pass()
+        draws = [self._draw_pass()] + ([self._draw_pass()] if self.adv else [])
         arrs = [(y, self.ya), (yb, self.yb), (np.array(lam, dtype=np.float32), self.lam)]
-        for k, (tm, keep, mk) in enumerate((d0, d1)):
+        for k, (tm, keep, mk) in enumerate(draws):
             arrs += [(tm, self.tmask[k]), (keep, self.keep[k]), (mk, self.mask[k])]
         self.ring.stage(arrs)
 
@@ -560,32 +564,31 @@ class GraphedMicroStep:
 
     def capture(self, warmup=2):
         tr = self.tr
-        tr.model.train()
-        if tr.freeze_bn:
-            for m in tr.model.modules():
-                if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
-                    m.eval()
+        tr.train_mode()
         saved_loss = tr.loss_sum.clone()
         side = torch.cuda.Stream(device=tr.device)
         side.wait_stream(torch.cuda.current_stream(tr.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self._pass(0)
-                self._fgm()
-                self._pass(1)
-                self._restore()
+                if self.adv:
+                    self._fgm()
+                    self._pass(1)
+                    self._restore()
         torch.cuda.current_stream(tr.device).wait_stream(side)
         torch.cuda.synchronize(tr.device)
-        self.pool = torch.cuda.graph_pool_handle()
         gs = []
-        for k in (0, 1):
+        for k in ((0, 1) if self.adv else (0,)):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool):
+            # one private memory pool per graph (sharing one pool between the clean and the adversarial
+            # graph corrupted bias-gradient reductions of the clean graph on ROCm 7 / torch 2.10)
+            with torch.cuda.graph(g):
                 self._pass(k)
             gs.append(g)
-            if k == 0:
+            if k == 0 and self.adv:
                 self._fgm()
-        self._restore()
+        if self.adv:
+            self._restore()
         torch.cuda.synchronize(tr.device)
         self._unbind()
         tr.grads.zero()
@@ -597,9 +600,10 @@ class GraphedMicroStep:
         tr = self.tr
         self._stage(y, lam, perm)
         self.graphs[0].replay()
-        self._fgm()
-        self.graphs[1].replay()
-        self._restore()
+        if self.adv:
+            self._fgm()
+            self.graphs[1].replay()
+            self._restore()
         tr.micro += 1
         tr.n_seen += self.B
         if tr.micro % tr.accum == 0 or last_in_epoch:
