@@ -28,6 +28,7 @@ for p in (PKG, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")  # see radhip/__init__.py (graph memset replay)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -474,6 +474,30 @@ class _PinnedRing:
         self.events[k] = ev
 
 
+def check_graph_memset_replay(device):
+    """Capture hipMemsetAsync(0) + add(1) and replay it three times: every replay must leave 1.
+    Raises if the HIP runtime replays captured memset nodes wrongly (see radhip/__init__.py)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemsetAsync.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+    buf = torch.zeros(64, dtype=torch.int32, device=device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        rc = hip.hipMemsetAsync(buf.data_ptr(), 0, buf.numel() * 4, torch.cuda.current_stream().cuda_stream)
+        buf.add_(1)
+    if rc != 0:
+        raise RuntimeError(f"hipMemsetAsync failed during capture ({rc})")
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize(device)
+        if not bool((buf == 1).all()):
+            raise RuntimeError(
+                "HIP graph replays a captured memset with a wrong value; run with "
+                "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 set before the HIP runtime initialises (radhip does this "
+                "on import — import radhip before touching the GPU)")
+    del g
+
+
 class GraphedMicroStep:
     """The Phase-6 micro-batch as two replayed HIP graphs: G0 = clean forward + loss + backward,
     G1 = adversarial forward + backward; the FGM attack (and its DDP all-reduce) and the restore run
@@ -564,6 +588,7 @@ class GraphedMicroStep:
 
     def capture(self, warmup=2):
         tr = self.tr
+        check_graph_memset_replay(tr.device)
         tr.train_mode()
         saved_loss = tr.loss_sum.clone()
         side = torch.cuda.Stream(device=tr.device)

@@ -1,4 +1,5 @@
 import os
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")  # see radhip/__init__.py (graph memset replay)
 import sys
 
 import numpy as np
