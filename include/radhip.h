@@ -90,13 +90,15 @@ int rdx_selective_scan_fwd(int dtype, const void* u, const void* delta, const fl
 /* Backward. dy [dirs, B, L, D] fp32 with direction stride dy_dir_stride (0 = both directions see
  * the same dy, the Bi-Mamba case). Outputs:
  *   du, ddelta [dirs, B, L, D] (dtype)           — overwritten
- *   dBC_part   [rdx_scan_nblk_d(D), dirs, B, L, 2N] fp32 — partial dB|dC, caller sums dim 0
+ *   dBC        [dirs, B, L, 2N] fp32 — dB|dC, ACCUMULATED with atomics: the caller zeroes it
  *   dA_part    [dirs*B, D, N] fp32 (d/dA_log)    — caller sums dim 0
- *   dD_part, dbias_part [dirs*B, D] fp32         — caller sums dim 0 */
+ *   dD_part, dbias_part [dirs*B, D] fp32         — caller sums dim 0
+ * Needs dynamic LDS of 4*L*24 + L*12*es + L*32*es + 30 KB bytes (es = dtype size) <= 160 KB:
+ * L <= 640 for bf16, L <= 460 for f32; RDX_EUNSUPPORTED beyond. */
 int rdx_selective_scan_bwd(int dtype, const void* u, const void* delta, const float* A_log,
                            const void* Bm, const void* Cm, int64_t ldbc, const float* Dp,
                            const float* dt_bias, const float* ckpt, const float* dy,
-                           int64_t dy_dir_stride, void* du, void* ddelta, float* dBC_part,
+                           int64_t dy_dir_stride, void* du, void* ddelta, float* dBC,
                            float* dA_part, float* dD_part, float* dbias_part, int B, int L, int D,
                            int N, int dirs, void* stream);
 

@@ -12,6 +12,7 @@
 // Scan block = (12 channels d) x (16 states n) = 192 lanes; each 16-lane DPP row owns one channel,
 // each lane one state; the reduction over n (y = C.h) is a 4-step DPP row reduction.
 #include "common.h"
+#include <stdlib.h>
 
 namespace rdx {
 
@@ -219,118 +220,237 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_fwd_kernel(
   }
 }
 
-// Backward: grid (ceil(D/12), B, dirs). Per direction-step s (t = time index):
+// Backward. Per direction-step s (t = time index of step s):
 //   G_s = C_s dy_s + a_{s+1} G_{s+1};  ddt = sum_n G (A a h_{s-1} + B u);  du = sum_n G dt B + Dp dy
 //   dB_s = sum_d G dt u;  dC_s = sum_d dy h_s;  dA += G dt a h_{s-1};  dD += dy u
-// States are recomputed chunk by chunk (CK steps) from the forward checkpoints.
-template <typename T>
-__global__ __launch_bounds__(SCAN_THREADS) void scan_bwd_kernel(
+//
+// Block = (12 channels x 16 states) x SB_SEG time segments: wave w handles 4 channels (one per DPP row)
+// of segment w / 3. The reverse recurrence G is linear, so it is split in time:
+//   pass A  each segment runs G with carry-in 0 and multiplies its decays: carry_out = c0 + P * c_in;
+//   combine segment carries compose in LDS (last segment first);
+//   pass B  each segment re-runs its chunks (CK steps, states recomputed from the forward checkpoints)
+//           with the true carry-in and produces every gradient.
+// The sequential depth drops from L to ~L/SB_SEG steps and the chip holds SB_SEG x more waves.
+// dB|dC: 4 channels reduced in-wave (3 cross-lane shuffles), the block's 3 channel groups through LDS,
+// then one fp32 atomic per (block, t, n) into dBC (caller zeroes it). du/ddelta are written into the
+// consumed LDS slots and stored coalesced at the end.
+constexpr int SB_CHW = 3;                      // channel waves per segment (4 channels each)
+constexpr int SB_DBLK = 4 * SB_CHW;            // 12 channels per block (== SCAN_DBLK)
+static_assert(SB_DBLK == SCAN_DBLK, "bwd and fwd share the channel blocking");
+
+template <typename T, int SB_SEG>
+__host__ __device__ constexpr size_t scan_bwd_smem(int L) {
+  return sizeof(float) * (size_t)L * SB_DBLK * 2          // s_dt (-> ddelta), s_dy
+         + sizeof(T) * (size_t)L * SB_DBLK                // s_u (-> du)
+         + sizeof(T) * (size_t)L * SCAN_N * 2             // s_B, s_C
+         + sizeof(float) * SB_SEG * SCAN_CK * SB_CHW * 2 * SCAN_N  // s_red
+         + sizeof(float) * SB_SEG * 64 * SB_CHW * 2;      // s_car, s_prod
+}
+
+template <typename T, int SB_SEG>
+__global__ __launch_bounds__(64 * SB_CHW * SB_SEG, SB_SEG == 4 ? 6 : 1) void scan_bwd_kernel(
     const T* __restrict__ u, const T* __restrict__ delta, const float* __restrict__ A_log,
     const T* __restrict__ Bm, const T* __restrict__ Cm, int64_t ldbc, const float* __restrict__ Dp,
     const float* __restrict__ dt_bias, const float* __restrict__ ckpt, const float* __restrict__ dy,
-    int64_t dy_dir_stride, T* __restrict__ du, T* __restrict__ ddelta, float* __restrict__ dBC_part,
+    int64_t dy_dir_stride, T* __restrict__ du, T* __restrict__ ddelta, float* __restrict__ dBC,
     float* __restrict__ dA_part, float* __restrict__ dD_part, float* __restrict__ dbias_part, int B,
-    int L, int D, int dirs) {
+    int L, int D) {
+  constexpr int SB_THREADS = 64 * SB_CHW * SB_SEG;
   extern __shared__ float smem[];
-  float* s_u = smem;
-  float* s_dt = s_u + L * SCAN_DBLK;
-  float* s_dy = s_dt + L * SCAN_DBLK;
-  float* s_B = s_dy + L * SCAN_DBLK;
-  float* s_C = s_B + L * SCAN_N;
-  float* s_red = s_C + L * SCAN_N;  // [CK][2N] dB | dC for the current chunk
+  float* s_dt = smem;                                  // [L][12]
+  float* s_dy = s_dt + L * SB_DBLK;                    // [L][12]
+  float* s_red = s_dy + L * SB_DBLK;                   // [SEG][CK][CHW][2N]
+  float* s_car = s_red + SB_SEG * SCAN_CK * SB_CHW * 2 * SCAN_N;  // [SEG][CHW*64]
+  float* s_prod = s_car + SB_SEG * 64 * SB_CHW;        // [SEG][CHW*64]
+  T* s_u = reinterpret_cast<T*>(s_prod + SB_SEG * 64 * SB_CHW);  // [L][12]
+  T* s_B = s_u + L * SB_DBLK;                          // [L][16]
+  T* s_C = s_B + L * SCAN_N;                           // [L][16]
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int seg = wave / SB_CHW, cw = wave - seg * SB_CHW;
+  const int row = lane >> 4, n = lane & 15;
+  const int dl = cw * 4 + row;
   const int dblk = blockIdx.x, b = blockIdx.y, dir = blockIdx.z;
-  const int dl = threadIdx.x >> 4, n = threadIdx.x & 15;
-  const int d0 = dblk * SCAN_DBLK, d = d0 + dl;
+  const int d0 = dblk * SB_DBLK, d = d0 + dl;
   const int64_t db = (int64_t)dir * B + b;
   const int64_t ud_base = db * L * D;
   const int64_t bc_base = db * L * ldbc;
-  scan_stage(u, delta, Bm, Cm, ldbc, dt_bias, s_u, s_dt, s_B, s_C, ud_base, bc_base, d0, L, D);
   const float* dyb = dy + dir * dy_dir_stride + (int64_t)b * L * D;
-  for (int i = threadIdx.x; i < L * SCAN_DBLK; i += SCAN_THREADS) {
-    int t = i / SCAN_DBLK, c = i - t * SCAN_DBLK;
-    s_dy[i] = (d0 + c < D) ? dyb[(int64_t)t * D + d0 + c] : 0.f;
+
+  for (int i = tid; i < L * SB_DBLK; i += SB_THREADS) {
+    const int t = i / SB_DBLK, c = i - t * SB_DBLK;
+    const int dd = d0 + c;
+    float dtv = 0.f, dyv = 0.f;
+    T uu = T(0.f);
+    if (dd < D) {
+      const int64_t o = ud_base + (int64_t)t * D + dd;
+      uu = u[o];
+      dtv = softplusf_(ld(delta, o) + dt_bias[dd]);
+      dyv = dyb[(int64_t)t * D + dd];
+    }
+    s_u[i] = uu;
+    s_dt[i] = dtv;
+    s_dy[i] = dyv;
   }
-  for (int i = threadIdx.x; i < SCAN_CK * 2 * SCAN_N; i += SCAN_THREADS) s_red[i] = 0.f;
+  for (int i = tid; i < L * SCAN_N; i += SB_THREADS) {
+    const int t = i >> 4, j = i & 15;
+    s_B[i] = Bm[bc_base + (int64_t)t * ldbc + j];
+    s_C[i] = Cm[bc_base + (int64_t)t * ldbc + j];
+  }
   __syncthreads();
+
   const bool active = d < D;
   const float Aval = active ? -__expf(A_log[d * SCAN_N + n]) : 0.f;
   const float A2 = Aval * LOG2E;
   const float Dd = active ? Dp[d] : 0.f;
   const int nck = (L + SCAN_CK - 1) / SCAN_CK;
-  const int nblk_d = gridDim.x;
-  float carry = 0.f;  // a_{s+1} * G_{s+1}
-  float dA = 0.f, dDacc = 0.f, dbacc = 0.f;
-  for (int c = nck - 1; c >= 0; --c) {
-    const int sbeg = c * SCAN_CK;
-    float h0 = 0.f;
-    if (c > 0 && active) h0 = ckpt[((db * (nck - 1) + (c - 1)) * D + d) * SCAN_N + n];
-    float hs[SCAN_CK];
-    {
-      float h = h0;
+  // chunks [cb, cb + cnt) belong to this wave's segment; every wave runs max_cnt rounds (barriers)
+  const int base = nck / SB_SEG, rem = nck - base * SB_SEG;
+  const int cnt = base + (seg < rem ? 1 : 0);
+  const int cb = seg * base + min(seg, rem);
+  const int max_cnt = base + (rem > 0 ? 1 : 0);
+  const int slot = cw * 64 + lane;
+
+  // ---- pass A: local reverse carry of the segment, and the product of its decays
+  {
+    float carry = 0.f, prod = 1.f;
+    for (int c = cb + cnt - 1; c >= cb; --c) {
 #pragma unroll
-      for (int i = 0; i < SCAN_CK; ++i) {
-        const int s = sbeg + i;
+      for (int i = SCAN_CK - 1; i >= 0; --i) {
+        const int s = c * SCAN_CK + i;
         if (s < L) {
           const int t = dir ? (L - 1 - s) : s;
-          const float dtv = s_dt[t * SCAN_DBLK + dl];
-          const float a = exp2f(dtv * A2);
-          h = fmaf(a, h, dtv * s_u[t * SCAN_DBLK + dl] * s_B[t * SCAN_N + n]);
+          const float a = exp2f(s_dt[t * SB_DBLK + dl] * A2);
+          const float G = fmaf((float)s_C[t * SCAN_N + n], s_dy[t * SB_DBLK + dl], carry);
+          carry = a * G;
+          prod *= a;
         }
-        hs[i] = h;
       }
     }
+    s_car[seg * 64 * SB_CHW + slot] = carry;
+    s_prod[seg * 64 * SB_CHW + slot] = prod;
+  }
+  __syncthreads();
+  float carry = 0.f;
+  for (int k = SB_SEG - 1; k > seg; --k)
+    carry = fmaf(s_prod[k * 64 * SB_CHW + slot], carry, s_car[k * 64 * SB_CHW + slot]);
+
+  // ---- pass B
+  float dA = 0.f, dDacc = 0.f, dbacc = 0.f;
+  for (int r = 0; r < max_cnt; ++r) {
+    if (r < cnt) {
+      const int c = cb + cnt - 1 - r;
+      const int sbeg = c * SCAN_CK;
+      float h0 = 0.f;
+      if (c > 0 && active) h0 = ckpt[((db * (nck - 1) + (c - 1)) * D + d) * SCAN_N + n];
+      float hs[SCAN_CK];
+      {
+        float h = h0;
 #pragma unroll
-    for (int i = SCAN_CK - 1; i >= 0; --i) {
-      const int s = sbeg + i;
-      if (s < L) {
-        const int t = dir ? (L - 1 - s) : s;
-        const float dtv = s_dt[t * SCAN_DBLK + dl];
-        const float uu = s_u[t * SCAN_DBLK + dl];
-        const float dyv = s_dy[t * SCAN_DBLK + dl];
-        const float Bn = s_B[t * SCAN_N + n];
-        const float Cn = s_C[t * SCAN_N + n];
-        const float a = exp2f(dtv * A2);
-        const float hprev = (i > 0) ? hs[i > 0 ? i - 1 : 0] : h0;
-        const float G = fmaf(Cn, dyv, carry);
-        const float ah = a * hprev;
-        if (active) {
-          atomicAdd(&s_red[i * 2 * SCAN_N + n], G * dtv * uu);            // dB
-          atomicAdd(&s_red[i * 2 * SCAN_N + SCAN_N + n], dyv * hs[i]);    // dC
+        for (int i = 0; i < SCAN_CK; ++i) {
+          const int s = sbeg + i;
+          if (s < L) {
+            const int t = dir ? (L - 1 - s) : s;
+            const float dtv = s_dt[t * SB_DBLK + dl];
+            const float a = exp2f(dtv * A2);
+            h = fmaf(a, h, dtv * (float)s_u[t * SB_DBLK + dl] * (float)s_B[t * SCAN_N + n]);
+          }
+          hs[i] = h;
         }
-        dA = fmaf(G * dtv, ah, dA);
-        const float ddt = row16_sum(G * fmaf(Aval, ah, Bn * uu));
-        const float dus = row16_sum(G * dtv * Bn);
-        if (n == 0 && active) {
-          const float sg = -expm1f(-dtv);  // sigmoid(pre) from softplus(pre) = dt
-          const float ddl = ddt * sg;
-          const int64_t o = ud_base + (int64_t)t * D + d;
-          st(ddelta, o, ddl);
-          st(du, o, fmaf(Dd, dyv, dus));
-          dDacc = fmaf(dyv, uu, dDacc);
-          dbacc += ddl;
+      }
+      float* red = s_red + (seg * SCAN_CK) * SB_CHW * 2 * SCAN_N;
+#pragma unroll
+      for (int i = SCAN_CK - 1; i >= 0; --i) {
+        const int s = sbeg + i;
+        if (s < L) {  // wave-uniform
+          const int t = dir ? (L - 1 - s) : s;
+          const int o = t * SB_DBLK + dl;
+          const float dtv = s_dt[o];
+          const float uu = (float)s_u[o];
+          const float dyv = s_dy[o];
+          const float Bn = (float)s_B[t * SCAN_N + n];
+          const float Cn = (float)s_C[t * SCAN_N + n];
+          const float a = exp2f(dtv * A2);
+          const float hprev = (i > 0) ? hs[i > 0 ? i - 1 : 0] : h0;
+          const float G = fmaf(Cn, dyv, carry);
+          const float ah = a * hprev;
+          // dB (sum over channels of G dt u) and dC (sum of dy h): rows -> row 0 (dB) / row 2 (dC)
+          const float vB = active ? G * dtv * uu : 0.f;
+          const float vC = active ? dyv * hs[i] : 0.f;
+          const float s1 = vB + __shfl_xor(vB, 16, 64);
+          const float s2 = vC + __shfl_xor(vC, 16, 64);
+          const float x = (lane < 32) ? s2 : s1;
+          const float y = __shfl_xor(x, 32, 64);
+          if (row == 0) red[(i * SB_CHW + cw) * 2 * SCAN_N + n] = s1 + y;
+          if (row == 2) red[(i * SB_CHW + cw) * 2 * SCAN_N + SCAN_N + n] = s2 + y;
+          dA = fmaf(G * dtv, ah, dA);
+          const float ddt = row16_sum(G * fmaf(Aval, ah, Bn * uu));
+          const float dus = row16_sum(G * dtv * Bn);
+          if (n == 0 && active) {
+            const float ddl = ddt * -expm1f(-dtv);  // softplus' = sigmoid(pre) = 1 - exp(-dt)
+            s_dt[o] = ddl;                          // slot consumed: becomes ddelta
+            s_u[o] = T(fmaf(Dd, dyv, dus));         // becomes du
+            dDacc = fmaf(dyv, uu, dDacc);
+            dbacc += ddl;
+          }
+          carry = a * G;
         }
-        carry = a * G;
       }
     }
     __syncthreads();
-    // flush the chunk's dB / dC partial sums (over this block's channels)
-    for (int i = threadIdx.x; i < SCAN_CK * 2 * SCAN_N; i += SCAN_THREADS) {
-      const int ii = i / (2 * SCAN_N), j = i - ii * 2 * SCAN_N;
-      const int s = sbeg + ii;
-      if (s < L) {
-        const int t = dir ? (L - 1 - s) : s;
-        dBC_part[((((int64_t)dblk * dirs + dir) * B + b) * L + t) * (2 * SCAN_N) + j] = s_red[i];
+    // flush this round's dB|dC: sum the channel groups, one atomic per (t, j) per block
+    for (int i = tid; i < SB_SEG * SCAN_CK * 2 * SCAN_N; i += SB_THREADS) {
+      const int k = i / (SCAN_CK * 2 * SCAN_N);
+      const int rr = i - k * SCAN_CK * 2 * SCAN_N;
+      const int ii = rr / (2 * SCAN_N), j = rr - ii * 2 * SCAN_N;
+      const int cntk = base + (k < rem ? 1 : 0);
+      if (r < cntk) {
+        const int cbk = k * base + min(k, rem);
+        const int s = (cbk + cntk - 1 - r) * SCAN_CK + ii;
+        if (s < L) {
+          const float* rk = s_red + ((k * SCAN_CK + ii) * SB_CHW) * 2 * SCAN_N + j;
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < SB_CHW; ++w) v += rk[w * 2 * SCAN_N];
+          const int t = dir ? (L - 1 - s) : s;
+          atomicAdd(&dBC[(db * L + t) * (2 * SCAN_N) + j], v);
+        }
       }
-      s_red[i] = 0.f;
     }
     __syncthreads();
   }
-  (void)nblk_d;
-  if (active) {
-    dA_part[(db * D + d) * SCAN_N + n] = dA * Aval;  // d/dA_log = dL/dA * A
+
+  // ---- per-(dir, b) parameter partials: sum the segments through LDS (reuse s_car / s_prod / s_red)
+  s_car[seg * 64 * SB_CHW + slot] = dA;
+  if (n == 0) {
+    s_red[seg * SB_DBLK + dl] = dDacc;
+    s_red[SB_SEG * SB_DBLK + seg * SB_DBLK + dl] = dbacc;
+  }
+  __syncthreads();
+  if (seg == 0 && active) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < SB_SEG; ++k) v += s_car[k * 64 * SB_CHW + slot];
+    dA_part[(db * D + d) * SCAN_N + n] = v * Aval;  // d/dA_log = dL/dA * A
     if (n == 0) {
-      dD_part[db * D + d] = dDacc;
-      dbias_part[db * D + d] = dbacc;
+      float vd = 0.f, vb = 0.f;
+#pragma unroll
+      for (int k = 0; k < SB_SEG; ++k) {
+        vd += s_red[k * SB_DBLK + dl];
+        vb += s_red[SB_SEG * SB_DBLK + k * SB_DBLK + dl];
+      }
+      dD_part[db * D + d] = vd;
+      dbias_part[db * D + d] = vb;
+    }
+  }
+  // ---- coalesced du / ddelta store
+  for (int i = tid; i < L * SB_DBLK; i += SB_THREADS) {
+    const int t = i / SB_DBLK, c = i - t * SB_DBLK;
+    if (d0 + c < D) {
+      const int64_t o = ud_base + (int64_t)t * D + d0 + c;
+      du[o] = s_u[i];
+      st(ddelta, o, s_dt[i]);
     }
   }
 }
@@ -439,27 +559,66 @@ extern "C" int rdx_selective_scan_fwd(int dtype, const void* u, const void* delt
   return RDX_OK;
 }
 
+template <typename T, int SEG>
+static int launch_scan_bwd(const void* u, const void* delta, const float* A_log, const void* Bm,
+                           const void* Cm, int64_t ldbc, const float* Dp, const float* dt_bias,
+                           const float* ckpt, const float* dy, int64_t dy_dir_stride, void* du,
+                           void* ddelta, float* dBC, float* dA_part, float* dD_part, float* dbias_part,
+                           int B, int L, int D, int dirs, hipStream_t st) {
+  const size_t smem = scan_bwd_smem<T, SEG>(L);
+  if (smem > 160 * 1024) return RDX_EUNSUPPORTED;
+  static bool attr_set = false;  // raise the dynamic-LDS cap once per instantiation
+  if (!attr_set && smem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_bwd_kernel<T, SEG>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  dim3 grid((D + SB_DBLK - 1) / SB_DBLK, B, dirs);
+  auto kern = &scan_bwd_kernel<T, SEG>;
+  hipLaunchKernelGGL(kern, grid, dim3(64 * SB_CHW * SEG), smem, st, (const T*)u, (const T*)delta,
+                     A_log, (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride, (T*)du,
+                     (T*)ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+template <typename T>
+static int launch_scan_bwd_any(const void* u, const void* delta, const float* A_log, const void* Bm,
+                               const void* Cm, int64_t ldbc, const float* Dp, const float* dt_bias,
+                               const float* ckpt, const float* dy, int64_t dy_dir_stride, void* du,
+                               void* ddelta, float* dBC, float* dA_part, float* dD_part, float* dbias_part,
+                               int B, int L, int D, int dirs, hipStream_t st) {
+  static int seg = [] {
+    const char* e = getenv("RADHIP_SCAN_BWD_SEG");  // tuning knob: 2 or 4 time segments per block
+    return (e && atoi(e) == 2) ? 2 : 4;
+  }();
+  if (seg == 2)
+    return launch_scan_bwd<T, 2>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride, du, ddelta,
+                                 dBC, dA_part, dD_part, dbias_part, B, L, D, dirs, st);
+  return launch_scan_bwd<T, 4>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride, du, ddelta,
+                               dBC, dA_part, dD_part, dbias_part, B, L, D, dirs, st);
+}
+
 extern "C" int rdx_selective_scan_bwd(int dtype, const void* u, const void* delta,
                                       const float* A_log, const void* Bm, const void* Cm,
                                       int64_t ldbc, const float* Dp, const float* dt_bias,
                                       const float* ckpt, const float* dy, int64_t dy_dir_stride,
-                                      void* du, void* ddelta, float* dBC_part, float* dA_part,
+                                      void* du, void* ddelta, float* dBC, float* dA_part,
                                       float* dD_part, float* dbias_part, int B, int L, int D, int N,
                                       int dirs, void* stream) {
   RDX_REQUIRE(u && delta && A_log && Bm && Cm && Dp && dt_bias && ckpt && dy && du && ddelta);
-  RDX_REQUIRE(dBC_part && dA_part && dD_part && dbias_part);
+  RDX_REQUIRE(dBC && dA_part && dD_part && dbias_part);
   RDX_REQUIRE(B > 0 && L > 0 && D > 0 && (dirs == 1 || dirs == 2) && ldbc >= N && dy_dir_stride >= 0);
   if (N != SCAN_N || L > SCAN_LMAX) return RDX_EUNSUPPORTED;
-  dim3 grid((D + SCAN_DBLK - 1) / SCAN_DBLK, B, dirs);
-  size_t smem = sizeof(float) * ((size_t)L * SCAN_DBLK * 3 + (size_t)L * SCAN_N * 2 +
-                                 (size_t)SCAN_CK * 2 * SCAN_N);
-  DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(scan_bwd_kernel<T>, grid, dim3(SCAN_THREADS), smem,
-                                           as_stream(stream), (const T*)u, (const T*)delta, A_log,
-                                           (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, dy,
-                                           dy_dir_stride, (T*)du, (T*)ddelta, dBC_part, dA_part, dD_part,
-                                           dbias_part, B, L, D, dirs));
-  RDX_LAUNCH_CHECK();
-  return RDX_OK;
+  if (dtype == RDX_F32)
+    return launch_scan_bwd_any<float>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride, du,
+                                  ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D, dirs, as_stream(stream));
+  if (dtype == RDX_BF16)
+    return launch_scan_bwd_any<__hip_bfloat16>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride,
+                                           du, ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D, dirs,
+                                           as_stream(stream));
+  return RDX_EINVAL;
 }
 
 extern "C" int rdx_bigate_fwd(int dtype, const float* y, int dirs, const void* z, int64_t ldz,

@@ -174,8 +174,7 @@ class SelectiveScan(torch.autograd.Function):
             dy_stride = B * L * D
         du = torch.empty_like(u)
         ddelta = torch.empty_like(u)
-        nblk = lib().rdx_scan_nblk_d(D)
-        dBC = torch.empty(nblk, dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)
+        dBC = torch.zeros(dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)  # accumulated atomically
         dA = torch.empty(dirs * B, D, N, device=u.device, dtype=torch.float32)
         dD = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
         dbias = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
@@ -185,7 +184,7 @@ class SelectiveScan(torch.autograd.Function):
                                                ctx.ldbc, _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du),
                                                _p(ddelta), _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs,
                                                _stream(u)), "selective_scan_bwd")
-        dBC = dBC.sum(0).to(Bm.dtype)
+        dBC = dBC.to(Bm.dtype)
         return du, ddelta, dA.sum(0), dBC[..., :N], dBC[..., N:], dD.sum(0), dbias.sum(0)
 
 

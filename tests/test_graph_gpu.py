@@ -80,9 +80,11 @@ def test_graphed_micro_steps_accumulate_same_grads(golden, fgm):
     for n, k in names:
         a, b = grads[0][off:off + k], grads[1][off:off + k]
         off += k
-        err = float((a - b).norm() / (a.norm() + 1e-12))
-        if err > 1e-4:
-            bad.append((n, err))
+        diff, ref = float((a - b).norm()), float(a.norm())
+        # absolute floor: e.g. attention_pool.bias feeds a softmax over time, its gradient is
+        # analytically zero and both paths return fp32 rounding noise
+        if diff > 1e-4 * ref and diff > 1e-6:
+            bad.append((n, diff, ref))
     assert not bad, bad
 
 
