@@ -55,9 +55,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-microsteps", type=int, default=1)
     ap.add_argument("--config", default="Phase6_Proposed.conf")
-    ap.add_argument("--graphs", action="store_true",
-                    help="replay the micro-step as HIP graphs (experimental: torch's captured bias-grad "
-                         "reductions are not replay-idempotent on this stack, see DESIGN.md)")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch the micro-step kernel by kernel instead of replaying it as HIP graphs")
     return ap.parse_args()
 
 
@@ -92,7 +91,7 @@ def build(config, device, layerdrop):
     return model
 
 
-def roofline_from_timing(timing):
+def roofline_from_timing(timing, graphed=False):
     rows = {}
     for name, evs in timing.items():
         ms = [s.elapsed_time(e) for s, e, _ in evs]
@@ -120,7 +119,10 @@ def roofline_from_timing(timing):
     roof = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": dom,
             "avg_launch_ms": round(r["avg_ms"], 5), "work_per_launch": r["avg_work"],
-            "work_unit": "FLOP" if bound == "mfma" else "bytes"}
+            "work_unit": "FLOP" if bound == "mfma" else "bytes",
+            "timing": ("HIP event-record nodes captured around each launch inside the replayed graphs; "
+                       "averaged over the launches of the timed region's last micro-batch") if graphed else
+                      "HIP events on the launch stream around every launch of the timed region"}
     return roof, rows
 
 
@@ -219,10 +221,12 @@ def main():
     import random as pyrandom
     pyrandom.seed(1234 + rank)
     B = args.micro_batch
-    graph = None
-    if args.graphs:
+    graph, graph_timing = None, {}
+    if not args.eager:
         graph = GraphedMicroStep(trainer, B)
+        ops.CAPTURE_TIMING = graph_timing   # event-record nodes around every radhip launch in the graphs
         graph.capture()
+        ops.CAPTURE_TIMING = None
 
     def micro(i, last):
         idx = np.random.randint(0, args.pool, size=B)
@@ -261,12 +265,16 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     timing, ops.TIMING = ops.TIMING, None
+    # graph mode: the captured events hold the timestamps of the last replay of each graph (the last
+    # micro-batch of the timed region); eager launches (augmentation, FGM) are in `timing`
+    for k, v in graph_timing.items():
+        timing.setdefault(k, []).extend(v)
     t = torch.tensor([wall], device=dev, dtype=torch.float64)
     if ws > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
     loss = trainer.epoch_loss()
-    roof, rows = roofline_from_timing(timing)
+    roof, rows = roofline_from_timing(timing, graphed=graph is not None)
     utts = ws * args.steps * args.accum * B
     value = utts / wall_max
     if rank == 0:

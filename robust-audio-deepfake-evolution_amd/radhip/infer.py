@@ -1,0 +1,90 @@
+"""Scoring pass: produce_evaluation_file (src/main.py:958-995) and its data-parallel form.
+
+Score = logits[:, 1] (or the OC-softmax cosine when the criterion carries a `center`). The output is
+one line "utt src key score" per trial, in protocol order. The score is written as Python's str() of
+the float32 value widened to a double, exactly as the reference's `.tolist()` + "{}".format does.
+
+`produce_evaluation_file_sharded` is the multi-GPU eval of SURVEY.md §8e. Each rank scores a
+contiguous shard of the trial list; the fp32 scores are all-gathered; rank 0 writes the file in
+protocol order. The bytes match the single-process file, because the scores are per-utterance and
+the order is fixed by the protocol.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+
+def _scores(model, batch_x, criterion=None):
+    feats, out = model(batch_x)
+    if criterion is not None and hasattr(criterion, "center"):
+        w = F.normalize(criterion.center, p=2, dim=1)
+        return F.normalize(feats, p=2, dim=1).mm(w.t()).view(-1)
+    return out[:, 1]
+
+
+def _write(save_path, trial_lines, fnames, scores):
+    if not (len(trial_lines) == len(fnames) == len(scores)):
+        raise AssertionError(f"{len(trial_lines)} trials, {len(fnames)} utterances, {len(scores)} scores")
+    with open(save_path, "w") as fh:
+        for fn, sco, trl in zip(fnames, scores, trial_lines):
+            _, utt_id, _, src, key = trl.strip().split(" ")
+            if fn != utt_id:
+                raise AssertionError(f"score order mismatch: {fn} != {utt_id}")
+            fh.write("{} {} {} {}\n".format(utt_id, src, key, sco))
+
+
+@torch.no_grad()
+def produce_evaluation_file(data_loader, model, device, save_path, trial_path, criterion=None):
+    """data_loader yields (batch_x [B, 64600], utt_ids); writes the score file."""
+    model.eval()
+    with open(trial_path) as f:
+        trial_lines = f.readlines()
+    fnames, scores = [], []
+    for batch_x, utt_id in data_loader:
+        s = _scores(model, batch_x.to(device), criterion)
+        fnames.extend(utt_id)
+        scores.extend(s.float().cpu().numpy().ravel().tolist())
+    _write(save_path, trial_lines, fnames, scores)
+    print("Scores saved to {}".format(save_path))
+
+
+def shard_bounds(n, world, rank):
+    """Contiguous shard [lo, hi) of n trials for `rank` (sizes differ by at most one)."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+@torch.no_grad()
+def produce_evaluation_file_sharded(dataset, model, device, save_path, trial_path, batch_size=32,
+                                    criterion=None, group=None):
+    """dataset[i] -> (x [64600], utt_id) in protocol order. Every rank calls this; rank 0 writes."""
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    model.eval()
+    n = len(dataset)
+    lo, hi = shard_bounds(n, world, rank)
+    local = []
+    for b0 in range(lo, hi, batch_size):
+        items = [dataset[i] for i in range(b0, min(hi, b0 + batch_size))]
+        xb = torch.stack([torch.as_tensor(it[0]) for it in items]).to(device)
+        local.append(_scores(model, xb, criterion).float())
+    local = torch.cat(local) if local else torch.zeros(0, device=device)
+    if world > 1:
+        width = shard_bounds(n, world, 0)[1]
+        buf = torch.zeros(width, device=local.device, dtype=torch.float32)
+        buf[:local.numel()] = local
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+        scores = torch.cat([p[:shard_bounds(n, world, r)[1] - shard_bounds(n, world, r)[0]]
+                            for r, p in enumerate(parts)])
+    else:
+        scores = local
+    if rank == 0:
+        with open(trial_path) as f:
+            trial_lines = f.readlines()
+        fnames = [dataset.utt_id(i) if hasattr(dataset, "utt_id") else dataset[i][1] for i in range(n)]
+        _write(save_path, trial_lines, fnames, scores.cpu().numpy().astype(np.float32).tolist())
+    if world > 1:
+        dist.barrier(group)

@@ -15,26 +15,36 @@ _DT = {torch.float32: _lib.RDX_F32, torch.bfloat16: _lib.RDX_BF16}
 # Optional live timing: when TIMING is a dict, every C-ABI launch below is bracketed by two HIP events
 # recorded on the stream it is launched on; TIMING[name] collects (start, end, work) tuples, where
 # `work` is the launch's algorithmic bytes or FLOPs (bench.py turns these into the roofline line).
+# CAPTURE_TIMING does the same while a HIP graph is being captured: the events are "external", i.e.
+# captured as event-record nodes, so every replay re-records them around the kernel and after the
+# last replay they hold that replay's timestamps.
 TIMING = None
+CAPTURE_TIMING = None
 
 
 class _timed:
-    __slots__ = ("name", "t", "work", "ev")
+    __slots__ = ("name", "t", "work", "ev", "reg")
 
     def __init__(self, name, t, work=0.0):
         self.name, self.t, self.work = name, t, work
+        self.reg = None
 
     def __enter__(self):
-        if TIMING is not None:
+        reg, external = TIMING, False
+        if CAPTURE_TIMING is not None and torch.cuda.is_current_stream_capturing():
+            reg, external = CAPTURE_TIMING, True
+        if reg is not None:
+            self.reg = reg
             s = torch.cuda.current_stream(self.t.device)
-            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev = (torch.cuda.Event(enable_timing=True, external=external),
+                       torch.cuda.Event(enable_timing=True, external=external))
             self.ev[0].record(s)
         return self
 
     def __exit__(self, *exc):
-        if TIMING is not None:
+        if self.reg is not None:
             self.ev[1].record(torch.cuda.current_stream(self.t.device))
-            TIMING.setdefault(self.name, []).append((self.ev[0], self.ev[1], self.work))
+            self.reg.setdefault(self.name, []).append((self.ev[0], self.ev[1], self.work))
         return False
 
 

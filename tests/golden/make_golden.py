@@ -12,6 +12,7 @@ import argparse
 import hashlib
 import io
 import json
+import tempfile
 import os
 import random
 import sys
@@ -297,6 +298,80 @@ def gen_eval(ref_root):
     print("wrote eval_golden.json")
 
 
+def gen_eval21(ref_src):
+    """2021-DF min-flip report (report_2021df_codec_breakdown.main) on a synthetic trial_metadata +
+    score file, run in a scratch cwd with relative file names (the report prints the paths)."""
+    import contextlib
+    import report_2021df_codec_breakdown as R21
+    rng = np.random.default_rng(21)
+    codecs = ["nocodec", "low_mp3", "high_mp3", "low_m4a", "high_m4a", "mp3m4a", "oggm4a"]
+    sources = ["asvspoof", "vcc2018", "vcc2020"]
+    meta, scores = [], []
+    for i in range(700):
+        key = "bonafide" if rng.random() < 0.2 else "spoof"
+        codec, src = codecs[i % 7], sources[(i // 7) % 3]
+        meta.append(f"LA_{i % 40:04d} DF_E_{2000000 + i} {codec} {src} {'bonafide' if key == 'bonafide' else 'A14'} "
+                    f"{key} notrim eval")
+        if i % 50 == 17:
+            continue                                   # unscored trial
+        mu = 0.8 if key == "bonafide" else -0.6
+        if codec in ("low_mp3", "mp3m4a"):
+            mu = -mu                                   # a flipped-sign group
+        sc = round(float(rng.normal(mu, 1.0)), 3)     # rounding -> ties
+        scores.append(f"DF_E_{2000000 + i} {sc}")
+    scores.append("garbage-line")
+    scores.append("DF_E_9999999 notafloat")
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            open("trial_metadata.txt", "w").write("\n".join(meta) + "\n")
+            open("scores.txt", "w").write("\n".join(scores) + "\n")
+            argv = sys.argv
+            sys.argv = ["r", "--score_file", "scores.txt", "--key_file", "trial_metadata.txt", "--out", "report.md"]
+            try:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    R21.main()
+            finally:
+                sys.argv = argv
+            report = open("report.md").read()
+        finally:
+            os.chdir(cwd)
+    with open(os.path.join(HERE, "eval21_golden.json"), "w") as f:
+        json.dump({"meta": meta, "scores": scores, "report": report}, f)
+    print("wrote eval21_golden.json")
+
+
+def gen_scorefile(main):
+    """produce_evaluation_file (src/main.py:958-995) with a toy model: the exact score-file bytes."""
+    import contextlib
+    rng = np.random.default_rng(22)
+    n = 37
+    x = rng.standard_normal((n, 6)).astype(np.float32)
+    w = rng.standard_normal((6, 2)).astype(np.float32)
+    trial = [f"LA_{i % 9:04d} LA_E_{1000000 + i} - {'-' if i % 4 == 0 else 'A1' + str(i % 10)} "
+             f"{'bonafide' if i % 4 == 0 else 'spoof'}" for i in range(n)]
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.from_numpy(w))
+
+        def forward(self, xb, Freq_aug=False):
+            return xb, xb @ self.w
+
+    ids = [t.split()[1] for t in trial]
+    batches = [(torch.from_numpy(x[i:i + 8]), ids[i:i + 8]) for i in range(0, n, 8)]
+    with tempfile.TemporaryDirectory() as d:
+        tp, sp = os.path.join(d, "trl.txt"), os.path.join(d, "score.txt")
+        open(tp, "w").write("\n".join(trial) + "\n")
+        with contextlib.redirect_stdout(io.StringIO()):
+            main.produce_evaluation_file(batches, Toy(), torch.device("cpu"), sp, tp)
+        text = open(sp).read()
+    npz(os.path.join(HERE, "scorefile.npz"), x=x, w=w, trial=np.array("\n".join(trial)), text=np.array(text))
+    print("wrote scorefile.npz")
+
+
 def gen_train(main):
     """FGM attack/restore and a toy train_epoch trajectory through the reference driver."""
     class Toy(torch.nn.Module):
@@ -396,11 +471,16 @@ def main_():
         gen_data(ref_src)
     if want("eval"):
         gen_eval(args.ref)
-    if want("train"):
+    if want("eval21"):
+        gen_eval21(ref_src)
+    if want("train") or want("scorefile"):
         import contextlib
         with contextlib.redirect_stdout(io.StringIO()):
             main = importlib.import_module("main")
-        gen_train(main)
+        if want("train"):
+            gen_train(main)
+        if want("scorefile"):
+            gen_scorefile(main)
     if want("model"):
         gen_model(DS)
 
