@@ -91,13 +91,7 @@ def build(config, device, layerdrop):
     return model
 
 
-def roofline_from_timing(timing, graphed=False):
-    rows = {}
-    for name, evs in timing.items():
-        ms = [s.elapsed_time(e) for s, e, _ in evs]
-        work = [w for _, _, w in evs]
-        rows[name] = {"launches": len(ms), "total_ms": float(sum(ms)), "avg_ms": float(np.mean(ms)),
-                      "avg_work": float(np.mean(work))}
+def roofline_from_rows(rows, graphed=False):
     if not rows:
         return None, rows
     dom = max(rows, key=lambda k: rows[k]["total_ms"])
@@ -120,8 +114,8 @@ def roofline_from_timing(timing, graphed=False):
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": dom,
             "avg_launch_ms": round(r["avg_ms"], 5), "work_per_launch": r["avg_work"],
             "work_unit": "FLOP" if bound == "mfma" else "bytes",
-            "timing": ("HIP event-record nodes captured around each launch inside the replayed graphs; "
-                       "averaged over the launches of the timed region's last micro-batch") if graphed else
+            "timing": ("device wall-clock stamps (rdx_timestamp_acc) captured around each launch inside the "
+                       "replayed HIP graphs, accumulated over every launch of the timed region") if graphed else
                       "HIP events on the launch stream around every launch of the timed region"}
     return roof, rows
 
@@ -221,10 +215,11 @@ def main():
     import random as pyrandom
     pyrandom.seed(1234 + rank)
     B = args.micro_batch
-    graph, graph_timing = None, {}
+    graph, graph_timer = None, None
     if not args.eager:
         graph = GraphedMicroStep(trainer, B)
-        ops.CAPTURE_TIMING = graph_timing   # event-record nodes around every radhip launch in the graphs
+        graph_timer = ops.GraphTimer(dev)
+        ops.CAPTURE_TIMING = graph_timer    # captured clock stamps around every radhip launch in the graphs
         graph.capture()
         ops.CAPTURE_TIMING = None
 
@@ -252,6 +247,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ops.TIMING = {}
+    if graph_timer is not None:
+        graph_timer.reset()
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -265,16 +262,23 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     timing, ops.TIMING = ops.TIMING, None
-    # graph mode: the captured events hold the timestamps of the last replay of each graph (the last
-    # micro-batch of the timed region); eager launches (augmentation, FGM) are in `timing`
-    for k, v in graph_timing.items():
-        timing.setdefault(k, []).extend(v)
+    rows = ops.event_rows(timing)            # eager launches (augmentation, FGM)
+    if graph_timer is not None:              # launches inside the replayed graphs
+        for k, r in graph_timer.rows().items():
+            if k in rows:
+                a = rows[k]
+                n = a["launches"] + r["launches"]
+                a["avg_work"] = (a["avg_work"] * a["launches"] + r["avg_work"] * r["launches"]) / n
+                a["launches"], a["total_ms"] = n, a["total_ms"] + r["total_ms"]
+                a["avg_ms"] = a["total_ms"] / n
+            else:
+                rows[k] = r
     t = torch.tensor([wall], device=dev, dtype=torch.float64)
     if ws > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
     loss = trainer.epoch_loss()
-    roof, rows = roofline_from_timing(timing, graphed=graph is not None)
+    roof, rows = roofline_from_rows(rows, graphed=graph is not None)
     utts = ws * args.steps * args.accum * B
     value = utts / wall_max
     if rank == 0:

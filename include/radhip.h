@@ -191,6 +191,13 @@ int rdx_fgm_attack(int ntensors, float* const* params, const float* const* grads
                    float* const* backup, const int64_t* numels, float eps, double* workspace,
                    void* stream);
 
+/* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
+ * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
+ * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its
+ * duration in device wall-clock ticks (rdx_wallclock_khz(device) kHz), acc[1] the launch count. */
+int rdx_timestamp_acc(int64_t* acc, int sign, void* stream);
+int rdx_wallclock_khz(int device);
+
 #ifdef __cplusplus
 }
 #endif

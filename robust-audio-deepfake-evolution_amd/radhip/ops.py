@@ -15,37 +15,86 @@ _DT = {torch.float32: _lib.RDX_F32, torch.bfloat16: _lib.RDX_BF16}
 # Optional live timing: when TIMING is a dict, every C-ABI launch below is bracketed by two HIP events
 # recorded on the stream it is launched on; TIMING[name] collects (start, end, work) tuples, where
 # `work` is the launch's algorithmic bytes or FLOPs (bench.py turns these into the roofline line).
-# CAPTURE_TIMING does the same while a HIP graph is being captured: the events are "external", i.e.
-# captured as event-record nodes, so every replay re-records them around the kernel and after the
-# last replay they hold that replay's timestamps.
+# Inside a HIP graph capture, events cannot become graph nodes on ROCm, so CAPTURE_TIMING (a
+# GraphTimer) brackets each launch with two captured device-clock stamp kernels (rdx_timestamp_acc)
+# that accumulate the launch's duration and count over every replay.
 TIMING = None
 CAPTURE_TIMING = None
 
 
+class GraphTimer:
+    """Per-launch-site accumulators [ticks, count] in device memory, filled by captured stamps."""
+
+    def __init__(self, device, capacity=1024):
+        self.device = torch.device(device)
+        self.acc = torch.zeros(capacity, 2, dtype=torch.int64, device=self.device)
+        self.sites = []                       # (name, work) per slot
+
+    def slot(self, name, work):
+        if len(self.sites) >= self.acc.shape[0]:
+            raise RuntimeError("GraphTimer: out of slots")
+        self.sites.append((name, float(work)))
+        return self.acc[len(self.sites) - 1]
+
+    def reset(self):
+        self.acc.zero_()
+
+    def rows(self):
+        """{name: {launches, total_ms, avg_ms, avg_work}} over everything replayed since reset()."""
+        khz = lib().rdx_wallclock_khz(self.device.index or 0)
+        if khz <= 0:
+            raise RuntimeError("rdx_wallclock_khz failed")
+        acc = self.acc.cpu().numpy()
+        out = {}
+        for i, (name, work) in enumerate(self.sites):
+            ticks, cnt = int(acc[i, 0]), int(acc[i, 1])
+            if cnt == 0:
+                continue
+            r = out.setdefault(name, {"launches": 0, "total_ms": 0.0, "work_sum": 0.0})
+            r["launches"] += cnt
+            r["total_ms"] += ticks / khz
+            r["work_sum"] += work * cnt
+        for r in out.values():
+            r["avg_ms"] = r["total_ms"] / r["launches"]
+            r["avg_work"] = r.pop("work_sum") / r["launches"]
+        return out
+
+
 class _timed:
-    __slots__ = ("name", "t", "work", "ev", "reg")
+    __slots__ = ("name", "t", "work", "ev", "reg", "site")
 
     def __init__(self, name, t, work=0.0):
         self.name, self.t, self.work = name, t, work
-        self.reg = None
+        self.reg = self.site = None
 
     def __enter__(self):
-        reg, external = TIMING, False
         if CAPTURE_TIMING is not None and torch.cuda.is_current_stream_capturing():
-            reg, external = CAPTURE_TIMING, True
-        if reg is not None:
-            self.reg = reg
+            self.site = CAPTURE_TIMING.slot(self.name, self.work)
+            check(lib().rdx_timestamp_acc(_p(self.site), -1, _stream(self.t)), "timestamp")
+        elif TIMING is not None:
+            self.reg = TIMING
             s = torch.cuda.current_stream(self.t.device)
-            self.ev = (torch.cuda.Event(enable_timing=True, external=external),
-                       torch.cuda.Event(enable_timing=True, external=external))
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev[0].record(s)
         return self
 
     def __exit__(self, *exc):
-        if self.reg is not None:
+        if self.site is not None:
+            check(lib().rdx_timestamp_acc(_p(self.site), 1, _stream(self.t)), "timestamp")
+        elif self.reg is not None:
             self.ev[1].record(torch.cuda.current_stream(self.t.device))
             self.reg.setdefault(self.name, []).append((self.ev[0], self.ev[1], self.work))
         return False
+
+
+def event_rows(timing):
+    """TIMING dict -> {name: {launches, total_ms, avg_ms, avg_work}} (call after synchronising)."""
+    rows = {}
+    for name, evs in timing.items():
+        ms = [s.elapsed_time(e) for s, e, _ in evs]
+        rows[name] = {"launches": len(ms), "total_ms": float(sum(ms)), "avg_ms": float(sum(ms) / len(ms)),
+                      "avg_work": float(sum(w for _, _, w in evs) / len(evs))}
+    return rows
 
 
 def sinc_flops(B, C, K, L):
