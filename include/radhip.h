@@ -191,6 +191,26 @@ int rdx_fgm_attack(int ntensors, float* const* params, const float* const* grads
                    float* const* backup, const int64_t* numels, float eps, double* workspace,
                    void* stream);
 
+/* ---- SincNet residual stack, NHWC fused epilogues (Residual_block.forward,
+ * src/models/DualStreamSEMamba.py:182-200, with freeze_bn: src/main.py:44-51,1016-1018) -----------
+ * Activations are [npix, C] row-major (channels_last), C % 8 == 0, C <= 512, 256 % (C/8) == 0.
+ * rdx_bnselu_fwd: y = selu(((c + conv_bias) - mean) * invstd * weight + bias)  (conv1 bias folded in,
+ *   frozen BN statistics). rdx_bnselu_bwd: dc = dy * selu'(u) * invstd * weight and ACCUMULATES into
+ *   sums[3][C] (caller zeroes): sum(dc) = d conv_bias, sum(dy selu' xhat) = d weight, sum(dy selu') = d bias.
+ * rdx_res_tail_fwd: y[r, wo, :] = max_{k<3} (a + identity + bias)[r, 3wo + k, :]  (MaxPool2d((1,3)) of
+ *   conv2 + identity; rows = N*H, W input columns, Wo = W/3); argmax one byte per output element.
+ * rdx_res_tail_bwd: dx[r, w, :] = dy at the argmax, 0 elsewhere (incl. the W % 3 tail); ACCUMULATES
+ *   sum(dy) per channel into dbias[C] (caller zeroes) = d conv2.bias = d conv_downsample.bias. */
+int rdx_bnselu_fwd(int dtype, const void* c, const float* conv_bias, const float* mean, const float* invstd,
+                   const float* weight, const float* bias, void* y, int64_t npix, int C, void* stream);
+int rdx_bnselu_bwd(int dtype, const void* c, const void* dy, const float* conv_bias, const float* mean,
+                   const float* invstd, const float* weight, const float* bias, void* dc, float* sums,
+                   int64_t npix, int C, void* stream);
+int rdx_res_tail_fwd(int dtype, const void* a, const void* identity, const float* bias, void* y,
+                     uint8_t* argmax, int64_t rows, int W, int C, void* stream);
+int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax, void* dx, float* dbias, int64_t rows,
+                     int W, int C, void* stream);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

@@ -81,6 +81,10 @@ SIGNATURES = {
     "rdx_resample_batch": (c_int, [c_vp, c_vp, c_vp, ctypes.POINTER(ResampleJob), c_int, c_vp]),
     "rdx_pad_mixup": (c_int, [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_int,
                               c_i64, ctypes.POINTER(c_int), c_f32, c_vp, c_vp]),
+    "rdx_bnselu_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "rdx_bnselu_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "rdx_res_tail_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "rdx_res_tail_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_timestamp_acc": (c_int, [c_vp, c_int, c_vp]),
     "rdx_wallclock_khz": (c_int, [c_int]),
     "rdx_fgm_attack": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),

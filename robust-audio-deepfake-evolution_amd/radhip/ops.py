@@ -404,3 +404,67 @@ def pad_mixup(sig_flat, offsets, lens, starts, max_len, perm=None, lam=1.0, out=
     check(lib().rdx_pad_mixup(_p(sig_flat), I64(*offsets), I64(*lens), I64(*starts), n, int(max_len), pa, float(lam),
                               _p(out), _stream(sig_flat)), "pad_mixup")
     return out
+
+
+# -------------------------------------------------------- SincNet residual stack (NHWC) -------
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+class BnSelu(torch.autograd.Function):
+    """selu(frozen_bn(c + conv_bias)) on an NHWC [N, C, H, W] tensor (conv1 run without its bias)."""
+
+    @staticmethod
+    def forward(ctx, c, conv_bias, mean, invstd, weight, bias):
+        _require_gpu(c)
+        c = _nhwc(c)
+        N, C, H, W = c.shape
+        f32 = [t.detach().contiguous().float() for t in (conv_bias, mean, invstd, weight, bias)]
+        y = torch.empty_like(c)
+        check(lib().rdx_bnselu_fwd(_dtype_code(c), _p(c), *[_p(t) for t in f32], _p(y), N * H * W, C, _stream(c)),
+              "bnselu_fwd")
+        ctx.save_for_backward(c, *f32)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        c, cb, mean, invstd, w, b = ctx.saved_tensors
+        N, C, H, W = c.shape
+        dy = _nhwc(dy.to(c.dtype))
+        dc = torch.empty_like(c)
+        sums = torch.zeros(3, C, device=c.device, dtype=torch.float32)
+        check(lib().rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(dy), _p(cb), _p(mean), _p(invstd), _p(w), _p(b), _p(dc),
+                                   _p(sums), N * H * W, C, _stream(c)), "bnselu_bwd")
+        return dc, sums[0], None, None, sums[1], sums[2]
+
+
+class ResTail(torch.autograd.Function):
+    """MaxPool2d((1, 3))(a + identity + bias) on NHWC tensors; the gradient w.r.t. a and identity is
+    the same scattered tensor, and bias gets sum(dy) per channel."""
+
+    @staticmethod
+    def forward(ctx, a, identity, bias):
+        _require_gpu(a, identity)
+        a, identity = _nhwc(a), _nhwc(identity.to(a.dtype))
+        N, C, H, W = a.shape
+        if identity.shape != a.shape:
+            raise ValueError(f"radhip: residual shapes differ {tuple(a.shape)} vs {tuple(identity.shape)}")
+        y = torch.empty(N, C, H, W // 3, device=a.device, dtype=a.dtype, memory_format=torch.channels_last)
+        arg = torch.empty(N, C, H, W // 3, device=a.device, dtype=torch.uint8, memory_format=torch.channels_last)
+        bf = bias.detach().contiguous().float()
+        check(lib().rdx_res_tail_fwd(_dtype_code(a), _p(a), _p(identity), _p(bf), _p(y), _p(arg), N * H, W, C,
+                                     _stream(a)), "res_tail_fwd")
+        ctx.save_for_backward(arg)
+        ctx.shape, ctx.dtype = (N, C, H, W), a.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dy = _nhwc(dy.to(ctx.dtype))
+        dx = torch.empty(N, C, H, W, device=dy.device, dtype=ctx.dtype, memory_format=torch.channels_last)
+        dbias = torch.zeros(C, device=dy.device, dtype=torch.float32)
+        check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(dx), _p(dbias), N * H, W, C, _stream(dy)),
+              "res_tail_bwd")
+        return dx, dx, dbias

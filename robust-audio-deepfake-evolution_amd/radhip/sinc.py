@@ -9,7 +9,9 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .ops import sincconv_absmaxpool
+import torch.nn.functional as F
+
+from .ops import BnSelu, ResTail, sincconv_absmaxpool
 
 
 def mel_edges(out_channels, sample_rate, nfft=512):
@@ -101,10 +103,29 @@ class Residual_block(nn.Module):
             self.conv_downsample = nn.Conv2d(nb_filts[0], nb_filts[1], padding=(0, 1), kernel_size=(1, 3), stride=1)
         self.mp = nn.MaxPool2d((1, 3))
 
+    def _fused_ok(self, x):
+        return (x.is_cuda and not self.bn2.training and x.dim() == 4
+                and x.is_contiguous(memory_format=torch.channels_last) and self.conv2.out_channels % 8 == 0)
+
     def forward(self, x):
         if not self.first and self.bn1.training:
             with torch.no_grad():
                 self.bn1(x)
+        if self._fused_ok(x):
+            # NHWC fused epilogues (csrc/sincnet.hip): conv1's bias is folded into the frozen-BN+SELU pass,
+            # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass
+            bn = self.bn2
+            c = F.conv2d(x, self.conv1.weight, None, self.conv1.stride, self.conv1.padding)
+            out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, torch.rsqrt(bn.running_var + bn.eps),
+                               bn.weight, bn.bias)
+            a = F.conv2d(out, self.conv2.weight, None, self.conv2.stride, self.conv2.padding)
+            if self.downsample:
+                idn = F.conv2d(x, self.conv_downsample.weight, None, self.conv_downsample.stride,
+                               self.conv_downsample.padding)
+                bias = self.conv2.bias + self.conv_downsample.bias
+            else:
+                idn, bias = x, self.conv2.bias
+            return ResTail.apply(a, idn, bias)
         out = self.conv1(x)
         out = self.selu(self.bn2(out))
         out = self.conv2(out)

@@ -260,3 +260,57 @@ def test_fgm_attack_matches_reference_fixture(golden):
     p = torch.ones(10, device=DEV)
     fgm_attack([p], [torch.zeros(10, device=DEV)], [torch.empty(10, device=DEV)], 0.5)
     assert torch.equal(p, torch.ones(10, device=DEV))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("first", [True, False])
+def test_fused_residual_block_matches_torch(dtype, first):
+    """SincNet Residual_block with frozen BN: fused NHWC epilogues (bnselu, res_tail) == the torch
+    conv/bn/selu/add/maxpool graph, forward and every gradient (incl. a W % 3 tail and ties)."""
+    from radhip.sinc import Residual_block
+    torch.manual_seed(0)
+    filts = [1, 32] if first else [32, 32]
+    blk = Residual_block(filts, first=first).to(DEV)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.5, 0.5)
+            m.running_var.uniform_(0.5, 2.0)
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    blk.eval()                                    # frozen BN (freeze_bn)
+    x = torch.randn(2, filts[0], 7, 101, device=DEV)
+    x[..., :3] = 0.0                              # ties inside the first pooling windows
+    x = x.contiguous(memory_format=torch.channels_last)
+    bf16 = dtype == torch.bfloat16
+
+    def run(fused, amp):
+        b = Residual_block(filts, first=first).to(DEV)
+        b.load_state_dict(blk.state_dict())
+        b.eval()
+        if not fused:
+            b._fused_ok = lambda _x: False         # torch conv/bn/selu/add/maxpool graph
+        xx = x.detach().clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = b(xx)
+        assert (not fused) or b._fused_ok(xx)
+        y.backward(g.to(y.dtype))
+        out = {"y": y.float(), "dx": xx.grad.float()}
+        out.update({n: p.grad.float() for n, p in b.named_parameters() if p.grad is not None})
+        return out
+
+    torch.manual_seed(1)
+    g = torch.randn(2, filts[1], 7, 101 // 3, device=DEV)
+    fused = run(True, bf16)
+    ref32 = run(False, False)
+    if not bf16:
+        for n, b in ref32.items():
+            scale = b.abs().max().item() + 1e-6
+            torch.testing.assert_close(fused[n] / scale, b / scale, rtol=1e-4, atol=1e-5, msg=n)
+    else:
+        # bf16 rounding can flip a max-pool argmax between near-equal values, which moves whole gradient
+        # entries: hold the fused path to torch's own bf16 graph's distance from the fp32 result
+        tb16 = run(False, True)
+        for n, b in ref32.items():
+            e_f = ((fused[n] - b).norm() / (b.norm() + 1e-12)).item()
+            e_t = ((tb16[n] - b).norm() / (b.norm() + 1e-12)).item()
+            assert e_f <= 1.5 * e_t + 1e-2, (n, e_f, e_t)
