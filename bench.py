@@ -33,10 +33,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PEAKS = {"hbm": 8000.0, "fp32": 157.3}      # GB/s ; TFLOP/s  (MI355X_MICROARCH.md, dense, no sparsity)
+PEAKS = {"hbm": 8000.0, "fp32": 157.3, "bf16": 2500.0}  # GB/s ; TFLOP/s (MI355X_MICROARCH.md, dense)
 KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "selective_scan_fwd": ("hbm", None),
                 "selective_scan_bwd": ("hbm", None), "layer_wsum_fwd": ("hbm", None),
-                "layer_wsum_bwd": ("hbm", None), "rawboost_batch": ("hbm", None)}
+                "layer_wsum_bwd": ("hbm", None), "rawboost_batch": ("hbm", None),
+                "attn_fwd": ("mfma", "bf16"), "attn_bwd": ("mfma", "bf16")}
 TRAIN_FLOP_PER_UTT = 0.72e12                # SURVEY.md §8d (algorithmic, FGM step)
 
 

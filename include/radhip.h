@@ -211,6 +211,26 @@ int rdx_res_tail_fwd(int dtype, const void* a, const void* identity, const float
 int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax, void* dx, float* dbias, int64_t rows,
                      int W, int C, void* stream);
 
+/* ---- WavLM self-attention with the gated relative-position bias (HF WavLMAttention as used by
+ * WavLMFrontend, src/models/DualStreamSEMamba.py:292-439), MFMA bf16, 64-dim heads -------------------
+ * q, k, v: bf16 [B, T, H*64] row views (row strides ldq/ldk/ldv, 16-byte aligned); gate [B, T, H] fp32;
+ * pos_bias [H, T, T] fp32 (frozen). S = q k^T * scale + gate[b,i,h] * pos_bias[h,i,j]; P = softmax(S);
+ * O = dropout_p(P) v -> o [B, T, H*64] bf16 (row stride ldo); lse [B, H, T] fp32 (saved for bwd).
+ * Dropout keeps (b,h,i,j) iff hash(seed, ((b*H+h)*T+i)*T+j) >= p*2^32, seed = f(seed_dev[0], salt)
+ * read on the device (HIP-graph replayable); rdx_attn_dropout_mask materialises that mask (tests).
+ * rdx_attn_bwd: D [B, H, T] fp32 workspace; dq, dk, dv bf16 [B, T, H*64] (row stride ldg), dgate
+ * [B, T, H] fp32 (all overwritten). */
+int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                 const float* gate, const float* pos_bias, const int64_t* seed_dev, int salt, float p_drop,
+                 float scale, void* o, int64_t ldo, float* lse, int B, int T, int H, int head_dim, void* stream);
+int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                 const float* gate, const float* pos_bias, const int64_t* seed_dev, int salt, float p_drop,
+                 float scale, const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo,
+                 float* D, void* dq, void* dk, void* dv, int64_t ldg, float* dgate, int B, int T, int H,
+                 int head_dim, void* stream);
+int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n,
+                          void* stream);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

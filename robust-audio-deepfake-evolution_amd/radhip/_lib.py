@@ -85,6 +85,12 @@ SIGNATURES = {
     "rdx_bnselu_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
     "rdx_res_tail_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_res_tail_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp,
+                             c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_attn_bwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp,
+                             c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int,
+                             c_int, c_vp]),
+    "rdx_attn_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_vp]),
     "rdx_timestamp_acc": (c_int, [c_vp, c_int, c_vp]),
     "rdx_wallclock_khz": (c_int, [c_int]),
     "rdx_fgm_attack": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),

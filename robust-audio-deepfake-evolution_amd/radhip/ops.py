@@ -468,3 +468,64 @@ class ResTail(torch.autograd.Function):
         check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(dx), _p(dbias), N * H, W, C, _stream(dy)),
               "res_tail_bwd")
         return dx, dx, dbias
+
+
+# ---------------------------------------------------------------- WavLM gated attention -------
+def _ld(t):
+    """Row stride of a [B, T, E] view whose last dim is contiguous (e.g. a column slice of q|k|v)."""
+    if t.dim() != 3 or t.stride(2) != 1 or t.stride(0) != t.shape[1] * t.stride(1):
+        raise ValueError("radhip attention: expected a [B, T, E] row view with unit column stride")
+    return t.stride(1)
+
+
+class GatedAttention(torch.autograd.Function):
+    """softmax(Q K^T / sqrt(64) + gate[b,i,h] * pb[h,i,j]) with dropout, times V, per head (64-dim heads),
+    on bf16 [B, T, H*64] row views; returns [B, T, H*64] bf16 (ready for out_proj). Gradients for q, k, v
+    and gate (the position bias pb comes from the frozen rel_attn_embed table and takes none)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, gate, pos_bias, seed, p_drop, salt):
+        _require_gpu(q, k, v, gate, pos_bias)
+        B, T, E = q.shape
+        H = gate.shape[2]
+        if E != H * 64 or q.dtype != torch.bfloat16 or k.dtype != q.dtype or v.dtype != q.dtype:
+            raise ValueError("radhip attention: bf16 q/k/v with 64-dim heads required")
+        if pos_bias.requires_grad:
+            raise ValueError("radhip attention: the position bias must be frozen")
+        gate = gate.contiguous().float()
+        pb = pos_bias.detach().contiguous().float()
+        o = torch.empty(B, T, E, device=q.device, dtype=q.dtype)
+        lse = torch.empty(B, H, T, device=q.device, dtype=torch.float32)
+        sd = seed if seed is not None else torch.zeros(1, dtype=torch.int64, device=q.device)
+        with _timed("attn_fwd", q, 2.0 * 2 * B * H * T * T * 64):
+            check(lib().rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), _p(sd), int(salt),
+                                     float(p_drop), 0.125, _p(o), E, _p(lse), B, T, H, 64, _stream(q)), "attn_fwd")
+        ctx.save_for_backward(q, k, v, gate, pb, sd, o, lse)
+        ctx.p, ctx.salt = float(p_drop), int(salt)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, gate, pb, sd, o, lse = ctx.saved_tensors
+        B, T, E = q.shape
+        H = gate.shape[2]
+        do = do.to(q.dtype).contiguous()
+        D = torch.empty(B, H, T, device=q.device, dtype=torch.float32)
+        dq = torch.empty(B, T, E, device=q.device, dtype=q.dtype)
+        dk, dv = torch.empty_like(dq), torch.empty_like(dq)
+        dgate = torch.empty(B, T, H, device=q.device, dtype=torch.float32)
+        with _timed("attn_bwd", q, 2.0 * 5 * B * H * T * T * 64):
+            check(lib().rdx_attn_bwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), _p(sd), ctx.salt,
+                                     ctx.p, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D), _p(dq), _p(dk), _p(dv), E,
+                                     _p(dgate), B, T, H, 64, _stream(q)), "attn_bwd")
+        return dq, dk, dv, dgate, None, None, None, None
+
+
+def attention_dropout_mask(seed, salt, p_drop, shape):
+    """The keep mask (uint8) GatedAttention uses for elements [B, H, T, T] (tests)."""
+    n = 1
+    for s in shape:
+        n *= s
+    keep = torch.empty(n, dtype=torch.uint8, device=seed.device)
+    check(lib().rdx_attn_dropout_mask(_p(seed), int(salt), float(p_drop), _p(keep), n, _stream(seed)), "attn_mask")
+    return keep.view(*shape)

@@ -23,6 +23,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .ops import GatedAttention
+
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
 # restated, not verifiable offline: parity unpinned for those regularisers)
 WAVLM_LARGE = dict(
@@ -252,8 +254,8 @@ class Attention(nn.Module):
         return buckets + torch.where(small, rel, large)
 
     def compute_bias(self, T, device):
-        """[H, T, T] relative position bias (HF WavLMAttention.compute_bias)."""
-        return self.rel_attn_embed(self._buckets(T, device)).permute(2, 0, 1)
+        """[H, T, T] relative position bias (HF WavLMAttention.compute_bias), contiguous."""
+        return self.rel_attn_embed(self._buckets(T, device)).permute(2, 0, 1).contiguous()
 
     def _qkv(self, h):
         q, k, v = self.q_proj, self.k_proj, self.v_proj
@@ -289,6 +291,16 @@ class Attention(nn.Module):
         gate = g[..., 0] * (g[..., 1] * self.gru_rel_pos_const.view(1, 1, H) - 1.0) + 2.0   # [B, T, H]
         qq, kk, vv = self._qkv(h)
         dt = qq.dtype
+        if (qq.is_cuda and dt == torch.bfloat16 and kk.dtype == dt and vv.dtype == dt and Dh == 64
+                and not position_bias.requires_grad):
+            # fused MFMA kernel (csrc/attention.hip): bias formed in registers, dropout mask from a device
+            # seed (HIP-graph replayable), output already [B, T, E] for out_proj
+            p = self.dropout if self.training else 0.0
+            seed = getattr(self, "_seed", None) if p > 0 else None
+            if p > 0 and seed is None:
+                raise RuntimeError("attention dropout needs the encoder's device seed (Encoder.forward sets it)")
+            o = GatedAttention.apply(qq, kk, vv, gate, position_bias, seed, p, getattr(self, "_salt", 0))
+            return frozen_linear(o, self.out_proj, self._out_cache), position_bias
         bias = (gate.permute(0, 2, 1).unsqueeze(-1) * position_bias.unsqueeze(0)).to(dt)   # [B, H, T, T]
         qh = qq.view(B, T, H, Dh).transpose(1, 2)
         kh = kk.view(B, T, H, Dh).transpose(1, 2)
@@ -345,6 +357,9 @@ class Encoder(nn.Module):
         self.layer_norm = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
         self.dropout = nn.Dropout(cfg.hidden_dropout)
         self.layers = nn.ModuleList([EncoderLayer(cfg, i == 0, self.stable) for i in range(cfg.num_hidden_layers)])
+        # device-side dropout seed of the fused attention kernel: advanced on the device once per forward,
+        # so a captured HIP graph draws fresh masks on every replay; initialised from torch's CPU RNG
+        self.register_buffer("_attn_rng", torch.randint(0, 2 ** 62, (1,), dtype=torch.int64), persistent=False)
         # HIP-graph mode: LayerDrop decisions come from this device bool [num_layers] (True = run the
         # layer); the layer is computed and torch.where selects, which is exact in value and gradient.
         self.keep_dev = None
@@ -357,6 +372,11 @@ class Encoder(nn.Module):
         h = self.dropout(h)
         states = []
         pos = None
+        if self.training and self.cfg.attention_dropout > 0 and h.is_cuda:
+            self._attn_rng.add_(1)
+            seed = self._attn_rng.clone()          # the value this forward (and its backward) uses
+            for i, layer in enumerate(self.layers):
+                layer.attention._seed, layer.attention._salt = seed, i
         for i, layer in enumerate(self.layers):
             states.append(h)
             if self.training and self.keep_dev is not None and i > 0:

@@ -314,3 +314,51 @@ def test_fused_residual_block_matches_torch(dtype, first):
             e_f = ((fused[n] - b).norm() / (b.norm() + 1e-12)).item()
             e_t = ((tb16[n] - b).norm() / (b.norm() + 1e-12)).item()
             assert e_f <= 1.5 * e_t + 1e-2, (n, e_f, e_t)
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_gated_attention_matches_torch(p_drop):
+    """Fused MFMA WavLM attention (gated rel-pos bias formed in registers, hashed dropout) vs an fp32
+    torch reference fed the same bf16 inputs and the kernel's own dropout mask; forward and the q/k/v/
+    gate gradients. k is a strided column view of a fused q|k|v tensor (as in the model)."""
+    from radhip.ops import GatedAttention, attention_dropout_mask
+    torch.manual_seed(0)
+    B, T, H, D = 2, 201, 4, 64
+    E = H * D
+    qkv = (0.5 * torch.randn(B, T, 3 * E, device=DEV)).to(torch.bfloat16)
+    q = qkv[..., :E].contiguous().requires_grad_()
+    k_full = qkv.clone().requires_grad_()
+    k = k_full[..., E:2 * E]
+    v = qkv[..., 2 * E:].contiguous().requires_grad_()
+    gate = torch.rand(B, T, H, device=DEV).mul(2).requires_grad_()
+    pb = torch.randn(H, T, T, device=DEV)
+    seed = torch.tensor([1234567], dtype=torch.int64, device=DEV)
+    o = GatedAttention.apply(q, k, v, gate, pb, seed, p_drop, 3)
+    go = torch.randn(B, T, E, device=DEV).to(torch.bfloat16)
+    o.backward(go)
+    # reference
+    qr, kr, vr = (t.detach().float().view(B, T, H, D).transpose(1, 2).requires_grad_() for t in (q, k, v))
+    gr = gate.detach().clone().requires_grad_()
+    s = qr @ kr.transpose(-1, -2) * 0.125 + gr.permute(0, 2, 1).unsqueeze(-1) * pb.unsqueeze(0)
+    pr = torch.softmax(s, -1)
+    if p_drop > 0:
+        keep = attention_dropout_mask(seed, 3, p_drop, (B, H, T, T)).float()
+        assert abs(keep.mean().item() - (1 - p_drop)) < 0.01
+        pr = pr * keep / (1 - p_drop)
+    orf = (pr @ vr).transpose(1, 2).reshape(B, T, E)
+    orf.backward(go.float())
+
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+    assert rel(o, orf) < 1e-2
+    assert rel(q.grad, qr.grad.transpose(1, 2).reshape(B, T, E)) < 2e-2
+    assert rel(k_full.grad[..., E:2 * E], kr.grad.transpose(1, 2).reshape(B, T, E)) < 2e-2
+    assert k_full.grad[..., :E].abs().max().item() == 0
+    assert rel(v.grad, vr.grad.transpose(1, 2).reshape(B, T, E)) < 2e-2
+    assert rel(gate.grad, gr.grad) < 2e-2
+    # a new seed gives a new mask; the same seed the same output
+    if p_drop > 0:
+        o2 = GatedAttention.apply(q, k, v, gate, pb, seed, p_drop, 3)
+        assert torch.equal(o2, o)
+        o3 = GatedAttention.apply(q, k, v, gate, pb, seed + 1, p_drop, 3)
+        assert not torch.equal(o3, o)
