@@ -157,7 +157,13 @@ class SincNetEncoder(nn.Module):
         x = self.conv_time.absmaxpool(x.float(), mask=freq_aug).unsqueeze(1)    # [B, 1, 23, T/3]
         x = self.selu(self.first_bn(x))
         if self.channels_last and x.is_cuda:
-            x = x.contiguous(memory_format=torch.channels_last)
+            x = x.contiguous()
+            # C == 1: NCHW memory is already NHWC, but torch keeps the NCHW strides and its layout
+            # heuristic would then run block 0's convs in NCHW (and copy every gradient back and forth).
+            # Restride to the channels_last form (same bytes) so MIOpen picks its NHWC kernels.
+            N, C, H, W = x.shape
+            x = x.as_strided((N, C, H, W), (C * H * W, 1, W * C, C)) if C == 1 else \
+                x.contiguous(memory_format=torch.channels_last)
         e = self.encoder(x)
         e_T, _ = torch.max(torch.abs(e), dim=2)
         return e_T.transpose(1, 2)

@@ -402,19 +402,32 @@ class Trainer:
                 if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
                     m.eval()
 
+    def cnn_reuse(self, mode, drop=False):
+        """FGM's adversarial pass reuses the frozen WavLM CNN features of the clean pass (identical input,
+        eval-mode frozen CNN), saving one CNN forward per micro-batch."""
+        wf = getattr(self.model, "wavlm_stream", None)
+        core = wf._core() if wf is not None and hasattr(wf, "_core") else None
+        if core is not None and hasattr(core, "cnn_reuse"):
+            core.cnn_reuse = mode
+            if drop:
+                core._cnn_feats = None
+
     def micro_step(self, x, y, lam=1.0, perm=None, last_in_epoch=False):
         """One micro-batch: x [B, 64600] already mixed (perm/lam are those used for the mix)."""
         self.train_mode()
         y = y.view(-1).long().to(self.device, non_blocking=True)
         ya = y
         yb = y[torch.tensor(perm, device=self.device)] if perm is not None else y
+        self.cnn_reuse("store" if self.fgm is not None else None)
         loss = self._fwd_loss(x, ya, yb, lam)
         self.scaler.scale(loss).backward()
         if self.fgm is not None:
             self.fgm.attack()
+            self.cnn_reuse("use")
             adv = self._fwd_loss(x, ya, yb, lam)
             self.scaler.scale(adv).backward()
             self.fgm.restore()
+        self.cnn_reuse(None, drop=True)
         self.micro += 1
         B = x.shape[0]
         self.loss_sum += loss.detach().double() * self.accum * B
@@ -561,6 +574,7 @@ class GraphedMicroStep:
     def _pass(self, k):
         tr = self.tr
         self._bind(k)
+        tr.cnn_reuse(("use" if k == 1 else "store") if self.adv else None)
         with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32, cache_enabled=False):
             _, out = tr.model(self.x, Freq_aug=tr.freq_aug)
             loss = (self.lam * tr.criterion(out, self.ya) + (1.0 - self.lam) * tr.criterion(out, self.yb)) / tr.accum

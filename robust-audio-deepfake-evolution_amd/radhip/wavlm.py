@@ -431,14 +431,28 @@ class WavLMEncoderModel(nn.Module):
             self.masked_spec_embed = nn.Parameter(torch.Tensor(c.hidden_size).uniform_())
         self.encoder = Encoder(c)
         self.time_mask_dev = None   # HIP-graph mode: SpecAugment time mask [B, T] bool on the device
+        # FGM: the adversarial pass feeds the same waveform through the frozen, eval-mode CNN, so its
+        # features equal the clean pass's. cnn_reuse = "store" keeps them, "use" reuses them (exact).
+        self.cnn_reuse = None
+        self._cnn_feats = None
+
+    def _cnn_frozen(self):
+        return not self.feature_extractor.training and not any(p.requires_grad for p in self.feature_extractor.parameters())
 
     def forward(self, input_values, output_hidden_states=True, layerdrop=None):
         x = input_values
-        if self.feature_extractor.training or any(p.requires_grad for p in self.feature_extractor.parameters()):
-            feats = self.feature_extractor(x)
-        else:
+        frozen = self._cnn_frozen()
+        if frozen and self.cnn_reuse == "use" and self._cnn_feats is not None:
+            if self._cnn_feats[0] != (x.data_ptr(), tuple(x.shape), x.dtype):
+                raise RuntimeError("WavLM CNN feature reuse: the adversarial pass got a different input")
+            feats = self._cnn_feats[1]
+        elif frozen:
             with torch.no_grad():
                 feats = self.feature_extractor(x)
+            if self.cnn_reuse == "store":
+                self._cnn_feats = ((x.data_ptr(), tuple(x.shape), x.dtype), feats)
+        else:
+            feats = self.feature_extractor(x)
         feats = feats.transpose(1, 2)
         h = self.feature_projection(feats)
         c = self.config

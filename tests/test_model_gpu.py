@@ -138,3 +138,31 @@ def test_train_trajectory_matches_reference_driver(golden):
     for k, p in toy.named_parameters():
         np.testing.assert_allclose(p.detach().cpu().numpy(), g[f"train_ema:{k}"], rtol=1e-5, atol=1e-6,
                                    err_msg=k)
+
+
+def test_fgm_cnn_feature_reuse_is_exact(golden):
+    """The adversarial FGM pass reuses the clean pass's frozen WavLM-CNN features: the accumulated
+    gradients equal those of a micro-step that recomputes the CNN (same seeds, fp32)."""
+    import random
+    from radhip.build import apply_lora_to_wavlm, load_config
+    from radhip.train import Trainer
+    cfg = load_config("Phase6_Proposed.conf")
+    cfg["training_config"]["accumulation_steps"] = 100
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy(np.clip(0.1 * rng.standard_normal((4, 64600)), -1, 1).astype(np.float32)).to(DEV)
+    y = torch.tensor([0, 1, 0, 1])
+    flats = []
+    for reuse in (True, False):
+        m, _ = _tiny_product(golden)
+        m = apply_lora_to_wavlm(m, cfg["training_config"])
+        tr = Trainer(m, cfg, DEV, total_steps=10, amp_dtype=torch.float32)
+        if not reuse:
+            tr.cnn_reuse = lambda mode, drop=False: None
+        np.random.seed(3)
+        random.seed(3)
+        torch.manual_seed(3)
+        tr.micro_step(x, y)
+        torch.cuda.synchronize()
+        flats.append(tr.grads.flat.clone())
+    err = ((flats[0] - flats[1]).norm() / flats[1].norm()).item()
+    assert err < 1e-5, err

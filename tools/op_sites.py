@@ -28,8 +28,11 @@ class Sites(TorchDispatchMode):
               if ("/radhip/" in f.filename or "/models/" in f.filename) and "op_sites" not in f.filename]
         loc = f"{st[-1].filename.split('/')[-1]}:{st[-1].lineno}" if st else "<autograd>"
         key = name
-        if name in ("_to_copy", "copy_") and hasattr(args[0], "dtype"):
-            key = f"{name} {str(args[0].dtype)[6:]}->{str(getattr(out, 'dtype', '?'))[6:]}"
+        if name in ("_to_copy", "copy_", "clone", "contiguous") and hasattr(args[0], "dtype"):
+            src = args[1] if name == "copy_" else args[0]
+            dst = args[0] if name == "copy_" else out
+            key = (f"{name} {str(src.dtype)[6:]}->{str(getattr(dst, 'dtype', '?'))[6:]} {tuple(src.shape)}"
+                   f" c={int(src.is_contiguous())}{int(dst.is_contiguous())}")
         self.c[(key, loc)] += 1
         return out
 
@@ -62,8 +65,9 @@ def main():
     for k, v in tot.most_common(40):
         print(f"{v:6d} {k}")
     print("== top (op, site)")
-    for (k, loc), v in s.c.most_common(70):
+    for (k, loc), v in s.c.most_common(90):
         print(f"{v:6d} {k:40s} {loc}")
+    return
     # SDPA backend with the WavLM attention shapes (B=2, H=16, T=201, Dh=64, float bias mask)
     from torch.profiler import ProfilerActivity, profile
     q = torch.randn(2, 16, 201, 64, device=dev, dtype=torch.bfloat16, requires_grad=True)
