@@ -4,6 +4,10 @@ Score = logits[:, 1] (or the OC-softmax cosine when the criterion carries a `cen
 one line "utt src key score" per trial, in protocol order. The score is written as Python's str() of
 the float32 value widened to a double, exactly as the reference's `.tolist()` + "{}".format does.
 
+`produce_evaluation_file_2021` fills the reference's missing 2021-DF scorer (src/main.py:36 comments
+out its import; :368 and :761 call it): one "utt score" line per trial of the 2021 protocol, which
+`calculate_EER_2021` / the codec report read back (first and last column).
+
 `produce_evaluation_file_sharded` is the multi-GPU eval of SURVEY.md §8e. Each rank scores a
 contiguous shard of the trial list; the fp32 scores are all-gathered; rank 0 writes the file in
 protocol order. The bytes match the single-process file, because the scores are per-utterance and
@@ -34,6 +38,27 @@ def _write(save_path, trial_lines, fnames, scores):
             fh.write("{} {} {} {}\n".format(utt_id, src, key, sco))
 
 
+def _write_2021(save_path, fnames, scores):
+    if len(fnames) != len(scores):
+        raise AssertionError(f"{len(fnames)} utterances, {len(scores)} scores")
+    with open(save_path, "w") as fh:
+        for fn, sco in zip(fnames, scores):
+            fh.write("{} {}\n".format(fn, sco))
+
+
+@torch.no_grad()
+def produce_evaluation_file_2021(data_loader, model, device, save_path, criterion=None):
+    """data_loader yields (batch_x, utt_ids) in 2021-protocol order; writes "utt score" lines."""
+    model.eval()
+    fnames, scores = [], []
+    for batch_x, utt_id in data_loader:
+        s = _scores(model, batch_x.to(device), criterion)
+        fnames.extend(utt_id)
+        scores.extend(s.float().cpu().numpy().ravel().tolist())
+    _write_2021(save_path, fnames, scores)
+    print("Scores saved to {}".format(save_path))
+
+
 @torch.no_grad()
 def produce_evaluation_file(data_loader, model, device, save_path, trial_path, criterion=None):
     """data_loader yields (batch_x [B, 64600], utt_ids); writes the score file."""
@@ -56,19 +81,29 @@ def shard_bounds(n, world, rank):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def _item_batches(dataset, batch_size):
+    def gen(lo, hi, device):
+        for b0 in range(lo, hi, batch_size):
+            items = [dataset[i] for i in range(b0, min(hi, b0 + batch_size))]
+            yield torch.stack([torch.as_tensor(it[0]) for it in items]).to(device), [it[1] for it in items]
+    return gen
+
+
 @torch.no_grad()
 def produce_evaluation_file_sharded(dataset, model, device, save_path, trial_path, batch_size=32,
-                                    criterion=None, group=None):
-    """dataset[i] -> (x [64600], utt_id) in protocol order. Every rank calls this; rank 0 writes."""
+                                    criterion=None, group=None, batches=None, fmt="2019"):
+    """dataset[i] -> (x [64600], utt_id) in protocol order. Every rank calls this; rank 0 writes.
+    `batches(lo, hi, device)` (e.g. data.EvalFeeder.batches: native decode + GPU pad) replaces the
+    item-wise path when given. fmt "2019": "utt src key score" checked against the 5-column trial
+    list; fmt "2021": "utt score" in 2021-protocol order."""
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
     model.eval()
     n = len(dataset)
     lo, hi = shard_bounds(n, world, rank)
+    batches = batches or _item_batches(dataset, batch_size)
     local = []
-    for b0 in range(lo, hi, batch_size):
-        items = [dataset[i] for i in range(b0, min(hi, b0 + batch_size))]
-        xb = torch.stack([torch.as_tensor(it[0]) for it in items]).to(device)
+    for xb, _ in batches(lo, hi, device):
         local.append(_scores(model, xb, criterion).float())
     local = torch.cat(local) if local else torch.zeros(0, device=device)
     if world > 1:
@@ -82,9 +117,14 @@ def produce_evaluation_file_sharded(dataset, model, device, save_path, trial_pat
     else:
         scores = local
     if rank == 0:
-        with open(trial_path) as f:
-            trial_lines = f.readlines()
         fnames = [dataset.utt_id(i) if hasattr(dataset, "utt_id") else dataset[i][1] for i in range(n)]
-        _write(save_path, trial_lines, fnames, scores.cpu().numpy().astype(np.float32).tolist())
+        vals = scores.cpu().numpy().astype(np.float32).tolist()
+        if fmt == "2021":
+            _write_2021(save_path, fnames, vals)
+        else:
+            with open(trial_path) as f:
+                trial_lines = f.readlines()
+            _write(save_path, trial_lines, fnames, vals)
+        print("Scores saved to {}".format(save_path))
     if world > 1:
         dist.barrier(group)

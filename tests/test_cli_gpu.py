@@ -1,0 +1,138 @@
+"""End-to-end CLI (main.py) on the GPU: a tiny ASVspoof-shaped database of FLAC files, one Phase-6
+training epoch through the HIP path (native decode -> GPU RawBoost/codec/pad/mixup -> graphed FGM
+micro-steps -> AdamW/EMA), the reference's output layout, then --eval with the saved weights and a
+2021-DF eval with the codec breakdown. Scores written by the CLI must equal a direct fp32 forward of
+the same weights on the reference's numpy `pad` of each file."""
+import json
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch
+
+from flac_writer import encode
+
+pytestmark = pytest.mark.gpu
+ATTACKS = [f"A{i:02d}" for i in range(7, 20)]
+
+
+def _write_utt(path, n, seed):
+    rng = np.random.default_rng(seed)
+    x = np.clip(np.round(3000 * rng.standard_normal(n)), -32768, 32767).astype(np.int64)
+    path.write_bytes(encode(x, plan=lambda f, c, b: {"kind": "verbatim"}))
+
+
+def _database(root, golden):
+    proto = root / "ASVspoof2019_LA_cm_protocols"
+    proto.mkdir(parents=True)
+    lens = [64000, 70000, 30000, 66000, 20000, 64000]
+    rows = {"train": [("LA_T_%07d" % i, "-" if i % 3 == 0 else "A01", "bonafide" if i % 3 == 0 else "spoof")
+                      for i in range(6)],
+            "dev": [("LA_D_%07d" % i, "-" if i % 2 == 0 else "A02", "bonafide" if i % 2 == 0 else "spoof")
+                    for i in range(4)],
+            "eval": [("LA_E_%07d" % i, "-", "bonafide") for i in range(2)]
+            + [("LA_E_%07d" % (i + 2), a, "spoof") for i, a in enumerate(ATTACKS)]}
+    names = {"train": "train.trn", "dev": "dev.trl", "eval": "eval.trl"}
+    for split, rs in rows.items():
+        d = root / f"ASVspoof2019_LA_{split}" / "flac"
+        d.mkdir(parents=True)
+        lines = []
+        for i, (utt, att, key) in enumerate(rs):
+            _write_utt(d / f"{utt}.flac", lens[i % len(lens)], seed=sum(map(ord, utt)))
+            lines.append(f"LA_00{i:02d} {utt} - {att} {key}")
+        (proto / f"ASVspoof2019.LA.cm.{names[split]}.txt").write_text("\n".join(lines) + "\n")
+    asv = root / "ASVspoof2019_LA_asv_scores"
+    asv.mkdir()
+    (asv / "ASVspoof2019.LA.asv.eval.gi.trl.scores.txt").write_text("\n".join(golden("eval_golden.json")["tdcf"]["asv_lines"]) + "\n")
+    return rows
+
+
+def _config(tmp_path, golden, db):
+    import main as cli  # noqa: F401  (puts the package on sys.path)
+    from radhip.build import load_config
+    cfg = load_config("Phase6_Proposed.conf")
+    g = golden("model_tiny.npz")
+    cfg["database_path"] = str(db)
+    cfg["num_epochs"] = 1
+    cfg["batch_size"] = 2
+    cfg["eval_output"] = "eval_scores.txt"
+    cfg["auto_eval_2021_df"] = False
+    cfg["test_config"] = {"batch_size": 4, "num_workers": 0}
+    cfg["training_config"]["accumulation_steps"] = 2
+    cfg["model_config"]["num_encoders"] = 2
+    cfg["model_config"]["wavlm_config"] = json.loads(str(g["wavlm_config"]))
+    p = tmp_path / "Tiny.conf"
+    p.write_text(json.dumps(cfg, indent=2))
+    return p, cfg
+
+
+def _direct_scores(cfg, weights, paths):
+    from radhip import audio
+    from radhip.build import apply_lora_to_wavlm, get_model, load_weights
+    from radhip.data import pad
+    m = apply_lora_to_wavlm(get_model(cfg["model_config"], "cuda"), cfg["training_config"])
+    load_weights(m, weights, "cuda", strict=False)
+    m.eval()
+    x = np.stack([pad(audio.read(p)[0]) for p in paths]).astype(np.float32)
+    with torch.no_grad():
+        _, out = m(torch.from_numpy(x).cuda())
+    return out[:, 1].float().cpu().numpy()
+
+
+def test_cli_train_eval_and_2021(tmp_path, golden):
+    import main as cli
+    db = tmp_path / "LA"
+    rows = _database(db, golden)
+    conf, cfg = _config(tmp_path, golden, db)
+    out = tmp_path / "exp"
+    cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--seed", "1234"]))
+    tag = out / "LA_Tiny_ep1_bs2"
+    for f in ("config.conf", "metric_log.txt", "eval_scores.txt", "t-DCF_EER.txt", "metrics/dev_score.txt",
+              "metrics/dev_t-DCF_EER_0epo.txt", "weights/best.pth", "weights/swa.pth",
+              "weights/checkpoint_epoch_000.pth"):
+        assert (tag / f).exists(), f
+    assert len(list((tag / "weights").glob("epoch_0_*.pth"))) == 1
+    assert "EER:" in (tag / "metric_log.txt").read_text()
+    lines = (tag / "eval_scores.txt").read_text().splitlines()
+    assert [ln.split()[0] for ln in lines] == [u for u, _, _ in rows["eval"]]
+    assert [ln.split()[1:3] for ln in lines] == [[a, k] for _, a, k in rows["eval"]]
+    scores = np.array([float(ln.split()[3]) for ln in lines])
+    assert np.isfinite(scores).all()
+
+    # --eval with the saved weights: the score file equals a direct fp32 forward of those weights
+    w = tag / "weights" / "best.pth"
+    cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--eval", "--eval_model_weights",
+                             str(w), "--comment", "ev"]))
+    ev = out / "LA_Tiny_ep1_bs2_ev"
+    lines = (ev / "eval_scores.txt").read_text().splitlines()
+    got = np.array([float(ln.split()[3]) for ln in lines])
+    paths = [db / "ASVspoof2019_LA_eval" / "flac" / f"{u}.flac" for u, _, _ in rows["eval"]]
+    ref = _direct_scores(cfg, w, paths)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)
+    assert (ev / "t-DCF_EER.txt").exists() and (ev / "loaded_model_t-DCF_EER.txt").exists()
+
+    # 2021 DF eval: "utt score" lines in protocol order + min-flip EER with the codec breakdown
+    df = tmp_path / "DF"
+    (df / "flac").mkdir(parents=True)
+    trl, meta = [], []
+    for i, (codec, key) in enumerate([("mp3m4a", "bonafide"), ("low_mp3", "spoof"), ("high_m4a", "spoof"),
+                                      ("nocodec", "bonafide"), ("low_mp3", "bonafide"), ("high_m4a", "spoof")]):
+        utt = "DF_E_%07d" % i
+        shutil.copy(paths[i], df / "flac" / f"{utt}.flac")
+        trl.append(f"LA_00{i:02d} {utt} {codec} asvspoof A{7 + i:02d} {key} notrim eval")
+        meta.append(trl[-1])
+    (df / "ASVspoof2021.DF.cm.eval.trl.txt").write_text("\n".join(trl) + "\n")
+    (tmp_path / "meta.txt").write_text("\n".join(meta) + "\n")
+    cfg21 = dict(cfg, database_path=str(df), is_eval_2021=True, key_file=str(tmp_path / "meta.txt"))
+    conf21 = tmp_path / "Tiny21.conf"
+    conf21.write_text(json.dumps(cfg21))
+    cli.main(cli.parse_args(["--config", str(conf21), "--output_dir", str(out), "--eval", "--eval_model_weights",
+                             str(w)]))
+    t21 = out / "LA_Tiny21_ep1_bs2"
+    lines = (t21 / "eval_scores.txt").read_text().splitlines()
+    assert [ln.split()[0] for ln in lines] == ["DF_E_%07d" % i for i in range(6)]
+    np.testing.assert_allclose([float(ln.split()[1]) for ln in lines], ref[:6], rtol=1e-4, atol=1e-5)
+    rep = (t21 / "t-DCF_EER_2021DF.txt").read_text()
+    assert "EER" in rep and "low_mp3" in rep
+    os.environ.pop("WORLD_SIZE", None)
