@@ -231,6 +231,45 @@ int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
 int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n,
                           void* stream);
 
+/* ---- Fused WavLM encoder layer pieces (HF WavLMEncoderLayerStableLayerNorm + peft LoRA q/v as
+ * run by WavLMFrontend, src/models/DualStreamSEMamba.py:292-439 and src/main.py:103-158). Row-major
+ * fp32 residual stream h [M, E] (M = B*T tokens, E = 1024, one wave per row), bf16 GEMM operands.
+ * Dropouts use the attention's counter hash keyed by (seed_dev[0], salt, m*E + e); p = 0 or a null
+ * seed_dev disables one.
+ * rdx_wl_ln1_fwd: x1 = LN1(h) -> bf16 x1[:, 0:E] (row stride ldx); gate[m, h] = ga (gb c_h - 1) + 2 with
+ *   (ga, gb) = sigmoid of the 4-sums of wg [8, 64] x1_head + bg (gconst = c [H]); with lora_aq/lora_av
+ *   [r, E] (r = 8) also x1[:, E + k] = sum_e A_k[e] drop_k(x1)[e] (k < r: q adapter, else v); mean/rstd [M] saved.
+ * rdx_wl_add_ln_fwd: h2 = h + drop(delta) (fp32 out), x = LN(h2) bf16, mean/rstd saved.
+ * rdx_wl_residual: out = h + drop(delta) over n elements.  rdx_wl_dropout_bwd: out = drop(g) in bf16.
+ * rdx_wl_gelu: mode 0 out = gelu(u) (erf form); mode 1 out = dy * gelu'(u).
+ * rdx_wl_ln_bwd: dh = dres + LN_bwd(dx) (dres nullable); ddrop = drop(dh) bf16 when non-null.
+ * rdx_wl_ln1_bwd: dx1 = dX1[:, :E] + gate and LoRA-A backward terms, dh = dres + LN1_bwd(dx1); with LoRA
+ *   also xd [2, M, E] bf16 = the dropped x1 of each adapter (operand of the d lora_A GEMMs).
+ * rdx_wl_lora_pack: for every layer l, wext[l] [3E, ldw] bf16 columns E..E+2r <- scale * lora_B
+ *   (q rows 0..E-1, v rows 2E..3E-1); bq, bv, wext are DEVICE arrays of nl pointers. */
+int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float eps, const float* wg,
+                   const float* bg, const float* gconst, const float* lora_aq, const float* lora_av, int r,
+                   const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean,
+                   float* rstd, int64_t M, int E, void* stream);
+int rdx_wl_add_ln_fwd(const float* h, const void* delta, const int64_t* seed_dev, int salt, float p, float* h2,
+                      const float* gamma, const float* beta, float eps, void* x, float* mean, float* rstd,
+                      int64_t M, int E, void* stream);
+int rdx_wl_residual(const float* h, const void* delta, const int64_t* seed_dev, int salt, float p, float* out,
+                    int64_t n, void* stream);
+int rdx_wl_dropout_bwd(const float* g, const int64_t* seed_dev, int salt, float p, void* out, int64_t n,
+                       void* stream);
+int rdx_wl_gelu(int mode, const void* u, const void* dy, void* out, int64_t n, void* stream);
+int rdx_wl_ln_bwd(const void* dx, int64_t ldd, const float* h, const float* mean, const float* rstd,
+                  const float* gamma, const float* dres, float* dh, const int64_t* seed_dev, int salt, float p,
+                  void* ddrop, int64_t M, int E, void* stream);
+int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
+                   const float* gconst, const float* lora_aq, const float* lora_av, int r,
+                   const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
+                   void* stream);
+int rdx_wl_lora_pack(int nl, const float* const* bq, const float* const* bv, void* const* wext, int64_t ldw,
+                     int r, float scale, int E, void* stream);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

@@ -62,24 +62,6 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x85ebca6bu;
-  h ^= h >> 13;
-  h *= 0xc2b2ae35u;
-  h ^= h >> 16;
-  return h;
-}
-// dropout keep decision for element index idx = ((b*H + h)*T + i)*T + j
-__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  uint32_t h = fmix32((uint32_t)idx * 0x9E3779B1u ^ (uint32_t)seed);
-  h = fmix32(h ^ (uint32_t)(idx >> 32) ^ ((uint32_t)(seed >> 32) * 0x85ebca6bu));
-  return h >= thr;
-}
-__device__ __forceinline__ uint64_t attn_seed(const int64_t* seed_dev, int salt) {
-  return (uint64_t)seed_dev[0] * 0x9E3779B97F4A7C15ull + (uint64_t)(uint32_t)salt * 0xD1B54A32D192ED03ull;
-}
-
 // stage the 32 x 64 tile held as 4 row-fragments (lane (r, h): row r, cols 16s + 8h + j) transposed
 // into LDS as t[col][row]
 __device__ __forceinline__ void stage_t(__bf16 (*t)[AT_LDP], const bf16x8* f, int r, int h) {

@@ -57,6 +57,26 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// Counter-hash dropout shared by every fused kernel: element `idx` is kept iff hash(seed, idx) >= p * 2^32,
+// so a backward pass regenerates the forward mask from (seed, salt, idx) alone.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+// dropout keep decision for element index idx = ((b*H + h)*T + i)*T + j
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
+  uint32_t h = fmix32((uint32_t)idx * 0x9E3779B1u ^ (uint32_t)seed);
+  h = fmix32(h ^ (uint32_t)(idx >> 32) ^ ((uint32_t)(seed >> 32) * 0x85ebca6bu));
+  return h >= thr;
+}
+__device__ __forceinline__ uint64_t attn_seed(const int64_t* seed_dev, int salt) {
+  return (uint64_t)seed_dev[0] * 0x9E3779B97F4A7C15ull + (uint64_t)(uint32_t)salt * 0xD1B54A32D192ED03ull;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace rdx

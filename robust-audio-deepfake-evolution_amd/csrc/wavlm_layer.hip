@@ -1,0 +1,626 @@
+// Fused pieces of the WavLM encoder layer (stable layer norm, frozen base + LoRA q/v) for the
+// Phase-6 training step: everything between the four hipBLASLt GEMMs and the MFMA attention.
+//
+// Reference: HF WavLMEncoderLayerStableLayerNorm / WavLMAttention / WavLMFeedForward (transformers
+// modeling_wavlm.py) as run by WavLMFrontend (src/models/DualStreamSEMamba.py:292-439), with peft
+// LoRA on q_proj/v_proj (src/main.py:103-158):
+//     x1 = LN1(h);  gate = ga * (gb * c_h - 1) + 2,  (ga, gb) = sigmoid(sum4(Wg x1_head + bg))
+//     [q k v] = x1 [Wq Wk Wv]^T + b + s * (B_q A_q drop(x1), 0, B_v A_v drop(x1))
+//     h2 = h + drop(out_proj(attn(q, k, v, gate)));  x2 = LN2(h2)
+//     h' = h2 + drop(W2 gelu(W1 x2 + b1) + b2)
+// Layout: one wave per token row (E = 1024 = 64 lanes x 16 contiguous fp32), so a row's LN
+// statistics, its 16 per-head gates (4 lanes per 64-dim head) and its 2r = 16 LoRA down-projections
+// are wave reductions. The LoRA down-projection a = A drop(x1) is written next to x1 into one
+// [M, E + 2r] bf16 operand, so the q/k/v GEMM (K = E + 2r against [Wqkv | s B]) applies the whole
+// LoRA update with no extra GEMM; its backward returns d a in the same GEMM.
+// Dropout: counter-hash masks (common.h) keyed by (layer seed, salt, m * E + e), regenerated in the
+// backward; the seed lives in device memory (HIP-graph replayable).
+#include "common.h"
+
+namespace rdx {
+
+constexpr int WL_E = 1024;
+constexpr int WL_VPL = WL_E / RDX_WAVE;  // 16 fp32 per lane
+constexpr int WL_R2 = 16;                // 2 * LoRA rank (q and v adapters, r = 8)
+
+struct Drop {
+  const int64_t* seed_dev;
+  int salt;
+  uint32_t thr;    // p * 2^32 (0: identity)
+  float inv_keep;  // 1 / (1 - p)
+};
+
+__device__ __forceinline__ float drop_scale(const Drop& d, uint64_t seed, uint64_t idx) {
+  return drop_keep(seed, idx, d.thr) ? d.inv_keep : 0.f;
+}
+
+__device__ __forceinline__ void load16(const float* p, float* v) {
+  const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float4 t = q[i];
+    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+  }
+}
+__device__ __forceinline__ void store16(float* p, const float* v) {
+  float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+__device__ __forceinline__ void load16_bf(const __hip_bfloat16* p, float* v) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint4 t = q[i];
+    uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[8 * i + 2 * j] = __uint_as_float(w[j] << 16);
+      v[8 * i + 2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+}
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return (uint32_t)(*reinterpret_cast<uint16_t*>(&b));
+}
+__device__ __forceinline__ void store16_bf(__hip_bfloat16* p, const float* v) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = bf16_bits(v[8 * i + 2 * j]) | (bf16_bits(v[8 * i + 2 * j + 1]) << 16);
+    q[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+__device__ __forceinline__ float bf16_round(float f) { return __bfloat162float(__float2bfloat16(f)); }
+
+// mean / rstd of a row held as 16 values per lane (two-pass, biased variance like torch)
+__device__ __forceinline__ void row_stats(const float* v, float eps, float& mean, float& rstd) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) s += v[i];
+  mean = wave_sum(s) * (1.0f / WL_E);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) {
+    float d = v[i] - mean;
+    q += d * d;
+  }
+  rstd = rsqrtf(wave_sum(q) * (1.0f / WL_E) + eps);
+}
+
+// Sum 16 per-lane values over the wave with 17 shuffles: lane l ends with the total of index
+// k(l) = 8 b5 + 4 b4 + 2 b3 + b2 (b = bits of l); lanes with l & 3 == 0 own distinct k.
+__device__ __forceinline__ float wave_sum16(float* v, int lane) {
+  float w8[8], w4[4], w2[2];
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float r = __shfl_xor(h5 ? v[j] : v[j + 8], 32, 64);
+    w8[j] = (h5 ? v[j + 8] : v[j]) + r;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float r = __shfl_xor(h4 ? w8[j] : w8[j + 4], 16, 64);
+    w4[j] = (h4 ? w8[j + 4] : w8[j]) + r;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float r = __shfl_xor(h3 ? w4[j] : w4[j + 2], 8, 64);
+    w2[j] = (h3 ? w4[j + 2] : w4[j]) + r;
+  }
+  float r = __shfl_xor(h2 ? w2[0] : w2[1], 4, 64);
+  float t = (h2 ? w2[1] : w2[0]) + r;
+  t += __shfl_xor(t, 2, 64);
+  t += __shfl_xor(t, 1, 64);
+  return t;
+}
+__device__ __forceinline__ int sum16_index(int lane) {
+  return 8 * ((lane >> 5) & 1) + 4 * ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+}
+
+struct GateW {
+  const float* wg;      // [8, 64] gru_rel_pos_linear.weight
+  const float* bg;      // [8]
+  const float* gconst;  // [H] gru_rel_pos_const
+};
+
+// gate pre-activations z[8] of this lane's head (4 lanes per head, 16 dims per lane)
+__device__ __forceinline__ void gate_z(const GateW& g, const float* x, int lane, float* z) {
+  const int part = lane & 3;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float4* w = reinterpret_cast<const float4*>(g.wg + j * 64 + part * 16);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 t = w[i];
+      acc += t.x * x[4 * i] + t.y * x[4 * i + 1] + t.z * x[4 * i + 2] + t.w * x[4 * i + 3];
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    z[j] = acc + g.bg[j];
+  }
+}
+
+struct Ln1Args {
+  const float* h;  // [M, E] layer input (fp32 residual stream)
+  const float* gamma;
+  const float* beta;
+  float eps;
+  GateW g;
+  const float* Aq;  // [r, E] lora_A (q), null without LoRA
+  const float* Av;  // [r, E] lora_A (v)
+  Drop dq, dv;      // LoRA dropouts (q, v)
+  __hip_bfloat16* x1;  // [M, ldx]: LN1 output in [0, E), LoRA down-projection in [E, E + 2r)
+  int64_t ldx;
+  float* gate;  // [M, H]
+  float* mean;
+  float* rstd;
+  int64_t M;
+};
+
+template <bool kLora>
+__global__ __launch_bounds__(256) void wl_ln1_fwd_kernel(Ln1Args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int e0 = lane * WL_VPL;
+  float v[WL_VPL], gm[WL_VPL], bt[WL_VPL];
+  load16(a.h + m * WL_E + e0, v);
+  float mean, rstd;
+  row_stats(v, a.eps, mean, rstd);
+  load16(a.gamma + e0, gm);
+  load16(a.beta + e0, bt);
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) v[i] = bf16_round((v[i] - mean) * rstd * gm[i] + bt[i]);
+  store16_bf(a.x1 + m * a.ldx + e0, v);
+  if (lane == 0) {
+    a.mean[m] = mean;
+    a.rstd[m] = rstd;
+  }
+  float z[8];
+  gate_z(a.g, v, lane, z);
+  if ((lane & 3) == 0) {
+    const int head = lane >> 2;
+    float ga = sigmoidf_(z[0] + z[1] + z[2] + z[3]);
+    float gb = sigmoidf_(z[4] + z[5] + z[6] + z[7]);
+    a.gate[m * (WL_E / 64) + head] = ga * (gb * a.g.gconst[head] - 1.0f) + 2.0f;
+  }
+  if (kLora) {
+    const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
+    const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
+    float mq[WL_VPL], mv[WL_VPL];
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i) {
+      const uint64_t idx = (uint64_t)m * WL_E + e0 + i;
+      mq[i] = v[i] * drop_scale(a.dq, sq, idx);
+      mv[i] = v[i] * drop_scale(a.dv, sv, idx);
+    }
+    float acc[WL_R2];
+#pragma unroll
+    for (int k = 0; k < WL_R2; ++k) {
+      const float* x = k < WL_R2 / 2 ? mq : mv;
+      const float* arow = k < WL_R2 / 2 ? a.Aq + (int64_t)k * WL_E : a.Av + (int64_t)(k - WL_R2 / 2) * WL_E;
+      const float4* w = reinterpret_cast<const float4*>(arow + e0);
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float4 t = w[i];
+        s += t.x * x[4 * i] + t.y * x[4 * i + 1] + t.z * x[4 * i + 2] + t.w * x[4 * i + 3];
+      }
+      acc[k] = s;
+    }
+    float tot = wave_sum16(acc, lane);
+    if ((lane & 3) == 0) a.x1[m * a.ldx + WL_E + sum16_index(lane)] = __float2bfloat16(tot);
+  }
+}
+
+// h2 = h + drop(delta) (fp32, stored), x = LN(h2) (bf16), mean / rstd saved
+struct AddLnArgs {
+  const float* h;
+  const __hip_bfloat16* delta;
+  Drop d;
+  float* h2;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  __hip_bfloat16* x;
+  float* mean;
+  float* rstd;
+  int64_t M;
+};
+
+__global__ __launch_bounds__(256) void wl_add_ln_fwd_kernel(AddLnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int e0 = lane * WL_VPL;
+  float v[WL_VPL], dl[WL_VPL], gm[WL_VPL], bt[WL_VPL];
+  load16(a.h + m * WL_E + e0, v);
+  load16_bf(a.delta + m * WL_E + e0, dl);
+  const uint64_t seed = a.d.thr ? attn_seed(a.d.seed_dev, a.d.salt) : 0;
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i)
+    v[i] += dl[i] * (a.d.thr ? drop_scale(a.d, seed, (uint64_t)m * WL_E + e0 + i) : 1.0f);
+  store16(a.h2 + m * WL_E + e0, v);
+  float mean, rstd;
+  row_stats(v, a.eps, mean, rstd);
+  load16(a.gamma + e0, gm);
+  load16(a.beta + e0, bt);
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) v[i] = (v[i] - mean) * rstd * gm[i] + bt[i];
+  store16_bf(a.x + m * WL_E + e0, v);
+  if (lane == 0) {
+    a.mean[m] = mean;
+    a.rstd[m] = rstd;
+  }
+}
+
+// out = h + drop(delta) over n = M * E elements (8 per thread)
+__global__ __launch_bounds__(256) void wl_residual_kernel(const float* __restrict__ h,
+                                                          const __hip_bfloat16* __restrict__ delta, Drop d,
+                                                          float* __restrict__ out, int64_t n) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i0 >= n) return;
+  const uint64_t seed = d.thr ? attn_seed(d.seed_dev, d.salt) : 0;
+  float4 a0 = reinterpret_cast<const float4*>(h + i0)[0], a1 = reinterpret_cast<const float4*>(h + i0)[1];
+  float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  uint4 t = *reinterpret_cast<const uint4*>(delta + i0);
+  uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float dv = __uint_as_float((j & 1) ? (w[j >> 1] & 0xffff0000u) : (w[j >> 1] << 16));
+    x[j] += dv * (d.thr ? drop_scale(d, seed, (uint64_t)(i0 + j)) : 1.0f);
+  }
+  reinterpret_cast<float4*>(out + i0)[0] = make_float4(x[0], x[1], x[2], x[3]);
+  reinterpret_cast<float4*>(out + i0)[1] = make_float4(x[4], x[5], x[6], x[7]);
+}
+
+// grad of drop(): out = drop_mask * g (fp32 in, bf16 out), n elements (8 per thread)
+__global__ __launch_bounds__(256) void wl_dropout_bwd_kernel(const float* __restrict__ g, Drop d,
+                                                             __hip_bfloat16* __restrict__ out, int64_t n) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i0 >= n) return;
+  const uint64_t seed = d.thr ? attn_seed(d.seed_dev, d.salt) : 0;
+  float4 a0 = reinterpret_cast<const float4*>(g + i0)[0], a1 = reinterpret_cast<const float4*>(g + i0)[1];
+  float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float s0 = d.thr ? drop_scale(d, seed, (uint64_t)(i0 + 2 * j)) : 1.0f;
+    float s1 = d.thr ? drop_scale(d, seed, (uint64_t)(i0 + 2 * j + 1)) : 1.0f;
+    w[j] = bf16_bits(x[2 * j] * s0) | (bf16_bits(x[2 * j + 1] * s1) << 16);
+  }
+  *reinterpret_cast<uint4*>(out + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
+// y = gelu(u) (mode 0) or du = dy * gelu'(u) (mode 1); bf16, 8 elements per thread
+template <int kMode>
+__global__ __launch_bounds__(256) void wl_gelu_kernel(const __hip_bfloat16* __restrict__ u,
+                                                      const __hip_bfloat16* __restrict__ dy,
+                                                      __hip_bfloat16* __restrict__ out, int64_t n) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i0 >= n) return;
+  uint4 t = *reinterpret_cast<const uint4*>(u + i0);
+  uint32_t w[4] = {t.x, t.y, t.z, t.w}, gw[4] = {0, 0, 0, 0};
+  if (kMode == 1) {
+    uint4 g = *reinterpret_cast<const uint4*>(dy + i0);
+    gw[0] = g.x; gw[1] = g.y; gw[2] = g.z; gw[3] = g.w;
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x0 = __uint_as_float(w[j] << 16), x1 = __uint_as_float(w[j] & 0xffff0000u);
+    float y0, y1;
+    if (kMode == 0) {
+      y0 = gelu_erf(x0);
+      y1 = gelu_erf(x1);
+    } else {
+      y0 = __uint_as_float(gw[j] << 16) * gelu_erf_grad(x0);
+      y1 = __uint_as_float(gw[j] & 0xffff0000u) * gelu_erf_grad(x1);
+    }
+    o[j] = bf16_bits(y0) | (bf16_bits(y1) << 16);
+  }
+  *reinterpret_cast<uint4*>(out + i0) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// LN backward with residual: dh = dres + rstd * (g - mean(g) - xhat * mean(g xhat)), g = dx * gamma.
+// Optionally also ddrop = drop_mask * dh (bf16): the gradient into the dropout that fed h.
+struct LnBwdArgs {
+  const __hip_bfloat16* dx;  // [M, ldd] (first E columns used)
+  int64_t ldd;
+  const float* h;  // LN input [M, E]
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* dres;  // [M, E] or null
+  float* dh;          // [M, E]
+  Drop d;
+  __hip_bfloat16* ddrop;  // [M, E] or null
+  int64_t M;
+};
+
+__device__ __forceinline__ void ln_bwd_row(const float* dx, const float* x, float mean, float rstd, const float* gm,
+                                           float* out) {
+  float g[WL_VPL], xh[WL_VPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) {
+    xh[i] = (x[i] - mean) * rstd;
+    g[i] = dx[i] * gm[i];
+    s1 += g[i];
+    s2 += g[i] * xh[i];
+  }
+  s1 = wave_sum(s1) * (1.0f / WL_E);
+  s2 = wave_sum(s2) * (1.0f / WL_E);
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) out[i] = rstd * (g[i] - s1 - xh[i] * s2);
+}
+
+__global__ __launch_bounds__(256) void wl_ln_bwd_kernel(LnBwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int e0 = lane * WL_VPL;
+  float dx[WL_VPL], x[WL_VPL], gm[WL_VPL], o[WL_VPL];
+  load16_bf(a.dx + m * a.ldd + e0, dx);
+  load16(a.h + m * WL_E + e0, x);
+  load16(a.gamma + e0, gm);
+  ln_bwd_row(dx, x, a.mean[m], a.rstd[m], gm, o);
+  if (a.dres) {
+    float r[WL_VPL];
+    load16(a.dres + m * WL_E + e0, r);
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i) o[i] += r[i];
+  }
+  store16(a.dh + m * WL_E + e0, o);
+  if (a.ddrop) {
+    const uint64_t seed = a.d.thr ? attn_seed(a.d.seed_dev, a.d.salt) : 0;
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i)
+      o[i] *= a.d.thr ? drop_scale(a.d, seed, (uint64_t)m * WL_E + e0 + i) : 1.0f;
+    store16_bf(a.ddrop + m * WL_E + e0, o);
+  }
+}
+
+// LN1 backward: dx1 = dX1[:, :E] + gate backward + LoRA-A backward; dh = dres + LN1_bwd(dx1).
+// Also writes the dropped LN output of each adapter (xd[0] q, xd[1] v) for the dA GEMMs.
+struct Ln1BwdArgs {
+  const __hip_bfloat16* dx1;  // [M, ldx] = d [x1 | a] from the qkv GEMM backward
+  int64_t ldx;
+  const float* dgate;  // [M, H]
+  const float* h;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+  GateW g;
+  const float* Aq;  // [r, E] or null
+  const float* Av;
+  Drop dq, dv;
+  const float* dres;  // [M, E]
+  float* dh;
+  __hip_bfloat16* xd;  // [2, M, E] or null
+  int64_t M;
+};
+
+template <bool kLora>
+__global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int e0 = lane * WL_VPL;
+  const int part = lane & 3, head = lane >> 2;
+  float x[WL_VPL], x1[WL_VPL], gm[WL_VPL], bt[WL_VPL], dx[WL_VPL];
+  load16(a.h + m * WL_E + e0, x);
+  load16(a.gamma + e0, gm);
+  load16(a.beta + e0, bt);
+  const float mean = a.mean[m], rstd = a.rstd[m];
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) x1[i] = bf16_round((x[i] - mean) * rstd * gm[i] + bt[i]);
+  load16_bf(a.dx1 + m * a.ldx + e0, dx);
+  // gate: gate = ga (gb c - 1) + 2
+  float z[8];
+  gate_z(a.g, x1, lane, z);
+  const float ga = sigmoidf_(z[0] + z[1] + z[2] + z[3]), gb = sigmoidf_(z[4] + z[5] + z[6] + z[7]);
+  const float c = a.g.gconst[head], dg = a.dgate[m * (WL_E / 64) + head];
+  const float dza = dg * (gb * c - 1.0f) * ga * (1.0f - ga);
+  const float dzb = dg * ga * c * gb * (1.0f - gb);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float dz = j < 4 ? dza : dzb;
+    const float4* w = reinterpret_cast<const float4*>(a.g.wg + j * 64 + part * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 t = w[i];
+      dx[4 * i] += t.x * dz;
+      dx[4 * i + 1] += t.y * dz;
+      dx[4 * i + 2] += t.z * dz;
+      dx[4 * i + 3] += t.w * dz;
+    }
+  }
+  if (kLora) {
+    const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
+    const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
+    float sq_[WL_VPL], sv_[WL_VPL], xq[WL_VPL], xv[WL_VPL], bq[WL_VPL], bv[WL_VPL];
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i) {
+      const uint64_t idx = (uint64_t)m * WL_E + e0 + i;
+      sq_[i] = drop_scale(a.dq, sq, idx);
+      sv_[i] = drop_scale(a.dv, sv, idx);
+      xq[i] = x1[i] * sq_[i];
+      xv[i] = x1[i] * sv_[i];
+      bq[i] = 0.f;
+      bv[i] = 0.f;
+    }
+    store16_bf(a.xd + m * WL_E + e0, xq);
+    store16_bf(a.xd + (a.M + m) * WL_E + e0, xv);
+#pragma unroll
+    for (int k = 0; k < WL_R2; ++k) {
+      const float da = __bfloat162float(a.dx1[m * a.ldx + WL_E + k]);
+      const float* arow = k < WL_R2 / 2 ? a.Aq + (int64_t)k * WL_E : a.Av + (int64_t)(k - WL_R2 / 2) * WL_E;
+      const float4* w = reinterpret_cast<const float4*>(arow + e0);
+      float* acc = k < WL_R2 / 2 ? bq : bv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float4 t = w[i];
+        acc[4 * i] += t.x * da;
+        acc[4 * i + 1] += t.y * da;
+        acc[4 * i + 2] += t.z * da;
+        acc[4 * i + 3] += t.w * da;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i) dx[i] += bq[i] * sq_[i] + bv[i] * sv_[i];
+  }
+  float o[WL_VPL], r[WL_VPL];
+  ln_bwd_row(dx, x, mean, rstd, gm, o);
+  load16(a.dres + m * WL_E + e0, r);
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) o[i] += r[i];
+  store16(a.dh + m * WL_E + e0, o);
+}
+
+// Wext[:, E:E+2r] <- s * B (q rows 0..E-1 columns E..E+r-1, v rows 2E..3E-1 columns E+r..E+2r-1);
+// one launch for every layer. Other rows of those columns stay zero.
+__global__ __launch_bounds__(256) void wl_lora_pack_kernel(int nl, const float* const* bq, const float* const* bv,
+                                                           __hip_bfloat16* const* wext, int64_t ldw, int r,
+                                                           float scale) {
+  const int l = blockIdx.y;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over 2 * E * r
+  if (l >= nl || t >= 2 * (int64_t)WL_E * r) return;
+  const int which = (int)(t / ((int64_t)WL_E * r));
+  const int64_t rem = t % ((int64_t)WL_E * r);
+  const int64_t row = rem / r;
+  const int k = (int)(rem % r);
+  const float* b = which ? bv[l] : bq[l];  // lora_B weight [E, r]
+  const int64_t wrow = which ? 2 * WL_E + row : row;
+  wext[l][wrow * ldw + WL_E + which * r + k] = __float2bfloat16(scale * b[row * r + k]);
+}
+
+}  // namespace rdx
+
+using namespace rdx;
+
+static Drop mk_drop(const int64_t* seed_dev, int salt, float p) {
+  Drop d;
+  d.seed_dev = seed_dev;
+  d.salt = salt;
+  d.thr = (p > 0.f && seed_dev) ? (uint32_t)fminf(4294967295.0f, p * 4294967296.0f) : 0u;
+  d.inv_keep = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  return d;
+}
+
+static int blocks_rows(int64_t M) { return (int)((M + 3) / 4); }
+
+extern "C" {
+
+int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
+                   const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                   int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean, float* rstd, int64_t M, int E,
+                   void* stream) {
+  RDX_REQUIRE(h && gamma && beta && wg && bg && gconst && x1 && gate && mean && rstd && M > 0);
+  const bool lora = lora_aq != nullptr;
+  RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
+  RDX_REQUIRE(ldx % 8 == 0);
+  Ln1Args a{h, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
+            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M};
+  if (lora)
+    hipLaunchKernelGGL(wl_ln1_fwd_kernel<true>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(wl_ln1_fwd_kernel<false>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_add_ln_fwd(const float* h, const void* delta, const int64_t* seed_dev, int salt, float p, float* h2,
+                      const float* gamma, const float* beta, float eps, void* x, float* mean, float* rstd, int64_t M,
+                      int E, void* stream) {
+  RDX_REQUIRE(h && delta && h2 && gamma && beta && x && mean && rstd && M > 0 && E == WL_E);
+  AddLnArgs a{h, reinterpret_cast<const __hip_bfloat16*>(delta), mk_drop(seed_dev, salt, p), h2, gamma, beta, eps,
+              reinterpret_cast<__hip_bfloat16*>(x), mean, rstd, M};
+  hipLaunchKernelGGL(wl_add_ln_fwd_kernel, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_residual(const float* h, const void* delta, const int64_t* seed_dev, int salt, float p, float* out,
+                    int64_t n, void* stream) {
+  RDX_REQUIRE(h && delta && out && n > 0 && n % 8 == 0);
+  hipLaunchKernelGGL(wl_residual_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, as_stream(stream), h,
+                     reinterpret_cast<const __hip_bfloat16*>(delta), mk_drop(seed_dev, salt, p), out, n);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_dropout_bwd(const float* g, const int64_t* seed_dev, int salt, float p, void* out, int64_t n,
+                       void* stream) {
+  RDX_REQUIRE(g && out && n > 0 && n % 8 == 0);
+  hipLaunchKernelGGL(wl_dropout_bwd_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, as_stream(stream), g,
+                     mk_drop(seed_dev, salt, p), reinterpret_cast<__hip_bfloat16*>(out), n);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_gelu(int mode, const void* u, const void* dy, void* out, int64_t n, void* stream) {
+  RDX_REQUIRE(u && out && n > 0 && n % 8 == 0 && (mode == 0 || (mode == 1 && dy)));
+  const auto* U = reinterpret_cast<const __hip_bfloat16*>(u);
+  const auto* DY = reinterpret_cast<const __hip_bfloat16*>(dy);
+  auto* O = reinterpret_cast<__hip_bfloat16*>(out);
+  const dim3 grid((unsigned)((n / 8 + 255) / 256));
+  if (mode == 0)
+    hipLaunchKernelGGL(wl_gelu_kernel<0>, grid, dim3(256), 0, as_stream(stream), U, DY, O, n);
+  else
+    hipLaunchKernelGGL(wl_gelu_kernel<1>, grid, dim3(256), 0, as_stream(stream), U, DY, O, n);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_ln_bwd(const void* dx, int64_t ldd, const float* h, const float* mean, const float* rstd,
+                  const float* gamma, const float* dres, float* dh, const int64_t* seed_dev, int salt, float p,
+                  void* ddrop, int64_t M, int E, void* stream) {
+  RDX_REQUIRE(dx && h && mean && rstd && gamma && dh && M > 0 && E == WL_E && ldd >= E && ldd % 8 == 0);
+  LnBwdArgs a{reinterpret_cast<const __hip_bfloat16*>(dx), ldd, h, mean, rstd, gamma, dres, dh,
+              mk_drop(seed_dev, salt, p), reinterpret_cast<__hip_bfloat16*>(ddrop), M};
+  hipLaunchKernelGGL(wl_ln_bwd_kernel, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
+                   const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                   int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
+                   void* stream) {
+  RDX_REQUIRE(dx1 && dgate && h && mean && rstd && gamma && beta && wg && bg && gconst && dres && dh && M > 0);
+  const bool lora = lora_aq != nullptr;
+  RDX_REQUIRE(E == WL_E && ldx % 8 == 0 && (!lora || (2 * r == WL_R2 && lora_av && xd && ldx >= E + 2 * r)));
+  Ln1BwdArgs a{reinterpret_cast<const __hip_bfloat16*>(dx1), ldx, dgate, h, mean, rstd, gamma, beta,
+               GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
+               dres, dh, reinterpret_cast<__hip_bfloat16*>(xd), M};
+  if (lora)
+    hipLaunchKernelGGL(wl_ln1_bwd_kernel<true>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(wl_ln1_bwd_kernel<false>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_lora_pack(int nl, const float* const* bq, const float* const* bv, void* const* wext, int64_t ldw, int r,
+                     float scale, int E, void* stream) {
+  RDX_REQUIRE(nl > 0 && bq && bv && wext && E == WL_E && r > 0 && ldw >= E + 2 * r);
+  const int64_t n = 2 * (int64_t)E * r;
+  hipLaunchKernelGGL(wl_lora_pack_kernel, dim3((unsigned)((n + 255) / 256), nl), dim3(256), 0, as_stream(stream), nl,
+                     bq, bv, reinterpret_cast<__hip_bfloat16* const*>(wext), ldw, r, scale);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

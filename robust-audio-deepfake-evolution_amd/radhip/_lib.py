@@ -91,6 +91,23 @@ SIGNATURES = {
                              c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int,
                              c_int, c_vp]),
     "rdx_attn_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_vp]),
+    "rdx_wl_ln1_fwd": (c_int, [c_vp] * 3 + [c_f32] + [c_vp] * 5 + [c_int, c_vp,
+                       c_int, c_int, c_f32, c_vp, c_i64] + [c_vp] * 3
+                       + [c_i64, c_int, c_vp]),
+    "rdx_wl_add_ln_fwd": (c_int, [c_vp, c_vp, c_vp, c_int, c_f32, c_vp, c_vp,
+                          c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_int,
+                          c_vp]),
+    "rdx_wl_residual": (c_int, [c_vp, c_vp, c_vp, c_int, c_f32, c_vp, c_i64,
+                        c_vp]),
+    "rdx_wl_dropout_bwd": (c_int, [c_vp, c_vp, c_int, c_f32, c_vp, c_i64,
+                           c_vp]),
+    "rdx_wl_gelu": (c_int, [c_int, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rdx_wl_ln_bwd": (c_int, [c_vp, c_i64] + [c_vp] * 7 + [c_int, c_f32, c_vp,
+                      c_i64, c_int, c_vp]),
+    "rdx_wl_ln1_bwd": (c_int, [c_vp, c_i64] + [c_vp] * 11 + [c_int, c_vp, c_int,
+                       c_int, c_f32, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "rdx_wl_lora_pack": (c_int, [c_int, c_vp, c_vp, c_vp, c_i64, c_int,
+                         c_f32, c_int, c_vp]),
     "rdx_timestamp_acc": (c_int, [c_vp, c_int, c_vp]),
     "rdx_wallclock_khz": (c_int, [c_int]),
     "rdx_fgm_attack": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),

@@ -630,6 +630,9 @@ class GraphedMicroStep:
             self._restore()
         torch.cuda.synchronize(tr.device)
         self._unbind()
+        # the graphs hold the "store"/"use" branches; eager calls (eval, tools) must recompute the CNN.
+        # The stored feature tensor stays referenced: graph 1 reads it on every replay.
+        tr.cnn_reuse(None)
         tr.grads.zero()
         tr.loss_sum.copy_(saved_loss)
         self.graphs = gs

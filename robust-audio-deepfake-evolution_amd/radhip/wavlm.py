@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import wavlm_fused
 from .ops import GatedAttention
 
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
@@ -372,15 +373,30 @@ class Encoder(nn.Module):
         h = self.dropout(h)
         states = []
         pos = None
-        if self.training and self.cfg.attention_dropout > 0 and h.is_cuda:
+        seed = None
+        if self.training and h.is_cuda:
             self._attn_rng.add_(1)
             seed = self._attn_rng.clone()          # the value this forward (and its backward) uses
             for i, layer in enumerate(self.layers):
                 layer.attention._seed, layer.attention._salt = seed, i
+        fused = wavlm_fused.eligible(self, h)
+        if fused:
+            # fused bf16 layers (radhip/wavlm_fused.py) on an fp32 residual stream
+            runner = self.__dict__.get("_fused")
+            if runner is None:
+                runner = self.__dict__["_fused"] = wavlm_fused.FusedEncoderRunner(self)
+            loras = runner.prepare(h.device)
+            pb = runner.position_bias(h.shape[1], h.device)
+            h = h.float()
+
+        def run(i, layer, h, pos):
+            if fused:
+                return runner.layer(i, h, pb, loras, seed), None
+            return layer(h, pos)
         for i, layer in enumerate(self.layers):
             states.append(h)
             if self.training and self.keep_dev is not None and i > 0:
-                hn, pos = layer(h, pos)
+                hn, pos = run(i, layer, h, pos)
                 h = torch.where(self.keep_dev[i], hn, h)
                 continue
             # HF draws torch.rand([]) for EVERY layer (train or eval) and skips when training, i > 0 and
@@ -388,7 +404,7 @@ class Encoder(nn.Module):
             r = float(torch.rand([])) if self.keep_dev is None else 1.0
             skip = self.training and i > 0 and p > 0 and r < p
             if not skip:
-                h, pos = layer(h, pos)
+                h, pos = run(i, layer, h, pos)
         if self.stable:
             h = self.layer_norm(h)
         states.append(h)

@@ -1,0 +1,284 @@
+"""Fused WavLM encoder layer for the bf16 training/eval step (csrc/wavlm_layer.hip + attention.hip).
+
+One autograd Function per layer replaces the ~44 forward / ~100 backward framework kernels of the
+module-by-module layer (casts, LN, gate MLP, LoRA GEMMs, dropouts, residual adds) with 9 forward and
+13 backward launches: four hipBLASLt GEMMs (q/k/v with the LoRA update folded in as 16 extra K
+columns, out_proj, FFN1, FFN2), the MFMA gated-bias attention, and wave-per-row fused kernels for
+LN1 + gate + LoRA-A, dropout + residual + LN2, GELU, and their backwards. Same math as the
+reference layer (HF WavLMEncoderLayerStableLayerNorm + peft LoRA q/v; DualStreamSEMamba.py:292-439,
+main.py:103-158); dropout masks come from the device-seeded counter hash (graph replayable).
+
+Used when: CUDA, bf16 autocast, stable layer norm, E = 1024 with 64-dim heads, GELU FFN, a frozen
+base layer, and either no LoRA or LoRA r = 8 on exactly q_proj and v_proj. Anything else takes the
+module path (radhip/wavlm.py), which is what the fp32 parity tests exercise.
+RADHIP_FUSED_WAVLM=0 disables the fused layer (A/B measurement).
+"""
+import ctypes
+import os
+
+import torch
+import torch.nn.functional as F
+
+from ._lib import check, lib
+from .ops import _p, _stream, _timed
+
+E_FUSED = 1024
+
+
+def _off(t, elems):
+    """Device address of element `elems` of t (a column offset into a row-major GEMM output)."""
+    return ctypes.c_void_p(t.data_ptr() + elems * t.element_size())
+SALT_BASE = 4096
+
+
+def enabled():
+    return os.environ.get("RADHIP_FUSED_WAVLM", "1") != "0"
+
+
+def _lora_parts(attn):
+    from .wavlm import LoraLinear
+    q, k, v, o = attn.q_proj, attn.k_proj, attn.v_proj, attn.out_proj
+    if isinstance(k, LoraLinear) or isinstance(o, LoraLinear):
+        return "unsupported"
+    if isinstance(q, LoraLinear) != isinstance(v, LoraLinear):
+        return "unsupported"
+    if not isinstance(q, LoraLinear):
+        return None
+    r = q.r[q.adapter]
+    if r != 8 or v.r[v.adapter] != 8 or q.scaling[q.adapter] != v.scaling[v.adapter]:
+        return "unsupported"
+    return q, v
+
+
+def eligible(encoder, h):
+    cfg = encoder.cfg
+    if not (enabled() and h.is_cuda and encoder.stable and cfg.hidden_size == E_FUSED
+            and cfg.hidden_size // cfg.num_attention_heads == 64 and cfg.hidden_act == "gelu"):
+        return False
+    if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    st = encoder.__dict__.get("_fused_ok")
+    if st is not None and st[0] == _trainable_signature(encoder):
+        return st[1]
+    ok = True
+    for layer in encoder.layers:
+        lp = _lora_parts(layer.attention)
+        if lp == "unsupported":
+            ok = False
+            break
+        lora_params = set()
+        if lp is not None:
+            for ad in lp:
+                lora_params |= {id(p) for p in ad.lora_A.parameters()} | {id(p) for p in ad.lora_B.parameters()}
+        if any(p.requires_grad and id(p) not in lora_params for p in layer.parameters()):
+            ok = False
+            break
+    encoder.__dict__["_fused_ok"] = (_trainable_signature(encoder), ok)
+    return ok
+
+
+def _trainable_signature(encoder):
+    return tuple(p.requires_grad for p in encoder.parameters())
+
+
+class _LayerCache:
+    """bf16 copies of a frozen layer's weights (rebuilt when a source tensor changes) and the
+    [3E, E + 2r] q/k/v operand whose last 2r columns receive s * lora_B every forward."""
+
+    def __init__(self):
+        self.key = None
+
+    def refresh(self, layer, lora):
+        a, ff = layer.attention, layer.feed_forward
+        from .wavlm import _base
+        bq, bk, bv = _base(a.q_proj), _base(a.k_proj), _base(a.v_proj)
+        src = [bq.weight, bk.weight, bv.weight, bq.bias, bk.bias, bv.bias, a.out_proj.weight, a.out_proj.bias,
+               ff.intermediate_dense.weight, ff.intermediate_dense.bias, ff.output_dense.weight,
+               ff.output_dense.bias]
+        key = (lora is not None,) + tuple((t.data_ptr(), t._version) for t in src)
+        if key == self.key:
+            return
+        E = bq.weight.shape[0]
+        r2 = 16 if lora is not None else 0
+        with torch.no_grad():
+            w = torch.zeros(3 * E, E + r2, device=bq.weight.device, dtype=torch.bfloat16)
+            w[:, :E] = torch.cat([bq.weight, bk.weight, bv.weight]).to(torch.bfloat16)
+            self.wext = w
+            self.bqkv = torch.cat([bq.bias, bk.bias, bv.bias]).to(torch.bfloat16)
+            self.wo = a.out_proj.weight.to(torch.bfloat16)
+            self.bo = a.out_proj.bias.to(torch.bfloat16)
+            self.w1 = ff.intermediate_dense.weight.to(torch.bfloat16)
+            self.b1 = ff.intermediate_dense.bias.to(torch.bfloat16)
+            self.w2 = ff.output_dense.weight.to(torch.bfloat16)
+            self.b2 = ff.output_dense.bias.to(torch.bfloat16)
+            self.wg = a.gru_rel_pos_linear.weight.detach().float().contiguous()
+            self.bg = a.gru_rel_pos_linear.bias.detach().float().contiguous()
+            self.gconst = a.gru_rel_pos_const.detach().float().reshape(-1).contiguous()
+        self.key = key
+
+
+class WavLMLayerFn(torch.autograd.Function):
+    """h_out = layer(h) for one stable-LN WavLM layer; inputs h fp32 [B, T, E] and the LoRA factors
+    (lora_A q, lora_B q, lora_A v, lora_B v, fp32 leaves, or None)."""
+
+    @staticmethod
+    def forward(ctx, h, aq, bq, av, bv, layer, cache, pb, seed, index, p_hidden, p_attn, p_lora, scale):
+        B, T, E = h.shape
+        H = E // 64
+        M = B * T
+        dev = h.device
+        lora = aq is not None
+        r2 = 16 if lora else 0
+        ldx = E + r2
+        hf = h.contiguous().view(M, E)
+        st = _stream(hf)
+        ln1, ln2 = layer.layer_norm, layer.final_layer_norm
+        sd = seed if seed is not None else None
+        sdp = _p(sd) if sd is not None else None
+        salt = SALT_BASE + 8 * index
+        x1 = torch.empty(M, ldx, device=dev, dtype=torch.bfloat16)
+        gate = torch.empty(M, H, device=dev, dtype=torch.float32)
+        mean1 = torch.empty(M, device=dev, dtype=torch.float32)
+        rstd1 = torch.empty_like(mean1)
+        with _timed("wl_ln1_fwd", hf, float(M * E * 4 + M * ldx * 2)):
+            check(lib().rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg),
+                                       _p(cache.gconst), _p(aq) if lora else None, _p(av) if lora else None, 8,
+                                       sdp, salt + 3, salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1),
+                                       _p(rstd1), M, E, st), "wl_ln1_fwd")
+        qkv = F.linear(x1, cache.wext, cache.bqkv)                          # [M, 3E] (LoRA folded in)
+        o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, T, device=dev, dtype=torch.float32)
+        zseed = sd if sd is not None else torch.zeros(1, dtype=torch.int64, device=dev)
+        with _timed("attn_fwd", hf, 2.0 * 2 * B * H * T * T * 64):
+            check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(pb),
+                                     _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse), B, T, H, 64, st),
+                  "attn_fwd")
+        aout = F.linear(o, cache.wo, cache.bo)
+        h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
+        x2 = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        mean2 = torch.empty_like(mean1)
+        rstd2 = torch.empty_like(mean1)
+        check(lib().rdx_wl_add_ln_fwd(_p(hf), _p(aout), sdp, salt + 1, float(p_hidden), _p(h2), _p(ln2.weight),
+                                      _p(ln2.bias), float(ln2.eps), _p(x2), _p(mean2), _p(rstd2), M, E, st),
+              "wl_add_ln_fwd")
+        u = F.linear(x2, cache.w1, cache.b1)
+        v = torch.empty_like(u)
+        check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
+        fo = F.linear(v, cache.w2, cache.b2)
+        out = torch.empty(M, E, device=dev, dtype=torch.float32)
+        check(lib().rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st), "wl_residual")
+        ctx.save_for_backward(hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, pb, aq, av)
+        ctx.layer, ctx.cache = layer, cache
+        ctx.meta = (B, T, E, H, index, float(p_hidden), float(p_attn), float(p_lora), float(scale), lora,
+                    sd is not None)
+        return out.view(B, T, E)
+
+    @staticmethod
+    def backward(ctx, dout):
+        hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, pb, aq, av = ctx.saved_tensors
+        B, T, E, H, index, p_hidden, p_attn, p_lora, scale, lora, has_seed = ctx.meta
+        layer, cache = ctx.layer, ctx.cache
+        M = B * T
+        dev = hf.device
+        st = _stream(hf)
+        sdp = _p(zseed) if has_seed else None
+        salt = SALT_BASE + 8 * index
+        ldx = x1.shape[1]
+        g = dout.contiguous().view(M, E).float()
+        dfo = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        check(lib().rdx_wl_dropout_bwd(_p(g), sdp, salt + 2, p_hidden, _p(dfo), M * E, st), "wl_dropout_bwd")
+        dv = torch.mm(dfo, cache.w2)
+        du = torch.empty_like(u)
+        check(lib().rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
+        dx2 = torch.mm(du, cache.w1)
+        dh2 = torch.empty(M, E, device=dev, dtype=torch.float32)
+        daout = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        ln1, ln2 = layer.layer_norm, layer.final_layer_norm
+        check(lib().rdx_wl_ln_bwd(_p(dx2), E, _p(h2), _p(mean2), _p(rstd2), _p(ln2.weight), _p(g), _p(dh2), sdp,
+                                  salt + 1, p_hidden, _p(daout), M, E, st), "wl_ln_bwd")
+        do = torch.mm(daout, cache.wo)
+        D = torch.empty(B, H, T, device=dev, dtype=torch.float32)
+        dqkv = torch.empty(M, 3 * E, device=dev, dtype=torch.bfloat16)
+        dgate = torch.empty(M, H, device=dev, dtype=torch.float32)
+        with _timed("attn_bwd", hf, 2.0 * 5 * B * H * T * T * 64):
+            check(lib().rdx_attn_bwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(pb),
+                                     _p(zseed), int(index), p_attn, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D),
+                                     _p(dqkv), _off(dqkv, E), _off(dqkv, 2 * E), 3 * E, _p(dgate), B, T, H, 64, st),
+                  "attn_bwd")
+        dx1 = torch.mm(dqkv, cache.wext)                                     # [M, E + 2r]
+        dh = torch.empty(M, E, device=dev, dtype=torch.float32)
+        xd = torch.empty(2, M, E, device=dev, dtype=torch.bfloat16) if lora else None
+        check(lib().rdx_wl_ln1_bwd(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
+                                   _p(ln1.bias), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
+                                   _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3, salt + 4,
+                                   p_lora, _p(dh2), _p(dh), _p(xd) if lora else None, M, E, st), "wl_ln1_bwd")
+        daq = dbq = dav = dbv = None
+        if lora:
+            r = 8
+            dbq = torch.mm(dqkv[:, :E].t(), x1[:, E:E + r]).float().mul_(scale)        # [E, r]
+            dbv = torch.mm(dqkv[:, 2 * E:].t(), x1[:, E + r:E + 2 * r]).float().mul_(scale)
+            daq = torch.mm(dx1[:, E:E + r].t(), xd[0]).float()                         # [r, E]
+            dav = torch.mm(dx1[:, E + r:E + 2 * r].t(), xd[1]).float()
+        return (dh.view(B, T, E), daq, dbq, dav, dbv) + (None,) * 9
+
+
+class FusedEncoderRunner:
+    """Per-Encoder state of the fused path: weight caches, the LoRA-B pack tables, the position bias."""
+
+    def __init__(self, encoder):
+        self.encoder = encoder
+        self.caches = [_LayerCache() for _ in encoder.layers]
+        self.pack_key = None
+        self.pb_key = None
+
+    def position_bias(self, T, device):
+        emb = self.encoder.layers[0].attention.rel_attn_embed.weight
+        key = (T, emb.data_ptr(), emb._version)
+        if key != self.pb_key:
+            with torch.no_grad():
+                self.pb = self.encoder.layers[0].attention.compute_bias(T, device).float().contiguous()
+            self.pb_key = key
+        return self.pb
+
+    def prepare(self, device):
+        loras = [_lora_parts(layer.attention) for layer in self.encoder.layers]
+        for layer, cache, lp in zip(self.encoder.layers, self.caches, loras):
+            cache.refresh(layer, lp)
+        if loras[0] is None:
+            return loras
+        key = tuple(c.wext.data_ptr() for c in self.caches) + tuple(
+            lp[i].lora_B[lp[i].adapter].weight.data_ptr() for lp in loras for i in (0, 1))
+        if key != self.pack_key:
+            bq = [lp[0].lora_B[lp[0].adapter].weight for lp in loras]
+            bv = [lp[1].lora_B[lp[1].adapter].weight for lp in loras]
+            self.tab = torch.tensor([[t.data_ptr() for t in bq], [t.data_ptr() for t in bv],
+                                     [c.wext.data_ptr() for c in self.caches]], dtype=torch.int64).to(device)
+            self.pack_key = key
+        lp0 = loras[0][0]
+        n = len(self.caches)
+        check(lib().rdx_wl_lora_pack(n, self.tab[0].data_ptr(), self.tab[1].data_ptr(), self.tab[2].data_ptr(),
+                                     self.caches[0].wext.shape[1], 8, float(lp0.scaling[lp0.adapter]), E_FUSED,
+                                     _stream(self.tab)), "wl_lora_pack")
+        return loras
+
+    def layer(self, i, h, pb, loras, seed):
+        layer = self.encoder.layers[i]
+        cfg = self.encoder.cfg
+        tr = layer.training
+        lp = loras[i]
+        p_hidden = cfg.hidden_dropout if tr else 0.0
+        p_attn = layer.attention.dropout if tr else 0.0
+        if lp is None:
+            aq = bq = av = bv = None
+            p_lora, scale = 0.0, 1.0
+        else:
+            q, v = lp
+            aq, bq = q.lora_A[q.adapter].weight, q.lora_B[q.adapter].weight
+            av, bv = v.lora_A[v.adapter].weight, v.lora_B[v.adapter].weight
+            dp = q.lora_dropout[q.adapter]
+            p_lora = float(getattr(dp, "p", 0.0)) if tr else 0.0
+            scale = float(q.scaling[q.adapter])
+        if (p_hidden > 0 or p_attn > 0 or p_lora > 0) and seed is None:
+            raise RuntimeError("fused WavLM layer: dropout needs the encoder's device seed")
+        return WavLMLayerFn.apply(h, aq, bq, av, bv, layer, self.caches[i], pb, seed, i, p_hidden, p_attn, p_lora,
+                                  scale)

@@ -89,7 +89,7 @@ def test_cli_train_eval_and_2021(tmp_path, golden):
     cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--seed", "1234"]))
     tag = out / "LA_Tiny_ep1_bs2"
     for f in ("config.conf", "metric_log.txt", "eval_scores.txt", "t-DCF_EER.txt", "metrics/dev_score.txt",
-              "metrics/dev_t-DCF_EER_0epo.txt", "weights/best.pth", "weights/swa.pth",
+              "weights/best.pth", "weights/swa.pth",
               "weights/checkpoint_epoch_000.pth"):
         assert (tag / f).exists(), f
     assert len(list((tag / "weights").glob("epoch_0_*.pth"))) == 1
