@@ -244,7 +244,10 @@ int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8
  * rdx_wl_gelu: mode 0 out = gelu(u) (erf form); mode 1 out = dy * gelu'(u).
  * rdx_wl_ln_bwd: dh = dres + LN_bwd(dx) (dres nullable); ddrop = drop(dh) bf16 when non-null.
  * rdx_wl_ln1_bwd: dx1 = dX1[:, :E] + gate and LoRA-A backward terms, dh = dres + LN1_bwd(dx1); with LoRA
- *   also xd [2, M, E] bf16 = the dropped x1 of each adapter (operand of the d lora_A GEMMs).
+ *   also (xd non-null) xd [2, M, E] bf16 = the dropped x1 of each adapter.
+ * rdx_wl_lora_grad: LoRA weight gradients ACCUMULATED into fp32 daq/dav [r, E] and dbq/dbv [E, r]:
+ *   dB += scale * d{q,v}^T a_{q,v}, dA += d a_{q,v}^T drop(x1) (dqkv [M, ldq] bf16, x1/dx1 [M, ld] bf16 with
+ *   a / d a in columns E..E+2r).
  * rdx_wl_lora_pack: for every layer l, wext[l] [3E, ldw] bf16 columns E..E+2r <- scale * lora_B
  *   (q rows 0..E-1, v rows 2E..3E-1); bq, bv, wext are DEVICE arrays of nl pointers. */
 int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float eps, const float* wg,
@@ -267,6 +270,9 @@ int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float
                    const float* gconst, const float* lora_aq, const float* lora_av, int r,
                    const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
                    void* stream);
+int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx, const void* dx1, int64_t ldd,
+                     const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, float scale, float* daq,
+                     float* dbq, float* dav, float* dbv, int64_t M, int E, int r, void* stream);
 int rdx_wl_lora_pack(int nl, const float* const* bq, const float* const* bv, void* const* wext, int64_t ldw,
                      int r, float scale, int E, void* stream);
 

@@ -30,6 +30,16 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 constexpr int AT_DH = 64;    // head dim
 constexpr int AT_TILE = 32;  // rows per wave
 constexpr int AT_LDP = AT_TILE + 4;  // padded LDS row (bf16) for transposed tiles
+// waves per block splitting the inner (key or query) loop of each kernel
+#ifndef AT_NS_FWD
+#define AT_NS_FWD 4
+#endif
+#ifndef AT_NS_DKDV
+#define AT_NS_DKDV 2
+#endif
+#ifndef AT_NS_DQ
+#define AT_NS_DQ 4
+#endif
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -91,11 +101,18 @@ struct AttnArgs {
   int B, T, H;
 };
 
-template <bool kDrop>
-__global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16* __restrict__ o, int64_t ldo,
-                                                      float* __restrict__ lse) {
-  __shared__ __bf16 s_vt[AT_DH][AT_LDP];
-  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+// NS waves per block share one 32-query tile and split its key tiles (wave w takes kb = w, w + NS,
+// ...); their online-softmax partials (m, l, O) are merged through LDS at the end. This multiplies the
+// waves in flight by NS (T = 201 gives only 7 query tiles per (b, h)).
+template <bool kDrop, int NS>
+__global__ __launch_bounds__(64 * NS) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16* __restrict__ o, int64_t ldo,
+                                                           float* __restrict__ lse) {
+  __shared__ __bf16 s_vt_all[NS][AT_DH][AT_LDP];
+  __shared__ float s_m[AT_TILE], s_l[AT_TILE];
+  __shared__ float s_o[2][16][64];
+  const int w = threadIdx.x >> 6;
+  __bf16 (*s_vt)[AT_LDP] = s_vt_all[w];
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int qb = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int T = a.T, H = a.H;
   const int qi = qb * AT_TILE + r;
@@ -112,7 +129,9 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16
   float m = -INFINITY, l = 0.f;
   f32x16 oacc[2] = {zero16(), zero16()};
   const int nkb = (T + AT_TILE - 1) / AT_TILE;
-  for (int kb = 0; kb < nkb; ++kb) {
+  const int niter = (nkb + NS - 1) / NS;  // equal trip counts keep the barriers uniform
+  for (int it = 0; it < niter; ++it) {
+    const int kb = w + NS * it;
     const int kr = kb * AT_TILE + r;
     const bool kvalid = kr < T;
     f32x16 sacc = zero16();
@@ -136,11 +155,11 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float mnew = fmaxf(m, mloc);
-    const float alpha = __expf(m - mnew);
+    const float alpha = mnew == -INFINITY ? 1.f : __expf(m - mnew);
     float lsum = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = __expf(sv[i] - mnew);
+      const float p = sv[i] == -INFINITY ? 0.f : __expf(sv[i] - mnew);
       lsum += p;
       if (kDrop) {
         const int key = kb * AT_TILE + crow(i, hh);
@@ -166,7 +185,35 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16
     }
     __syncthreads();
   }
-  if (qvalid) {
+  // merge the NS partials into wave 0
+  for (int src = 1; src < NS; ++src) {
+    __syncthreads();
+    if (w == src) {
+      if (hh == 0) {
+        s_m[r] = m;
+        s_l[r] = l;
+      }
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s_o[db][i][lane] = oacc[db][i];
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float mw = s_m[r], lw = s_l[r];
+      if (mw != -INFINITY) {
+        const float mnew = fmaxf(m, mw);
+        const float a0 = __expf(m - mnew), a1 = __expf(mw - mnew);
+        l = l * a0 + lw * a1;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[db][i] = oacc[db][i] * a0 + s_o[db][i][lane] * a1;
+        m = mnew;
+      }
+    }
+  }
+  if (w == 0 && qvalid) {
     const float inv = 1.f / l;
     __hip_bfloat16* orow = o + ((int64_t)b * T + qi) * ldo + col0;
 #pragma unroll
@@ -206,12 +253,19 @@ struct AttnBwdArgs {
   const float* D;    // [B, H, T]
 };
 
-template <bool kDrop>
-__global__ __launch_bounds__(64) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdArgs g, __hip_bfloat16* __restrict__ dk,
-                                                           __hip_bfloat16* __restrict__ dv, int64_t ldg) {
-  __shared__ __bf16 s_qt[AT_DH][AT_LDP];
-  __shared__ __bf16 s_dot[AT_DH][AT_LDP];
-  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+// NS waves per block share one 32-key tile and split its query tiles; dK/dV partials are summed
+// through LDS at the end.
+template <bool kDrop, int NS>
+__global__ __launch_bounds__(64 * NS) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdArgs g,
+                                                                __hip_bfloat16* __restrict__ dk,
+                                                                __hip_bfloat16* __restrict__ dv, int64_t ldg) {
+  __shared__ __bf16 s_qt_all[NS][AT_DH][AT_LDP];
+  __shared__ __bf16 s_dot_all[NS][AT_DH][AT_LDP];
+  __shared__ float s_acc[4][16][64];
+  const int w = threadIdx.x >> 6;
+  __bf16 (*s_qt)[AT_LDP] = s_qt_all[w];
+  __bf16 (*s_dot)[AT_LDP] = s_dot_all[w];
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int kb = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int T = a.T, H = a.H;
   const int key = kb * AT_TILE + r;  // this lane's key column
@@ -227,7 +281,9 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdAr
   const int64_t bh = (int64_t)b * H + head;
   f32x16 dkacc[2] = {zero16(), zero16()}, dvacc[2] = {zero16(), zero16()};
   const int nqb = (T + AT_TILE - 1) / AT_TILE;
-  for (int qb = 0; qb < nqb; ++qb) {
+  const int niter = (nqb + NS - 1) / NS;
+  for (int it = 0; it < niter; ++it) {
+    const int qb = w + NS * it;
     const int qr = qb * AT_TILE + r;  // row loaded by this lane for the A fragments
     const bool qrv = qr < T;
     bf16x8 qa[4], da[4];
@@ -270,6 +326,29 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdAr
     }
     __syncthreads();
   }
+  for (int src = 1; src < NS; ++src) {
+    __syncthreads();
+    if (w == src) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s_acc[0][i][lane] = dkacc[0][i];
+        s_acc[1][i][lane] = dkacc[1][i];
+        s_acc[2][i][lane] = dvacc[0][i];
+        s_acc[3][i][lane] = dvacc[1][i];
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        dkacc[0][i] += s_acc[0][i][lane];
+        dkacc[1][i] += s_acc[1][i][lane];
+        dvacc[0][i] += s_acc[2][i][lane];
+        dvacc[1][i] += s_acc[3][i][lane];
+      }
+    }
+  }
+  if (w != 0) return;
   // Z[key][d]: col = d (lane), row = key (registers)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -285,11 +364,18 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdAr
   }
 }
 
-template <bool kDrop>
-__global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs g, __hip_bfloat16* __restrict__ dq,
-                                                         int64_t ldg, float* __restrict__ dgate) {
-  __shared__ __bf16 s_kt[AT_DH][AT_LDP];
-  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+// NS waves per block share one 32-query tile and split its key tiles; dQ / dgate partials are
+// summed through LDS at the end.
+template <bool kDrop, int NS>
+__global__ __launch_bounds__(64 * NS) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs g,
+                                                              __hip_bfloat16* __restrict__ dq, int64_t ldg,
+                                                              float* __restrict__ dgate) {
+  __shared__ __bf16 s_kt_all[NS][AT_DH][AT_LDP];
+  __shared__ float s_acc[2][16][64];
+  __shared__ float s_dg[64];
+  const int w = threadIdx.x >> 6;
+  __bf16 (*s_kt)[AT_LDP] = s_kt_all[w];
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int qb = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int T = a.T, H = a.H;
   const int qi = qb * AT_TILE + r;
@@ -312,7 +398,9 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs
   f32x16 dqacc[2] = {zero16(), zero16()};
   float dg = 0.f;
   const int nkb = (T + AT_TILE - 1) / AT_TILE;
-  for (int kb = 0; kb < nkb; ++kb) {
+  const int niter = (nkb + NS - 1) / NS;
+  for (int it = 0; it < niter; ++it) {
+    const int kb = w + NS * it;
     const int kr = kb * AT_TILE + r;
     const bool krv = kr < T;
     bf16x8 kfr[4];
@@ -349,6 +437,27 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs
     }
     __syncthreads();
   }
+  for (int src = 1; src < NS; ++src) {
+    __syncthreads();
+    if (w == src) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s_acc[0][i][lane] = dqacc[0][i];
+        s_acc[1][i][lane] = dqacc[1][i];
+      }
+      s_dg[lane] = dg;
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        dqacc[0][i] += s_acc[0][i][lane];
+        dqacc[1][i] += s_acc[1][i][lane];
+      }
+      dg += s_dg[lane];
+    }
+  }
+  if (w != 0) return;
   dg += __shfl_xor(dg, 32, 64);
   if (qvalid) {
     __hip_bfloat16* row = dq + ((int64_t)b * T + qi) * ldg + col0;
@@ -412,9 +521,11 @@ extern "C" int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t l
   const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, pos_bias, seed_dev, salt, p_drop, scale, B, T, H);
   dim3 grid((T + AT_TILE - 1) / AT_TILE, H, B);
   if (a.thr)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(64), 0, as_stream(stream), a, (__hip_bfloat16*)o, ldo, lse);
+    hipLaunchKernelGGL((attn_fwd_kernel<true, AT_NS_FWD>), grid, dim3(64 * AT_NS_FWD), 0, as_stream(stream), a,
+                       (__hip_bfloat16*)o, ldo, lse);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(64), 0, as_stream(stream), a, (__hip_bfloat16*)o, ldo, lse);
+    hipLaunchKernelGGL((attn_fwd_kernel<false, AT_NS_FWD>), grid, dim3(64 * AT_NS_FWD), 0, as_stream(stream), a,
+                       (__hip_bfloat16*)o, ldo, lse);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -437,13 +548,15 @@ extern "C" int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
   AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
   dim3 grid((T + AT_TILE - 1) / AT_TILE, H, B);
   if (a.thr) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(64), 0, st, a, g, (__hip_bfloat16*)dk,
-                       (__hip_bfloat16*)dv, ldg);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(64), 0, st, a, g, (__hip_bfloat16*)dq, ldg, dgate);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, AT_NS_DKDV>), grid, dim3(64 * AT_NS_DKDV), 0, st, a, g,
+                       (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<true, AT_NS_DQ>), grid, dim3(64 * AT_NS_DQ), 0, st, a, g,
+                       (__hip_bfloat16*)dq, ldg, dgate);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(64), 0, st, a, g, (__hip_bfloat16*)dk,
-                       (__hip_bfloat16*)dv, ldg);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(64), 0, st, a, g, (__hip_bfloat16*)dq, ldg, dgate);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, AT_NS_DKDV>), grid, dim3(64 * AT_NS_DKDV), 0, st, a, g,
+                       (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<false, AT_NS_DQ>), grid, dim3(64 * AT_NS_DQ), 0, st, a, g,
+                       (__hip_bfloat16*)dq, ldg, dgate);
   }
   RDX_LAUNCH_CHECK();
   return RDX_OK;

@@ -460,8 +460,10 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
       bq[i] = 0.f;
       bv[i] = 0.f;
     }
-    store16_bf(a.xd + m * WL_E + e0, xq);
-    store16_bf(a.xd + (a.M + m) * WL_E + e0, xv);
+    if (a.xd) {
+      store16_bf(a.xd + m * WL_E + e0, xq);
+      store16_bf(a.xd + (a.M + m) * WL_E + e0, xv);
+    }
 #pragma unroll
     for (int k = 0; k < WL_R2; ++k) {
       const float da = __bfloat162float(a.dx1[m * a.ldx + WL_E + k]);
@@ -486,6 +488,68 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
 #pragma unroll
   for (int i = 0; i < WL_VPL; ++i) o[i] += r[i];
   store16(a.dh + m * WL_E + e0, o);
+}
+
+// LoRA weight gradients of one layer, ACCUMULATED into the fp32 .grad buffers:
+//   dB_q[e, k] += s sum_m dq[m, e] a_q[m, k]        dA_q[k, e] += sum_m da_q[m, k] drop_q(x1)[m, e]
+// (same for v). Thread = one column e; a block walks WL_LG_ROWS rows, staging the rows' 32 per-row
+// factors (a_q, a_v, da_q, da_v) in LDS, then adds its 32 partial sums with fp32 atomics.
+constexpr int WL_LG_ROWS = 96;
+
+struct LoraGradArgs {
+  const __hip_bfloat16* dqkv;  // [M, ldq]: dq at column 0, dv at column 2E
+  int64_t ldq;
+  const __hip_bfloat16* x1;    // [M, ldx]: x1 in [0, E), a in [E, E + 2r)
+  int64_t ldx;
+  const __hip_bfloat16* dx1;   // [M, ldd]: d a in [E, E + 2r)
+  int64_t ldd;
+  Drop dq, dv;
+  float scale;
+  float *dAq, *dBq, *dAv, *dBv;
+  int64_t M;
+};
+
+__global__ __launch_bounds__(256) void wl_lora_grad_kernel(LoraGradArgs a) {
+  __shared__ float s_row[WL_LG_ROWS][WL_R2 * 2];
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.y * WL_LG_ROWS;
+  const int nrow = (int)min((int64_t)WL_LG_ROWS, a.M - m0);
+  for (int t = threadIdx.x; t < nrow * 2 * WL_R2; t += 256) {
+    const int rr = t / (2 * WL_R2), c = t % (2 * WL_R2);
+    const int64_t m = m0 + rr;
+    s_row[rr][c] = c < WL_R2 ? __bfloat162float(a.x1[m * a.ldx + WL_E + c])
+                             : __bfloat162float(a.dx1[m * a.ldd + WL_E + c - WL_R2]);
+  }
+  __syncthreads();
+  constexpr int R = WL_R2 / 2;
+  float bq[R], bv[R], aq[R], av[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) bq[k] = bv[k] = aq[k] = av[k] = 0.f;
+  const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
+  const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
+  for (int rr = 0; rr < nrow; ++rr) {
+    const int64_t m = m0 + rr;
+    const float gq = __bfloat162float(a.dqkv[m * a.ldq + e]);
+    const float gv = __bfloat162float(a.dqkv[m * a.ldq + 2 * WL_E + e]);
+    const float x = __bfloat162float(a.x1[m * a.ldx + e]);
+    const uint64_t idx = (uint64_t)m * WL_E + e;
+    const float xq = x * drop_scale(a.dq, sq, idx), xv = x * drop_scale(a.dv, sv, idx);
+    const float* f = s_row[rr];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      bq[k] = fmaf(gq, f[k], bq[k]);
+      bv[k] = fmaf(gv, f[R + k], bv[k]);
+      aq[k] = fmaf(f[2 * R + k], xq, aq[k]);
+      av[k] = fmaf(f[3 * R + k], xv, av[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    atomicAdd(a.dBq + (int64_t)e * R + k, a.scale * bq[k]);
+    atomicAdd(a.dBv + (int64_t)e * R + k, a.scale * bv[k]);
+    atomicAdd(a.dAq + (int64_t)k * WL_E + e, aq[k]);
+    atomicAdd(a.dAv + (int64_t)k * WL_E + e, av[k]);
+  }
 }
 
 // Wext[:, E:E+2r] <- s * B (q rows 0..E-1 columns E..E+r-1, v rows 2E..3E-1 columns E+r..E+2r-1);
@@ -601,7 +665,7 @@ int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float
                    void* stream) {
   RDX_REQUIRE(dx1 && dgate && h && mean && rstd && gamma && beta && wg && bg && gconst && dres && dh && M > 0);
   const bool lora = lora_aq != nullptr;
-  RDX_REQUIRE(E == WL_E && ldx % 8 == 0 && (!lora || (2 * r == WL_R2 && lora_av && xd && ldx >= E + 2 * r)));
+  RDX_REQUIRE(E == WL_E && ldx % 8 == 0 && (!lora || (2 * r == WL_R2 && lora_av && ldx >= E + 2 * r)));
   Ln1BwdArgs a{reinterpret_cast<const __hip_bfloat16*>(dx1), ldx, dgate, h, mean, rstd, gamma, beta,
                GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
                dres, dh, reinterpret_cast<__hip_bfloat16*>(xd), M};
@@ -609,6 +673,20 @@ int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float
     hipLaunchKernelGGL(wl_ln1_bwd_kernel<true>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
   else
     hipLaunchKernelGGL(wl_ln1_bwd_kernel<false>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx, const void* dx1, int64_t ldd,
+                     const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, float scale, float* daq,
+                     float* dbq, float* dav, float* dbv, int64_t M, int E, int r, void* stream) {
+  RDX_REQUIRE(dqkv && x1 && dx1 && daq && dbq && dav && dbv && M > 0 && E == WL_E && 2 * r == WL_R2);
+  RDX_REQUIRE(ldq >= 3 * (int64_t)E && ldx >= E + 2 * r && ldd >= E + 2 * r);
+  LoraGradArgs a{reinterpret_cast<const __hip_bfloat16*>(dqkv), ldq, reinterpret_cast<const __hip_bfloat16*>(x1), ldx,
+                 reinterpret_cast<const __hip_bfloat16*>(dx1), ldd, mk_drop(seed_dev, salt_q, p_lora),
+                 mk_drop(seed_dev, salt_v, p_lora), scale, daq, dbq, dav, dbv, M};
+  const dim3 grid(WL_E / 256, (unsigned)((M + WL_LG_ROWS - 1) / WL_LG_ROWS));
+  hipLaunchKernelGGL(wl_lora_grad_kernel, grid, dim3(256), 0, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return 0;
 }

@@ -395,12 +395,13 @@ class Encoder(nn.Module):
             return layer(h, pos)
         for i, layer in enumerate(self.layers):
             states.append(h)
-            if self.training and self.keep_dev is not None and i > 0:
+            if self.training and self.keep_dev is not None and i > 0 and p > 0:
                 hn, pos = run(i, layer, h, pos)
                 h = torch.where(self.keep_dev[i], hn, h)
                 continue
             # HF draws torch.rand([]) for EVERY layer (train or eval) and skips when training, i > 0 and
             # draw < layerdrop; the same CPU-RNG consumption is kept here
+            # (graph mode with layerdrop 0 keeps every layer: no select, no draw needed)
             r = float(torch.rand([])) if self.keep_dev is None else 1.0
             skip = self.training and i > 0 and p > 0 and r < p
             if not skip:

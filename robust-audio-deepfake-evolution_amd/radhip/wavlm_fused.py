@@ -1,8 +1,10 @@
 """Fused WavLM encoder layer for the bf16 training/eval step (csrc/wavlm_layer.hip + attention.hip).
 
+The LoRA weight gradients (four skinny reductions over the tokens) are one kernel that accumulates
+into the fp32 .grad buffers directly (so the Function returns no gradient for those leaves).
 One autograd Function per layer replaces the ~44 forward / ~100 backward framework kernels of the
 module-by-module layer (casts, LN, gate MLP, LoRA GEMMs, dropouts, residual adds) with 9 forward and
-13 backward launches: four hipBLASLt GEMMs (q/k/v with the LoRA update folded in as 16 extra K
+11 backward launches: four hipBLASLt GEMMs (q/k/v with the LoRA update folded in as 16 extra K
 columns, out_proj, FFN1, FFN2), the MFMA gated-bias attention, and wave-per-row fused kernels for
 LN1 + gate + LoRA-A, dropout + residual + LN2, GELU, and their backwards. Same math as the
 reference layer (HF WavLMEncoderLayerStableLayerNorm + peft LoRA q/v; DualStreamSEMamba.py:292-439,
@@ -140,11 +142,10 @@ class WavLMLayerFn(torch.autograd.Function):
         gate = torch.empty(M, H, device=dev, dtype=torch.float32)
         mean1 = torch.empty(M, device=dev, dtype=torch.float32)
         rstd1 = torch.empty_like(mean1)
-        with _timed("wl_ln1_fwd", hf, float(M * E * 4 + M * ldx * 2)):
-            check(lib().rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg),
-                                       _p(cache.gconst), _p(aq) if lora else None, _p(av) if lora else None, 8,
-                                       sdp, salt + 3, salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1),
-                                       _p(rstd1), M, E, st), "wl_ln1_fwd")
+        check(lib().rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg),
+                                   _p(cache.gconst), _p(aq) if lora else None, _p(av) if lora else None, 8,
+                                   sdp, salt + 3, salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1),
+                                   _p(rstd1), M, E, st), "wl_ln1_fwd")
         qkv = F.linear(x1, cache.wext, cache.bqkv)                          # [M, 3E] (LoRA folded in)
         o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(B, H, T, device=dev, dtype=torch.float32)
@@ -169,6 +170,7 @@ class WavLMLayerFn(torch.autograd.Function):
         check(lib().rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st), "wl_residual")
         ctx.save_for_backward(hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, pb, aq, av)
         ctx.layer, ctx.cache = layer, cache
+        ctx.lora_b = (bq, bv)
         ctx.meta = (B, T, E, H, index, float(p_hidden), float(p_attn), float(p_lora), float(scale), lora,
                     sd is not None)
         return out.view(B, T, E)
@@ -207,19 +209,23 @@ class WavLMLayerFn(torch.autograd.Function):
                   "attn_bwd")
         dx1 = torch.mm(dqkv, cache.wext)                                     # [M, E + 2r]
         dh = torch.empty(M, E, device=dev, dtype=torch.float32)
-        xd = torch.empty(2, M, E, device=dev, dtype=torch.bfloat16) if lora else None
         check(lib().rdx_wl_ln1_bwd(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
                                    _p(ln1.bias), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
                                    _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3, salt + 4,
-                                   p_lora, _p(dh2), _p(dh), _p(xd) if lora else None, M, E, st), "wl_ln1_bwd")
-        daq = dbq = dav = dbv = None
+                                   p_lora, _p(dh2), _p(dh), None, M, E, st), "wl_ln1_bwd")
         if lora:
-            r = 8
-            dbq = torch.mm(dqkv[:, :E].t(), x1[:, E:E + r]).float().mul_(scale)        # [E, r]
-            dbv = torch.mm(dqkv[:, 2 * E:].t(), x1[:, E + r:E + 2 * r]).float().mul_(scale)
-            daq = torch.mm(dx1[:, E:E + r].t(), xd[0]).float()                         # [r, E]
-            dav = torch.mm(dx1[:, E + r:E + 2 * r].t(), xd[1]).float()
-        return (dh.view(B, T, E), daq, dbq, dav, dbv) + (None,) * 9
+            # the four LoRA weight gradients in one launch, accumulated straight into .grad (fp32; with
+            # FlatGrads these are views of the flat all-reduce buffer) instead of returned to autograd
+            bq, bv = ctx.lora_b
+            gs = []
+            for prm in (aq, bq, av, bv):
+                if prm.grad is None:
+                    prm.grad = torch.zeros_like(prm)
+                gs.append(prm.grad)
+            check(lib().rdx_wl_lora_grad(_p(dqkv), 3 * E, _p(x1), ldx, _p(dx1), ldx, sdp, salt + 3, salt + 4,
+                                         p_lora, scale, _p(gs[0]), _p(gs[1]), _p(gs[2]), _p(gs[3]), M, E, 8, st),
+                  "wl_lora_grad")
+        return (dh.view(B, T, E),) + (None,) * 13
 
 
 class FusedEncoderRunner:

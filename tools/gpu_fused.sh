@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/fz
-timeout -k 10 600 python -u -m pytest tests/test_wavlm_fused_gpu.py tests/test_cli_gpu.py tests/test_model_gpu.py tests/test_graph_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/fz/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_wavlm_fused_gpu.py tests/test_cli_gpu.py tests/test_model_gpu.py tests/test_graph_gpu.py} -x -v --timeout 300 --timeout-method thread > gpurun_out/fz/pytest.log 2>&1; rc=$?
 grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/fz/pytest.log | tail -25
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/fz/bench.json 2> gpurun_out/fz/bench.err; rc=$?
