@@ -37,8 +37,33 @@ PEAKS = {"hbm": 8000.0, "fp32": 157.3, "bf16": 2500.0}  # GB/s ; TFLOP/s (MI355X
 KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "selective_scan_fwd": ("hbm", None),
                 "selective_scan_bwd": ("hbm", None), "layer_wsum_fwd": ("hbm", None),
                 "layer_wsum_bwd": ("hbm", None), "rawboost_batch": ("hbm", None),
-                "attn_fwd": ("mfma", "bf16"), "attn_bwd": ("mfma", "bf16")}
+                "attn_fwd": ("mfma", "bf16"), "attn_bwd": ("mfma", "bf16"),
+                "posconv_fwd": ("mfma", "bf16"), "posconv_bwd": ("mfma", "bf16"),
+                "sincnet_b0_bwd": ("hbm", None)}
 TRAIN_FLOP_PER_UTT = 0.72e12                # SURVEY.md §8d (algorithmic, FGM step)
+
+
+class Heartbeat:
+    """A line on stderr every `every` seconds naming the current phase: a first run on a fresh box spends
+    minutes in MIOpen find / graph capture without other output."""
+
+    def __init__(self, every=30.0):
+        import threading
+        self.phase, self.t0 = "start", time.time()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, args=(every,), daemon=True)
+        self._th.start()
+
+    def _run(self, every):
+        while not self._stop.wait(every):
+            print(f"[bench] {self.phase} ({time.time() - self.t0:.0f} s)", file=sys.stderr, flush=True)
+
+    def set(self, phase):
+        self.phase = phase
+        print(f"[bench] {phase} ({time.time() - self.t0:.0f} s)", file=sys.stderr, flush=True)
+
+    def stop(self):
+        self._stop.set()
 
 
 def parse():
@@ -58,6 +83,9 @@ def parse():
     ap.add_argument("--config", default="Phase6_Proposed.conf")
     ap.add_argument("--eager", action="store_true",
                     help="launch the micro-step kernel by kernel instead of replaying it as HIP graphs")
+    ap.add_argument("--no-window", action="store_true",
+                    help="run the accumulation window micro-batch by micro-batch (reference order) instead of "
+                         "batching its clean passes (radhip/window.py)")
     return ap.parse_args()
 
 
@@ -115,8 +143,8 @@ def roofline_from_rows(rows, graphed=False):
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": dom,
             "avg_launch_ms": round(r["avg_ms"], 5), "work_per_launch": r["avg_work"],
             "work_unit": "FLOP" if bound == "mfma" else "bytes",
-            "timing": ("device wall-clock stamps (rdx_timestamp_acc) captured around each launch inside the "
-                       "replayed HIP graphs, accumulated over every launch of the timed region") if graphed else
+            "timing": ("device wall-clock stamps (rdx_timestamp_acc) captured around the first 2 launch sites of each "
+                       "kernel in each replayed HIP graph, accumulated over every replay of the timed region") if graphed else
                       "HIP events on the launch stream around every launch of the timed region"}
     return roof, rows
 
@@ -194,6 +222,7 @@ def cpu_baseline(config, threads, microsteps):
 
 def main():
     args = parse()
+    hb = Heartbeat()
     ws, rank, local = dist_setup()
     dev = torch.device("cuda", local)
     from radhip import ops
@@ -216,12 +245,23 @@ def main():
     import random as pyrandom
     pyrandom.seed(1234 + rank)
     B = args.micro_batch
-    graph, graph_timer = None, None
-    if not args.eager:
+    graph, graph_timer, window = None, None, None
+    if not args.no_window:
+        from radhip.window import WindowStep
+        window = WindowStep(trainer, B, graphs=not args.eager)
+    elif not args.eager:
         graph = GraphedMicroStep(trainer, B)
+    if not args.eager:
+        hb.set("capturing HIP graphs")
         graph_timer = ops.GraphTimer(dev)
         ops.CAPTURE_TIMING = graph_timer    # captured clock stamps around every radhip launch in the graphs
-        graph.capture()
+        if window is not None:
+            for k in range(args.accum):     # capture needs one staged window of draws
+                window.add(k, np.zeros(B, dtype=np.int64))
+            window.capture()
+            window.reset_host()
+        else:
+            graph.capture()
         ops.CAPTURE_TIMING = None
 
     def micro(i, last):
@@ -230,7 +270,12 @@ def main():
         lens = [L_RAW] * B
         plan = aug.draw(lens)
         lam, perm = trainer.mixup_draw(B)
-        if graph is not None:
+        if window is not None:
+            aug.run(pool_x, offs, lens, plan, perm, lam, out=window.xslot(i))
+            window.add(i, pool_y[idx].numpy(), lam, perm)
+            if last:
+                window.run()
+        elif graph is not None:
             aug.run(pool_x, offs, lens, plan, perm, lam, out=graph.x)
             graph.run(pool_y[idx].numpy(), lam, perm, last_in_epoch=last)
         else:
@@ -241,12 +286,14 @@ def main():
         for i in range(args.accum):
             micro(i, i == args.accum - 1)
 
+    hb.set("warm-up")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    hb.set("timed steps")
     ops.TIMING = {}
     if graph_timer is not None:
         graph_timer.reset()
@@ -279,7 +326,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
     loss = trainer.epoch_loss()
-    roof, rows = roofline_from_rows(rows, graphed=graph is not None)
+    roof, rows = roofline_from_rows(rows, graphed=not args.eager)
     utts = ws * args.steps * args.accum * B
     value = utts / wall_max
     if rank == 0:
@@ -293,7 +340,8 @@ def main():
                        "micro_batch": B, "accumulation": args.accum, "global_batch": ws * B * args.accum,
                        "seq_len": 64600, "parallelism": f"dp{ws}", "fgm": True, "mixup": True,
                        "rawboost_algo": dc.get("rawboost_algo"), "codec_p": dc.get("codec_p"),
-                       "wavlm_layerdrop": args.layerdrop, "hip_graphs": graph is not None},
+                       "wavlm_layerdrop": args.layerdrop, "hip_graphs": not args.eager,
+                       "window_batched_clean_passes": window is not None},
             "roofline": roof,
             "step_mfma_frac": round(value / ws * TRAIN_FLOP_PER_UTT / 2.5e15, 4),
             "kernels": {k: {kk: round(vv, 5) if isinstance(vv, float) else vv for kk, vv in v.items()}
@@ -302,10 +350,12 @@ def main():
         }
         if ws == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 8)
+            hb.set("cpu baseline")
             line["cpu_baseline"] = cpu_baseline(config, threads, args.cpu_microsteps)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
+    hb.stop()
     if ws > 1:
         dist.destroy_process_group()
 

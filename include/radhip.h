@@ -47,11 +47,14 @@ const char* rdx_strerror(int code);
 int rdx_sincconv_absmaxpool_fwd(const float* x, int64_t batch, int64_t len, const float* filters,
                                 int channels, int ksize, int mask_lo, int mask_hi, float* out,
                                 void* stream);
-/* Same, with the band mask [lo, hi) read from device memory (int32[2]) at execution time, so a
- * captured HIP graph can be replayed with a fresh mask per call. */
+/* Same, with the band mask [lo, hi) read from device memory at execution time, so a captured HIP
+ * graph can be replayed with a fresh mask per call: utterance b uses mask_dev[b*mask_stride + {0,1}]
+ * (mask_stride 0: one int32[2] mask for the batch, as one CONV.forward call draws; 2: one mask per
+ * utterance, for several forward calls batched into one launch). */
 int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch, int64_t len,
                                         const float* filters, int channels, int ksize,
-                                        const int32_t* mask_dev, float* out, void* stream);
+                                        const int32_t* mask_dev, int mask_stride, float* out,
+                                        void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Bidirectional Mamba (replaces mamba_ssm Mamba.forward -> mamba_inner_fn, called twice per
@@ -210,22 +213,43 @@ int rdx_res_tail_fwd(int dtype, const void* a, const void* identity, const float
                      uint8_t* argmax, int64_t rows, int W, int C, void* stream);
 int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax, void* dx, float* dbias, int64_t rows,
                      int W, int C, void* stream);
+/* SincNet block 0 (ONE input channel, C = 32 output channels): backward of conv1 (2 x 3, padding (1, 1)) and
+ * conv_downsample (1 x 3, padding (0, 1)) (Residual_block.forward, src/models/DualStreamSEMamba.py:182-200) in
+ * one pass. x bf16 [N, H, W] (the block input); dc bf16 [N, H+1, W, C] = d conv1 output (NHWC); di bf16
+ * [N, H, W, C] = d conv_downsample output (NHWC); w1 fp32 [C][2][3], wd fp32 [C][3]. Writes dx fp32 [N, H, W]
+ * and per-block partial weight gradients part fp32 [nblk][C][9] (taps 0..5 = conv1 kh*3+kw, 6..8 =
+ * conv_downsample kw; the caller sums dim 0), nblk = rdx_sincnet_b0_nblk(N*H*W). C != 32: RDX_EUNSUPPORTED. */
+int rdx_sincnet_b0_nblk(int64_t npix);
+int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di, const float* w1, const float* wd, float* dx,
+                       float* part, int N, int H, int W, int C, void* stream);
+
+/* ---- WavLM positional convolution (HF WavLMPositionalConvEmbedding inside WavLMFrontend,
+ * src/models/DualStreamSEMamba.py:292-439): grouped Conv1d 1024 -> 1024, 16 groups x 64 channels, 128 taps,
+ * padding 64, last frame dropped, + bias, GELU (erf), MFMA bf16 with fp32 accumulation ----------------------
+ * h, y, u, dy, dh: bf16 [B, T, 1024] token-major rows, 16-byte aligned.
+ * rdx_posconv_fwd: u = conv(h) + bias (kept for the backward), y = gelu(u); wk bf16 [16][128][64][64] holds
+ *   W[g*64+n, c, k] at [g][k][n][c]; bias fp32 [1024].
+ * rdx_posconv_bwd: dh = conv^T(dy * gelu'(u)); wkt bf16 [16][128][64][64] holds W[g*64+n, c, 127-k] at
+ *   [g][k][c][n]. The weights are frozen in Phase 6: no weight gradient. */
+int rdx_posconv_fwd(const void* h, const void* wk, const float* bias, void* y, void* u, int B, int T, void* stream);
+int rdx_posconv_bwd(const void* dy, const void* u, const void* wkt, void* dh, int B, int T, void* stream);
 
 /* ---- WavLM self-attention with the gated relative-position bias (HF WavLMAttention as used by
  * WavLMFrontend, src/models/DualStreamSEMamba.py:292-439), MFMA bf16, 64-dim heads -------------------
  * q, k, v: bf16 [B, T, H*64] row views (row strides ldq/ldk/ldv, 16-byte aligned); gate [B, T, H] fp32;
- * pos_bias [H, T, T] fp32 (frozen). S = q k^T * scale + gate[b,i,h] * pos_bias[h,i,j]; P = softmax(S);
+ * pos_bias [H, T, ldpb] fp32 (frozen; ldpb >= 32*ceil(T/32), a multiple of 4, 16-byte aligned).
+ * S = q k^T * scale + gate[b,i,h] * pos_bias[h,i,j]; P = softmax(S);
  * O = dropout_p(P) v -> o [B, T, H*64] bf16 (row stride ldo); lse [B, H, T] fp32 (saved for bwd).
  * Dropout keeps (b,h,i,j) iff hash(seed, ((b*H+h)*T+i)*T+j) >= p*2^32, seed = f(seed_dev[0], salt)
  * read on the device (HIP-graph replayable); rdx_attn_dropout_mask materialises that mask (tests).
  * rdx_attn_bwd: D [B, H, T] fp32 workspace; dq, dk, dv bf16 [B, T, H*64] (row stride ldg), dgate
  * [B, T, H] fp32 (all overwritten). */
 int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                 const float* gate, const float* pos_bias, const int64_t* seed_dev, int salt, float p_drop,
-                 float scale, void* o, int64_t ldo, float* lse, int B, int T, int H, int head_dim, void* stream);
+                 const float* gate, const float* pos_bias, int64_t ldpb, const int64_t* seed_dev, int salt,
+                 float p_drop, float scale, void* o, int64_t ldo, float* lse, int B, int T, int H, int head_dim, void* stream);
 int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                 const float* gate, const float* pos_bias, const int64_t* seed_dev, int salt, float p_drop,
-                 float scale, const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo,
+                 const float* gate, const float* pos_bias, int64_t ldpb, const int64_t* seed_dev, int salt,
+                 float p_drop, float scale, const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo,
                  float* D, void* dq, void* dk, void* dv, int64_t ldg, float* dgate, int B, int T, int H,
                  int head_dim, void* stream);
 int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n,

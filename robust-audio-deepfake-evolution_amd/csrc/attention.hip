@@ -11,44 +11,40 @@
 // (seed, index) >= p * 2^32, so the backward regenerates the same mask; the seed is read from device
 // memory, which keeps the launch replayable inside a HIP graph.
 //
-// Tiling: one wave per 32-row tile; mfma_f32_32x32x16_bf16 (A: lane (r, h) holds A[r][8h + j],
-// B: B[8h + j][r], C: col = lane & 31, row = (i & 3) + 8 (i >> 2) + 4h). T = 201 is covered by 7
-// tiles of 32 keys; Dh = 64 = 4 k-steps.
-//   forward   S^T = K Q^T (query on the lane, keys in registers), online softmax over key tiles,
-//             O^T += V^T P^T with P^T taken straight from the accumulator (B operand) and V^T from LDS.
-//   dK, dV    key-stationary: S = Q K^T, dP = dO V^T (query rows in registers), dV += P^T dO and
-//             dK += dS^T Q with P / dS as the A operand and dO^T / Q^T from LDS.
-//   dQ, dgate query-stationary: S^T, dP^T as the forward, dQ^T += K^T dS^T (K^T from LDS); the gate
-//             gradient is a lane-local sum plus one cross-half exchange.
-//   D         rowsum(dO o O) per (b, h, i), the softmax-backward correction.
+// Structure (T <= 256, i.e. at most 8 tiles of 32 rows; the WavLM stream at 64 600 samples has T = 201).
+// A workgroup is 4 waves of one (b, h). It first stages the whole sequence of the two operands it sweeps
+// into LDS images (K and V for the query-stationary forward and dQ kernels, Q and dO for the
+// key-stationary dK/dV kernel); then each wave owns one 32-row tile and loops over every tile of the other
+// side with no barrier and no global load but the position-bias row. MFMA is mfma_f32_32x32x16_bf16
+// (A: lane (r, h) holds A[r][8h + j]; B: B[8h + j][r]; C: col = lane & 31, row = (i & 3) + 8 (i >> 2) + 4h).
+// A fragment that runs along a row of an image is one 16-byte ds_read; a fragment that runs down a column
+// (V^T, K^T, Q^T, dO^T in the k order of an accumulator fed back as an operand) is two
+// ds_read_b64_tr_b16 hardware-transposed reads. The images use 8-row x 32-column subtiles with the 16-byte
+// chunk XOR-swizzled by (row >> 2) & 3, which keeps both kinds of read conflict-free with no padding.
+//   forward  S^T = K Q^T (query on the lane), online softmax over the key tiles, O^T += V^T P^T.
+//   dQ       query-stationary; also writes D = rowsum(dO o O) for its rows. S^T and dP^T = V dO^T as the
+//            forward, dQ^T += K^T dS^T; d gate is a lane-local sum plus one cross-half exchange.
+//   dK, dV   key-stationary: S = Q K^T, dP = dO V^T (query rows from the images), dV += P^T dO and
+//            dK += dS^T Q; gate, lse and D of every query row are staged in LDS with Q and dO.
 #include "common.h"
 
 namespace rdx {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
-constexpr int AT_DH = 64;    // head dim
-constexpr int AT_TILE = 32;  // rows per wave
-constexpr int AT_LDP = AT_TILE + 4;  // padded LDS row (bf16) for transposed tiles
-// waves per block splitting the inner (key or query) loop of each kernel
-#ifndef AT_NS_FWD
-#define AT_NS_FWD 4
-#endif
-#ifndef AT_NS_DKDV
-#define AT_NS_DKDV 2
-#endif
-#ifndef AT_NS_DQ
-#define AT_NS_DQ 4
-#endif
+typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 bf16x4v;
+typedef __attribute__((address_space(3))) bf16x4v lds_bf16x4v;
+constexpr int AT_DH = 64;                  // head dim
+constexpr int AT_TILE = 32;                // rows per wave
+constexpr int AT_MAXNT = 8;                // tiles per sequence: T <= 256
+constexpr int AT_WAVES = 4;                // waves (tiles) per workgroup
+constexpr int AT_TILE_BYTES = AT_TILE * AT_DH * 2;  // one 32-row tile of an image: 4 KB
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 // C/D row held in accumulator register i by lane half h
 __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
-// k index (a row of the accumulator X) carried by element j of lane half h at k-step s when X is fed
-// back as an MFMA operand (registers 8s .. 8s+7)
-__device__ __forceinline__ int krow(int s, int j, int h) { return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3); }
 
 __device__ __forceinline__ bf16x8 pack8(const float* x) {
   bf16x8 r;
@@ -72,19 +68,58 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-// stage the 32 x 64 tile held as 4 row-fragments (lane (r, h): row r, cols 16s + 8h + j) transposed
-// into LDS as t[col][row]
-__device__ __forceinline__ void stage_t(__bf16 (*t)[AT_LDP], const bf16x8* f, int r, int h) {
+// the 16 position-bias values of key tile kb this lane needs (keys kb*32 + crow(i, hh)): four float4
+// loads from a row padded to a multiple of 32
+__device__ __forceinline__ void load_pb16(const float* pbrow, int kb, int hh, float* v) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[16 * s + 8 * h + j][r] = f[s][j];
+  for (int c = 0; c < 4; ++c) {
+    const float4 t = *reinterpret_cast<const float4*>(pbrow + kb * AT_TILE + 8 * c + 4 * hh);
+    v[4 * c] = t.x;
+    v[4 * c + 1] = t.y;
+    v[4 * c + 2] = t.z;
+    v[4 * c + 3] = t.w;
+  }
 }
-// operand fragment whose element j is t[row][krow(s, j, h)]
-__device__ __forceinline__ bf16x8 read_t(const __bf16 (*t)[AT_LDP], int row, int s, int h) {
+
+// Byte offset of 16-byte chunk ch (0..7, columns 8 ch .. 8 ch + 7) of image row `row`: 8-row x 32-column
+// subtiles of 512 B, chunk XOR-swizzled by (row >> 2) & 3 (MI355X guide T10, layout (a), on 64-column rows).
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return 1024 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// rows [0, 32 nt) of the head slice (columns col0 .. col0 + 63) of a [B, T, ld] bf16 tensor into an LDS
+// image; rows past T are zero. Every thread of the workgroup takes part.
+__device__ __forceinline__ void stage_image(char* img, const __hip_bfloat16* src, int64_t ld, int b, int T,
+                                            int64_t col0, int nt) {
+  for (int i = threadIdx.x; i < nt * AT_TILE * 8; i += AT_WAVES * 64) {
+    const int row = i >> 3, ch = i & 7;
+    *reinterpret_cast<bf16x8*>(img + img_off(row, ch)) =
+        load8(src + ((int64_t)b * T + row) * ld + col0 + 8 * ch, row < T);
+  }
+}
+// fragment along a row: element j = X[row][16 s + 8 h + j]
+__device__ __forceinline__ bf16x8 read_row(const char* img, int row, int s, int h) {
+  return *reinterpret_cast<const bf16x8*>(img + img_off(row, 2 * s + h));
+}
+// fragment down a column in the k order of an accumulator fed back as an operand:
+//   element j = X[r0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)][c0 + (lane & 31)].
+// Each ds_read_b64_tr_b16 gives 16-lane group g the 4 x 16 block at rows r0 + 16 s + 4 (g >> 1) (+ 8 for
+// elements 4..7), columns c0 + 16 (g & 1) .. + 15, column-major (lane i of the group gets column i, row q in
+// element q); lane 4q + p of the group supplies the address of row q, columns 4p .. 4p + 3.
+__device__ __forceinline__ bf16x8 read_tr(char* img, int r0, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = r0 + 16 * s + 4 * (g >> 1) + (i >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const int sub = 2 * (col & 7);  // 0 or 8 bytes into the chunk
+  const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)(img + img_off(row, col >> 3) + sub));
+  const bf16x4v hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)(img + img_off(row + 8, col >> 3) + sub));
   bf16x8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = t[row][krow(s, j, h)];
+  for (int j = 0; j < 4; ++j) {
+    r[j] = lo[j];
+    r[4 + j] = hi[j];
+  }
   return r;
 }
 
@@ -92,7 +127,8 @@ struct AttnArgs {
   const __hip_bfloat16 *q, *k, *v;
   int64_t ldq, ldk, ldv;
   const float* gate;  // [B, T, H]
-  const float* pb;    // [H, T, T]
+  const float* pb;    // [H, T, ldpb], ldpb >= 32 * ceil(T / 32), rows 16-byte aligned
+  int64_t ldpb;
   const int64_t* seed_dev;
   int salt;
   uint32_t thr;   // p * 2^32 (0: no dropout)
@@ -101,55 +137,52 @@ struct AttnArgs {
   int B, T, H;
 };
 
-// NS waves per block share one 32-query tile and split its key tiles (wave w takes kb = w, w + NS,
-// ...); their online-softmax partials (m, l, O) are merged through LDS at the end. This multiplies the
-// waves in flight by NS (T = 201 gives only 7 query tiles per (b, h)).
-template <bool kDrop, int NS>
-__global__ __launch_bounds__(64 * NS) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16* __restrict__ o, int64_t ldo,
-                                                           float* __restrict__ lse) {
-  __shared__ __bf16 s_vt_all[NS][AT_DH][AT_LDP];
-  __shared__ float s_m[AT_TILE], s_l[AT_TILE];
-  __shared__ float s_o[2][16][64];
-  const int w = threadIdx.x >> 6;
-  __bf16 (*s_vt)[AT_LDP] = s_vt_all[w];
-  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int qb = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
-  const int T = a.T, H = a.H;
+struct AttnBwdArgs {
+  const __hip_bfloat16* dO;
+  int64_t lddo;
+  const float* lse;  // [B, H, T]
+  float* D;          // [B, H, T]: written by the dQ kernel, read by the dK/dV kernel
+};
+
+template <bool kDrop>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16* __restrict__ o, int64_t ldo,
+                                                       float* __restrict__ lse) {
+  extern __shared__ __attribute__((aligned(16))) char at_lds[];
+  const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int64_t col0 = (int64_t)head * AT_DH;
+  char* Ks = at_lds;
+  char* Vs = at_lds + nt * AT_TILE_BYTES;
+  stage_image(Ks, a.k, a.ldk, b, T, col0, nt);
+  stage_image(Vs, a.v, a.ldv, b, T, col0, nt);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int qb = blockIdx.x * AT_WAVES + w;
+  if (qb >= nt) return;  // no barrier follows
   const int qi = qb * AT_TILE + r;
   const bool qvalid = qi < T;
   const int qc = qvalid ? qi : T - 1;
-  const int64_t col0 = (int64_t)head * AT_DH;
   bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = load8(a.q + ((int64_t)b * T + qc) * a.ldq + col0 + 16 * s + 8 * hh, qvalid);
   const float g = a.gate[((int64_t)b * T + qc) * H + head];
-  const float* pbrow = a.pb + ((int64_t)head * T + qc) * T;
+  const float* pbrow = a.pb + ((int64_t)head * T + qc) * a.ldpb;
   const uint64_t seed = kDrop ? attn_seed(a.seed_dev, a.salt) : 0;
   const uint64_t ibase = (((uint64_t)b * H + head) * T + qc) * (uint64_t)T;
   float m = -INFINITY, l = 0.f;
   f32x16 oacc[2] = {zero16(), zero16()};
-  const int nkb = (T + AT_TILE - 1) / AT_TILE;
-  const int niter = (nkb + NS - 1) / NS;  // equal trip counts keep the barriers uniform
-  for (int it = 0; it < niter; ++it) {
-    const int kb = w + NS * it;
-    const int kr = kb * AT_TILE + r;
-    const bool kvalid = kr < T;
+  for (int kb = 0; kb < nt; ++kb) {
     f32x16 sacc = zero16();
-    bf16x8 vfr[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 kf = load8(a.k + ((int64_t)b * T + kr) * a.ldk + col0 + 16 * s + 8 * hh, kvalid);
-      sacc = mfma32(kf, qf[s], sacc);
-      vfr[s] = load8(a.v + ((int64_t)b * T + kr) * a.ldv + col0 + 16 * s + 8 * hh, kvalid);
-    }
-    stage_t(s_vt, vfr, r, hh);
-    float sv[16];
+    for (int s = 0; s < 4; ++s) sacc = mfma32(read_row(Ks, kb * AT_TILE + r, s, hh), qf[s], sacc);
+    float sv[16], pbv[16];
+    load_pb16(pbrow, kb, hh, pbv);
     float mloc = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = kb * AT_TILE + crow(i, hh);
       float x = -INFINITY;
-      if (key < T) x = fmaf(sacc[i], a.scale, g * pbrow[key]);
+      if (key < T) x = fmaf(sacc[i], a.scale, g * pbv[i]);
       sv[i] = x;
       mloc = fmaxf(mloc, x);
     }
@@ -176,44 +209,14 @@ __global__ __launch_bounds__(64 * NS) void attn_fwd_kernel(AttnArgs a, __hip_bfl
       oacc[0][i] *= alpha;
       oacc[1][i] *= alpha;
     }
-    __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 pf = pack8(sv + 8 * s);
 #pragma unroll
-      for (int db = 0; db < 2; ++db) oacc[db] = mfma32(read_t(s_vt, db * 32 + r, s, hh), pf, oacc[db]);
-    }
-    __syncthreads();
-  }
-  // merge the NS partials into wave 0
-  for (int src = 1; src < NS; ++src) {
-    __syncthreads();
-    if (w == src) {
-      if (hh == 0) {
-        s_m[r] = m;
-        s_l[r] = l;
-      }
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s_o[db][i][lane] = oacc[db][i];
-    }
-    __syncthreads();
-    if (w == 0) {
-      const float mw = s_m[r], lw = s_l[r];
-      if (mw != -INFINITY) {
-        const float mnew = fmaxf(m, mw);
-        const float a0 = __expf(m - mnew), a1 = __expf(mw - mnew);
-        l = l * a0 + lw * a1;
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[db][i] = oacc[db][i] * a0 + s_o[db][i][lane] * a1;
-        m = mnew;
-      }
+      for (int db = 0; db < 2; ++db) oacc[db] = mfma32(read_tr(Vs, kb * AT_TILE, db * 32, s, lane), pf, oacc[db]);
     }
   }
-  if (w == 0 && qvalid) {
+  if (qvalid) {
     const float inv = 1.f / l;
     __hip_bfloat16* orow = o + ((int64_t)b * T + qi) * ldo + col0;
 #pragma unroll
@@ -224,53 +227,117 @@ __global__ __launch_bounds__(64 * NS) void attn_fwd_kernel(AttnArgs a, __hip_bfl
   }
 }
 
-// D[b, h, i] = sum_d dO[b, i, h, d] * O[b, i, h, d]
-__global__ __launch_bounds__(256) void attn_bwd_dot_kernel(const __hip_bfloat16* __restrict__ dO, int64_t lddo,
-                                                           const __hip_bfloat16* __restrict__ O, int64_t ldo,
-                                                           float* __restrict__ D, int B, int T, int H) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (b, i, h)
-  if (t >= (int64_t)B * T * H) return;
-  const int head = (int)(t % H);
-  const int64_t bi = t / H;
-  const int b = (int)(bi / T), i = (int)(bi - (int64_t)b * T);
-  const __hip_bfloat16* x = dO + bi * lddo + head * AT_DH;
-  const __hip_bfloat16* y = O + bi * ldo + head * AT_DH;
-  float acc = 0.f;
+// query-stationary: dQ, d gate and D = rowsum(dO o O) of the wave's 32 query rows
+template <bool kDrop>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs g,
+                                                          const __hip_bfloat16* __restrict__ O, int64_t ldo,
+                                                          __hip_bfloat16* __restrict__ dq, int64_t ldg,
+                                                          float* __restrict__ dgate) {
+  extern __shared__ __attribute__((aligned(16))) char at_lds[];
+  const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int64_t col0 = (int64_t)head * AT_DH;
+  char* Ks = at_lds;
+  char* Vs = at_lds + nt * AT_TILE_BYTES;
+  stage_image(Ks, a.k, a.ldk, b, T, col0, nt);
+  stage_image(Vs, a.v, a.ldv, b, T, col0, nt);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int qb = blockIdx.x * AT_WAVES + w;
+  if (qb >= nt) return;
+  const int qi = qb * AT_TILE + r;
+  const bool qvalid = qi < T;
+  const int qc = qvalid ? qi : T - 1;
+  const int64_t trow = (int64_t)b * T + qc;
+  bf16x8 qf[4], dof[4];
+  float dpart = 0.f;
 #pragma unroll
-  for (int c = 0; c < AT_DH / 8; ++c) {
-    const bf16x8 u = *reinterpret_cast<const bf16x8*>(x + 8 * c);
-    const bf16x8 w = *reinterpret_cast<const bf16x8*>(y + 8 * c);
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = load8(a.q + trow * a.ldq + col0 + 16 * s + 8 * hh, qvalid);
+    dof[s] = load8(g.dO + trow * g.lddo + col0 + 16 * s + 8 * hh, qvalid);
+    const bf16x8 of = load8(O + trow * ldo + col0 + 16 * s + 8 * hh, qvalid);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf((float)u[j], (float)w[j], acc);
+    for (int j = 0; j < 8; ++j) dpart = fmaf((float)dof[s][j], (float)of[j], dpart);
   }
-  D[((int64_t)b * H + head) * T + i] = acc;
+  const float Dq = dpart + __shfl_xor(dpart, 32, 64);
+  const int64_t bh = (int64_t)b * H + head;
+  if (hh == 0 && qvalid) g.D[bh * T + qi] = Dq;
+  const float gq = a.gate[trow * H + head];
+  const float lq = g.lse[bh * T + qc];
+  const float* pbrow = a.pb + ((int64_t)head * T + qc) * a.ldpb;
+  const uint64_t seed = kDrop ? attn_seed(a.seed_dev, a.salt) : 0;
+  const uint64_t ibase = ((uint64_t)bh * T + qc) * (uint64_t)T;
+  f32x16 dqacc[2] = {zero16(), zero16()};
+  float dg = 0.f;
+  for (int kb = 0; kb < nt; ++kb) {
+    f32x16 S = zero16(), dP = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      S = mfma32(read_row(Ks, kb * AT_TILE + r, s, hh), qf[s], S);
+      dP = mfma32(read_row(Vs, kb * AT_TILE + r, s, hh), dof[s], dP);
+    }
+    float dS[16], pbt[16];
+    load_pb16(pbrow, kb, hh, pbt);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kb * AT_TILE + crow(i, hh);
+      float ds = 0.f;
+      if (key < T && qvalid) {
+        const float p = __expf(fmaf(S[i], a.scale, gq * pbt[i]) - lq);
+        float mk = 1.f;
+        if (kDrop) mk = drop_keep(seed, ibase + key, a.thr) ? a.inv_keep : 0.f;
+        ds = p * (dP[i] * mk - Dq);
+        dg = fmaf(ds, pbt[i], dg);
+      }
+      dS[i] = ds;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 xs = pack8(dS + 8 * s);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) dqacc[db] = mfma32(read_tr(Ks, kb * AT_TILE, db * 32, s, lane), xs, dqacc[db]);
+    }
+  }
+  dg += __shfl_xor(dg, 32, 64);
+  if (qvalid) {
+    __hip_bfloat16* row = dq + ((int64_t)b * T + qi) * ldg + col0;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) row[db * 32 + crow(i, hh)] = __float2bfloat16(dqacc[db][i] * a.scale);
+    if (hh == 0) dgate[((int64_t)b * T + qi) * H + head] = dg;
+  }
 }
 
-struct AttnBwdArgs {
-  const __hip_bfloat16* dO;
-  int64_t lddo;
-  const float* lse;  // [B, H, T]
-  const float* D;    // [B, H, T]
-};
-
-// NS waves per block share one 32-key tile and split its query tiles; dK/dV partials are summed
-// through LDS at the end.
-template <bool kDrop, int NS>
-__global__ __launch_bounds__(64 * NS) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdArgs g,
-                                                                __hip_bfloat16* __restrict__ dk,
-                                                                __hip_bfloat16* __restrict__ dv, int64_t ldg) {
-  __shared__ __bf16 s_qt_all[NS][AT_DH][AT_LDP];
-  __shared__ __bf16 s_dot_all[NS][AT_DH][AT_LDP];
-  __shared__ float s_acc[4][16][64];
-  const int w = threadIdx.x >> 6;
-  __bf16 (*s_qt)[AT_LDP] = s_qt_all[w];
-  __bf16 (*s_dot)[AT_LDP] = s_dot_all[w];
-  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int kb = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
-  const int T = a.T, H = a.H;
+// key-stationary: dK and dV of the wave's 32 keys
+template <bool kDrop>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdArgs g,
+                                                            __hip_bfloat16* __restrict__ dk,
+                                                            __hip_bfloat16* __restrict__ dv, int64_t ldg) {
+  extern __shared__ __attribute__((aligned(16))) char at_lds[];
+  const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE, tp = nt * AT_TILE;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int64_t col0 = (int64_t)head * AT_DH;
+  const int64_t bh = (int64_t)b * H + head;
+  char* Qs = at_lds;
+  char* dOs = at_lds + nt * AT_TILE_BYTES;
+  float* s_gate = reinterpret_cast<float*>(at_lds + 2 * nt * AT_TILE_BYTES);  // [tp] gate, then lse, then D
+  float* s_lse = s_gate + tp;
+  float* s_D = s_lse + tp;
+  stage_image(Qs, a.q, a.ldq, b, T, col0, nt);
+  stage_image(dOs, g.dO, g.lddo, b, T, col0, nt);
+  for (int i = threadIdx.x; i < tp; i += AT_WAVES * 64) {
+    const bool ok = i < T;
+    s_gate[i] = ok ? a.gate[((int64_t)b * T + i) * H + head] : 0.f;
+    s_lse[i] = ok ? g.lse[bh * T + i] : 0.f;
+    s_D[i] = ok ? g.D[bh * T + i] : 0.f;
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int kb = blockIdx.x * AT_WAVES + w;
+  if (kb >= nt) return;
   const int key = kb * AT_TILE + r;  // this lane's key column
   const bool kvalid = key < T;
-  const int64_t col0 = (int64_t)head * AT_DH;
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -278,77 +345,51 @@ __global__ __launch_bounds__(64 * NS) void attn_bwd_dkdv_kernel(AttnArgs a, Attn
     vf[s] = load8(a.v + ((int64_t)b * T + key) * a.ldv + col0 + 16 * s + 8 * hh, kvalid);
   }
   const uint64_t seed = kDrop ? attn_seed(a.seed_dev, a.salt) : 0;
-  const int64_t bh = (int64_t)b * H + head;
+  const uint64_t kbase = (uint64_t)bh * T * (uint64_t)T + (uint64_t)key;
+  const float* pbcol = a.pb + (int64_t)head * T * a.ldpb + key;
   f32x16 dkacc[2] = {zero16(), zero16()}, dvacc[2] = {zero16(), zero16()};
-  const int nqb = (T + AT_TILE - 1) / AT_TILE;
-  const int niter = (nqb + NS - 1) / NS;
-  for (int it = 0; it < niter; ++it) {
-    const int qb = w + NS * it;
-    const int qr = qb * AT_TILE + r;  // row loaded by this lane for the A fragments
-    const bool qrv = qr < T;
-    bf16x8 qa[4], da[4];
+  for (int qb = 0; qb < nt; ++qb) {
     f32x16 S = zero16(), dP = zero16();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      qa[s] = load8(a.q + ((int64_t)b * T + qr) * a.ldq + col0 + 16 * s + 8 * hh, qrv);
-      da[s] = load8(g.dO + ((int64_t)b * T + qr) * g.lddo + col0 + 16 * s + 8 * hh, qrv);
-      S = mfma32(qa[s], kf[s], S);
-      dP = mfma32(da[s], vf[s], dP);
+      S = mfma32(read_row(Qs, qb * AT_TILE + r, s, hh), kf[s], S);
+      dP = mfma32(read_row(dOs, qb * AT_TILE + r, s, hh), vf[s], dP);
     }
-    stage_t(s_qt, qa, r, hh);
-    stage_t(s_dot, da, r, hh);
     float P[16], dS[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qi = qb * AT_TILE + crow(i, hh);
-      float p = 0.f, ds = 0.f;
-      if (qi < T && kvalid) {
-        const float gq = a.gate[((int64_t)b * T + qi) * H + head];
-        const float s = fmaf(S[i], a.scale, gq * a.pb[((int64_t)head * T + qi) * T + key]);
-        p = __expf(s - g.lse[bh * T + qi]);
-        float mk = 1.f;
-        if (kDrop) mk = drop_keep(seed, ((uint64_t)bh * T + qi) * (uint64_t)T + key, a.thr) ? a.inv_keep : 0.f;
-        ds = p * (dP[i] * mk - g.D[bh * T + qi]);
-        p *= mk;
+    for (int c = 0; c < 4; ++c) {
+      const int q0 = qb * AT_TILE + 8 * c + 4 * hh;  // rows crow(4c + e, hh) = q0 + e
+      const float4 g4 = *reinterpret_cast<const float4*>(s_gate + q0);
+      const float4 l4 = *reinterpret_cast<const float4*>(s_lse + q0);
+      const float4 d4 = *reinterpret_cast<const float4*>(s_D + q0);
+      const float gv[4] = {g4.x, g4.y, g4.z, g4.w}, lv[4] = {l4.x, l4.y, l4.z, l4.w};
+      const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * c + e, qi = q0 + e;
+        float p = 0.f, ds = 0.f;
+        if (qi < T && kvalid) {
+          const float sc = fmaf(S[i], a.scale, gv[e] * pbcol[(int64_t)qi * a.ldpb]);
+          p = __expf(sc - lv[e]);
+          float mk = 1.f;
+          if (kDrop) mk = drop_keep(seed, kbase + (uint64_t)(qi * T), a.thr) ? a.inv_keep : 0.f;
+          ds = p * (dP[i] * mk - dd[e]);
+          p *= mk;
+        }
+        P[i] = p;
+        dS[i] = ds;
       }
-      P[i] = p;
-      dS[i] = ds;
     }
-    __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 xp = pack8(P + 8 * s), xs = pack8(dS + 8 * s);
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
-        dvacc[db] = mfma32(xp, read_t(s_dot, db * 32 + r, s, hh), dvacc[db]);
-        dkacc[db] = mfma32(xs, read_t(s_qt, db * 32 + r, s, hh), dkacc[db]);
-      }
-    }
-    __syncthreads();
-  }
-  for (int src = 1; src < NS; ++src) {
-    __syncthreads();
-    if (w == src) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s_acc[0][i][lane] = dkacc[0][i];
-        s_acc[1][i][lane] = dkacc[1][i];
-        s_acc[2][i][lane] = dvacc[0][i];
-        s_acc[3][i][lane] = dvacc[1][i];
-      }
-    }
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        dkacc[0][i] += s_acc[0][i][lane];
-        dkacc[1][i] += s_acc[1][i][lane];
-        dvacc[0][i] += s_acc[2][i][lane];
-        dvacc[1][i] += s_acc[3][i][lane];
+        dvacc[db] = mfma32(xp, read_tr(dOs, qb * AT_TILE, db * 32, s, lane), dvacc[db]);
+        dkacc[db] = mfma32(xs, read_tr(Qs, qb * AT_TILE, db * 32, s, lane), dkacc[db]);
       }
     }
   }
-  if (w != 0) return;
   // Z[key][d]: col = d (lane), row = key (registers)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -364,111 +405,6 @@ __global__ __launch_bounds__(64 * NS) void attn_bwd_dkdv_kernel(AttnArgs a, Attn
   }
 }
 
-// NS waves per block share one 32-query tile and split its key tiles; dQ / dgate partials are
-// summed through LDS at the end.
-template <bool kDrop, int NS>
-__global__ __launch_bounds__(64 * NS) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs g,
-                                                              __hip_bfloat16* __restrict__ dq, int64_t ldg,
-                                                              float* __restrict__ dgate) {
-  __shared__ __bf16 s_kt_all[NS][AT_DH][AT_LDP];
-  __shared__ float s_acc[2][16][64];
-  __shared__ float s_dg[64];
-  const int w = threadIdx.x >> 6;
-  __bf16 (*s_kt)[AT_LDP] = s_kt_all[w];
-  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  const int qb = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
-  const int T = a.T, H = a.H;
-  const int qi = qb * AT_TILE + r;
-  const bool qvalid = qi < T;
-  const int qc = qvalid ? qi : T - 1;
-  const int64_t col0 = (int64_t)head * AT_DH;
-  bf16x8 qf[4], dof[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = load8(a.q + ((int64_t)b * T + qc) * a.ldq + col0 + 16 * s + 8 * hh, qvalid);
-    dof[s] = load8(g.dO + ((int64_t)b * T + qc) * g.lddo + col0 + 16 * s + 8 * hh, qvalid);
-  }
-  const int64_t bh = (int64_t)b * H + head;
-  const float gq = a.gate[((int64_t)b * T + qc) * H + head];
-  const float lq = g.lse[bh * T + qc];
-  const float Dq = g.D[bh * T + qc];
-  const float* pbrow = a.pb + ((int64_t)head * T + qc) * T;
-  const uint64_t seed = kDrop ? attn_seed(a.seed_dev, a.salt) : 0;
-  const uint64_t ibase = ((uint64_t)bh * T + qc) * (uint64_t)T;
-  f32x16 dqacc[2] = {zero16(), zero16()};
-  float dg = 0.f;
-  const int nkb = (T + AT_TILE - 1) / AT_TILE;
-  const int niter = (nkb + NS - 1) / NS;
-  for (int it = 0; it < niter; ++it) {
-    const int kb = w + NS * it;
-    const int kr = kb * AT_TILE + r;
-    const bool krv = kr < T;
-    bf16x8 kfr[4];
-    f32x16 S = zero16(), dP = zero16();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kfr[s] = load8(a.k + ((int64_t)b * T + kr) * a.ldk + col0 + 16 * s + 8 * hh, krv);
-      const bf16x8 vfr = load8(a.v + ((int64_t)b * T + kr) * a.ldv + col0 + 16 * s + 8 * hh, krv);
-      S = mfma32(kfr[s], qf[s], S);
-      dP = mfma32(vfr, dof[s], dP);
-    }
-    stage_t(s_kt, kfr, r, hh);
-    float dS[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = kb * AT_TILE + crow(i, hh);
-      float ds = 0.f;
-      if (key < T && qvalid) {
-        const float pbv = pbrow[key];
-        const float p = __expf(fmaf(S[i], a.scale, gq * pbv) - lq);
-        float mk = 1.f;
-        if (kDrop) mk = drop_keep(seed, ibase + key, a.thr) ? a.inv_keep : 0.f;
-        ds = p * (dP[i] * mk - Dq);
-        dg = fmaf(ds, pbv, dg);
-      }
-      dS[i] = ds;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 xs = pack8(dS + 8 * s);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) dqacc[db] = mfma32(read_t(s_kt, db * 32 + r, s, hh), xs, dqacc[db]);
-    }
-    __syncthreads();
-  }
-  for (int src = 1; src < NS; ++src) {
-    __syncthreads();
-    if (w == src) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s_acc[0][i][lane] = dqacc[0][i];
-        s_acc[1][i][lane] = dqacc[1][i];
-      }
-      s_dg[lane] = dg;
-    }
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        dqacc[0][i] += s_acc[0][i][lane];
-        dqacc[1][i] += s_acc[1][i][lane];
-      }
-      dg += s_dg[lane];
-    }
-  }
-  if (w != 0) return;
-  dg += __shfl_xor(dg, 32, 64);
-  if (qvalid) {
-    __hip_bfloat16* row = dq + ((int64_t)b * T + qi) * ldg + col0;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) row[db * 32 + crow(i, hh)] = __float2bfloat16(dqacc[db][i] * a.scale);
-    if (hh == 0) dgate[((int64_t)b * T + qi) * H + head] = dg;
-  }
-}
-
 // element-wise dropout mask of the same hash (tests only): keep[b, h, i, j] in {0, 1}
 __global__ void attn_mask_kernel(const int64_t* seed_dev, int salt, uint32_t thr, uint8_t* keep, int64_t n) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -476,8 +412,8 @@ __global__ void attn_mask_kernel(const int64_t* seed_dev, int salt, uint32_t thr
 }
 
 inline AttnArgs make_args(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                          const float* gate, const float* pb, const int64_t* seed_dev, int salt, float p_drop,
-                          float scale, int B, int T, int H) {
+                          const float* gate, const float* pb, int64_t ldpb, const int64_t* seed_dev, int salt,
+                          float p_drop, float scale, int B, int T, int H) {
   AttnArgs a;
   a.q = (const __hip_bfloat16*)q;
   a.k = (const __hip_bfloat16*)k;
@@ -487,6 +423,7 @@ inline AttnArgs make_args(const void* q, int64_t ldq, const void* k, int64_t ldk
   a.ldv = ldv;
   a.gate = gate;
   a.pb = pb;
+  a.ldpb = ldpb;
   a.seed_dev = seed_dev;
   a.salt = salt;
   const double t = (double)p_drop * 4294967296.0;
@@ -511,61 +448,90 @@ static bool attn_ok(const void* q, int64_t ldq, const void* k, int64_t ldk, cons
          ldv >= (int64_t)H * AT_DH;
 }
 
-extern "C" int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                            const float* gate, const float* pos_bias, const int64_t* seed_dev, int salt,
-                            float p_drop, float scale, void* o, int64_t ldo, float* lse, int B, int T, int H,
-                            int head_dim, void* stream) {
-  RDX_REQUIRE(attn_ok(q, ldq, k, ldk, v, ldv, B, T, H) && gate && pos_bias && o && lse && ldo >= (int64_t)H * AT_DH);
-  RDX_REQUIRE(p_drop >= 0.f && p_drop < 1.f && (p_drop == 0.f || seed_dev));
-  if (head_dim != AT_DH) return RDX_EUNSUPPORTED;
-  const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, pos_bias, seed_dev, salt, p_drop, scale, B, T, H);
-  dim3 grid((T + AT_TILE - 1) / AT_TILE, H, B);
-  if (a.thr)
-    hipLaunchKernelGGL((attn_fwd_kernel<true, AT_NS_FWD>), grid, dim3(64 * AT_NS_FWD), 0, as_stream(stream), a,
-                       (__hip_bfloat16*)o, ldo, lse);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<false, AT_NS_FWD>), grid, dim3(64 * AT_NS_FWD), 0, as_stream(stream), a,
-                       (__hip_bfloat16*)o, ldo, lse);
+static bool pb_ok(const float* pb, int64_t ldpb, int T) {
+  return ((uintptr_t)pb & 15) == 0 && ldpb >= (int64_t)((T + AT_TILE - 1) / AT_TILE) * AT_TILE && ldpb % 4 == 0;
+}
+
+// the dK/dV kernel's images and row scalars exceed the default 64 KB dynamic-LDS cap at T = 256
+static int attn_allow_lds(const void* fn, bool& done) {
+  if (done) return RDX_OK;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return (int)e;
+  done = true;
+  return RDX_OK;
+}
+
+template <bool kDrop>
+static int launch_fwd(dim3 grid, size_t lds, hipStream_t st, const AttnArgs& a, __hip_bfloat16* o, int64_t ldo,
+                      float* lse) {
+  static bool done = false;
+  const int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_fwd_kernel<kDrop>), done);
+  if (rc != RDX_OK) return rc;
+  hipLaunchKernelGGL((attn_fwd_kernel<kDrop>), grid, dim3(AT_WAVES * 64), lds, st, a, o, ldo, lse);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
 
+template <bool kDrop>
+static int launch_bwd(dim3 grid, size_t lds_dq, size_t lds_kv, hipStream_t st, const AttnArgs& a,
+                      const AttnBwdArgs& g, const __hip_bfloat16* o, int64_t ldo, __hip_bfloat16* dq,
+                      __hip_bfloat16* dk, __hip_bfloat16* dv, int64_t ldg, float* dgate) {
+  static bool done_dq = false, done_kv = false;
+  int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<kDrop>), done_dq);
+  if (rc != RDX_OK) return rc;
+  rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<kDrop>), done_kv);
+  if (rc != RDX_OK) return rc;
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<kDrop>), grid, dim3(AT_WAVES * 64), lds_dq, st, a, g, o, ldo, dq, ldg,
+                     dgate);
+  RDX_LAUNCH_CHECK();
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<kDrop>), grid, dim3(AT_WAVES * 64), lds_kv, st, a, g, dk, dv, ldg);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+extern "C" int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                            const float* gate, const float* pos_bias, int64_t ldpb, const int64_t* seed_dev,
+                            int salt, float p_drop, float scale, void* o, int64_t ldo, float* lse, int B, int T, int H,
+                            int head_dim, void* stream) {
+  RDX_REQUIRE(attn_ok(q, ldq, k, ldk, v, ldv, B, T, H) && gate && pos_bias && o && lse && ldo >= (int64_t)H * AT_DH);
+  RDX_REQUIRE(pb_ok(pos_bias, ldpb, T));
+  RDX_REQUIRE(p_drop >= 0.f && p_drop < 1.f && (p_drop == 0.f || seed_dev));
+  if (head_dim != AT_DH || T > AT_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
+  const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, pos_bias, ldpb, seed_dev, salt, p_drop, scale, B, T, H);
+  const int nt = (T + AT_TILE - 1) / AT_TILE;
+  const dim3 grid((nt + AT_WAVES - 1) / AT_WAVES, H, B);
+  const size_t lds = 2 * (size_t)nt * AT_TILE_BYTES;
+  return a.thr ? launch_fwd<true>(grid, lds, as_stream(stream), a, (__hip_bfloat16*)o, ldo, lse)
+               : launch_fwd<false>(grid, lds, as_stream(stream), a, (__hip_bfloat16*)o, ldo, lse);
+}
+
 extern "C" int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                            const float* gate, const float* pos_bias, const int64_t* seed_dev, int salt,
-                            float p_drop, float scale, const void* o, int64_t ldo, const float* lse,
+                            const float* gate, const float* pos_bias, int64_t ldpb, const int64_t* seed_dev,
+                            int salt, float p_drop, float scale, const void* o, int64_t ldo, const float* lse,
                             const void* dout, int64_t lddo, float* D, void* dq, void* dk, void* dv, int64_t ldg,
                             float* dgate, int B, int T, int H, int head_dim, void* stream) {
   RDX_REQUIRE(attn_ok(q, ldq, k, ldk, v, ldv, B, T, H) && gate && pos_bias && o && lse && dout && D);
-  RDX_REQUIRE(dq && dk && dv && dgate && ldg >= (int64_t)H * AT_DH && ldg % 8 == 0 && lddo % 8 == 0);
+  RDX_REQUIRE(pb_ok(pos_bias, ldpb, T));
+  RDX_REQUIRE(dq && dk && dv && dgate && ldg >= (int64_t)H * AT_DH && ldg % 8 == 0 && lddo % 8 == 0 && ldo % 8 == 0);
+  RDX_REQUIRE(((uintptr_t)o & 15) == 0 && ((uintptr_t)dout & 15) == 0);
   RDX_REQUIRE(p_drop >= 0.f && p_drop < 1.f && (p_drop == 0.f || seed_dev));
-  if (head_dim != AT_DH) return RDX_EUNSUPPORTED;
-  const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, pos_bias, seed_dev, salt, p_drop, scale, B, T, H);
-  hipStream_t st = as_stream(stream);
-  const int64_t nrow = (int64_t)B * T * H;
-  hipLaunchKernelGGL(attn_bwd_dot_kernel, dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, st,
-                     (const __hip_bfloat16*)dout, lddo, (const __hip_bfloat16*)o, ldo, D, B, T, H);
-  RDX_LAUNCH_CHECK();
-  AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
-  dim3 grid((T + AT_TILE - 1) / AT_TILE, H, B);
-  if (a.thr) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, AT_NS_DKDV>), grid, dim3(64 * AT_NS_DKDV), 0, st, a, g,
-                       (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<true, AT_NS_DQ>), grid, dim3(64 * AT_NS_DQ), 0, st, a, g,
-                       (__hip_bfloat16*)dq, ldg, dgate);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, AT_NS_DKDV>), grid, dim3(64 * AT_NS_DKDV), 0, st, a, g,
-                       (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<false, AT_NS_DQ>), grid, dim3(64 * AT_NS_DQ), 0, st, a, g,
-                       (__hip_bfloat16*)dq, ldg, dgate);
-  }
-  RDX_LAUNCH_CHECK();
-  return RDX_OK;
+  if (head_dim != AT_DH || T > AT_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
+  const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, pos_bias, ldpb, seed_dev, salt, p_drop, scale, B, T, H);
+  const AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
+  const int nt = (T + AT_TILE - 1) / AT_TILE;
+  const dim3 grid((nt + AT_WAVES - 1) / AT_WAVES, H, B);
+  const size_t lds_dq = 2 * (size_t)nt * AT_TILE_BYTES;
+  const size_t lds_kv = lds_dq + 3 * (size_t)nt * AT_TILE * sizeof(float);
+  return a.thr ? launch_bwd<true>(grid, lds_dq, lds_kv, as_stream(stream), a, g, (const __hip_bfloat16*)o, ldo,
+                                  (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg, dgate)
+               : launch_bwd<false>(grid, lds_dq, lds_kv, as_stream(stream), a, g, (const __hip_bfloat16*)o, ldo,
+                                   (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg, dgate);
 }
 
 extern "C" int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n,
                                      void* stream) {
   RDX_REQUIRE(seed_dev && keep && n > 0 && p_drop >= 0.f && p_drop < 1.f);
-  const AttnArgs a = make_args(nullptr, 0, nullptr, 0, nullptr, 0, nullptr, nullptr, seed_dev, salt, p_drop, 1.f, 1, 1, 1);
+  const AttnArgs a = make_args(nullptr, 0, nullptr, 0, nullptr, 0, nullptr, nullptr, 0, seed_dev, salt, p_drop, 1.f, 1, 1, 1);
   hipLaunchKernelGGL(attn_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), seed_dev,
                      salt, a.thr, keep, n);
   RDX_LAUNCH_CHECK();

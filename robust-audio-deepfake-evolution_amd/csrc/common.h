@@ -69,9 +69,10 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 }
 // dropout keep decision for element index idx = ((b*H + h)*T + i)*T + j
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  uint32_t h = fmix32((uint32_t)idx * 0x9E3779B1u ^ (uint32_t)seed);
-  h = fmix32(h ^ (uint32_t)(idx >> 32) ^ ((uint32_t)(seed >> 32) * 0x85ebca6bu));
-  return h >= thr;
+  // one murmur3 finaliser over the (bijectively) mixed 64-bit index and seed
+  const uint32_t x = (((uint32_t)idx ^ (uint32_t)seed) * 0x9E3779B1u) ^ (uint32_t)(idx >> 32) ^
+                     ((uint32_t)(seed >> 32) * 0x85ebca6bu);
+  return fmix32(x) >= thr;
 }
 __device__ __forceinline__ uint64_t attn_seed(const int64_t* seed_dev, int salt) {
   return (uint64_t)seed_dev[0] * 0x9E3779B97F4A7C15ull + (uint64_t)(uint32_t)salt * 0xD1B54A32D192ED03ull;

@@ -18,13 +18,14 @@ constexpr int SINC_T3 = 256;  // pooled outputs per block (= threads)
 
 __global__ __launch_bounds__(SINC_T3) void sincconv_absmaxpool_kernel(
     const float* __restrict__ x, int64_t len, const float* __restrict__ filters, int channels, int K,
-    int mask_lo, int mask_hi, const int32_t* __restrict__ mask_dev, float* __restrict__ out, int64_t T3, int C3) {
+    int mask_lo, int mask_hi, const int32_t* __restrict__ mask_dev, int mask_stride, float* __restrict__ out,
+    int64_t T3, int C3) {
   extern __shared__ float s_x[];
-  if (mask_dev != nullptr) {  // band mask read from device memory (HIP-graph replayable)
-    mask_lo = mask_dev[0];
-    mask_hi = mask_dev[1];
-  }
   const int b = blockIdx.y;
+  if (mask_dev != nullptr) {  // band mask read from device memory (HIP-graph replayable), per utterance
+    mask_lo = mask_dev[(int64_t)b * mask_stride];
+    mask_hi = mask_dev[(int64_t)b * mask_stride + 1];
+  }
   const int64_t t3_0 = (int64_t)blockIdx.x * SINC_T3;
   const int64_t base = 3 * t3_0;                 // first conv time of the block
   const int win = 3 * SINC_T3 + K - 1;
@@ -83,15 +84,17 @@ extern "C" int rdx_sincconv_absmaxpool_fwd(const float* x, int64_t batch, int64_
   dim3 grid((unsigned)((T3 + SINC_T3 - 1) / SINC_T3), (unsigned)batch);
   size_t smem = sizeof(float) * (3 * SINC_T3 + ksize - 1 + 2);
   hipLaunchKernelGGL(sincconv_absmaxpool_kernel, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
-                     filters, channels, ksize, mask_lo, mask_hi, (const int32_t*)nullptr, out, T3, C3);
+                     filters, channels, ksize, mask_lo, mask_hi, (const int32_t*)nullptr, 0, out, T3, C3);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
 
 extern "C" int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch, int64_t len,
                                                    const float* filters, int channels, int ksize,
-                                                   const int32_t* mask_dev, float* out, void* stream) {
+                                                   const int32_t* mask_dev, int mask_stride, float* out,
+                                                   void* stream) {
   RDX_REQUIRE(x && filters && out && mask_dev && batch > 0 && channels >= 3 && ksize > 0 && len >= ksize);
+  RDX_REQUIRE(mask_stride == 0 || mask_stride == 2);
   RDX_REQUIRE(batch <= 65535);
   const int64_t T3 = (len - ksize + 1) / 3;
   const int C3 = channels / 3;
@@ -100,7 +103,7 @@ extern "C" int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch
   dim3 grid((unsigned)((T3 + SINC_T3 - 1) / SINC_T3), (unsigned)batch);
   size_t smem = sizeof(float) * (3 * SINC_T3 + ksize - 1 + 2);
   hipLaunchKernelGGL(sincconv_absmaxpool_kernel, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
-                     filters, channels, ksize, 0, 0, mask_dev, out, T3, C3);
+                     filters, channels, ksize, 0, 0, mask_dev, mask_stride, out, T3, C3);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

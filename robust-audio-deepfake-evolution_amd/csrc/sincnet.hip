@@ -240,6 +240,89 @@ __global__ __launch_bounds__(SN_THREADS) void tail_bwd_kernel(const T* __restric
   flush_channel_sums<1>(acc, c0, has, C, sums);
 }
 
+// Block 0 of the residual stack (the only block with one input channel): the input gradient and the
+// weight gradients of conv1 (2 x 3, padding (1, 1)) and conv_downsample (1 x 3, padding (0, 1)) in ONE
+// pass over the two output gradients, instead of MIOpen's two backward-data convolutions with a single
+// output channel (an implicit GEMM with N = 1, ~0.5 ms each at B = 8) and two weight-gradient passes:
+//   dx[n,h,w]      = sum_c [ sum_{kh,kw} dc[n, h+1-kh, w+1-kw, c] W1[c,kh,kw] + sum_kw di[n, h, w+1-kw, c] Wd[c,kw] ]
+//   dW1[c,kh,kw]  += x[n,h,w] dc[n, h+1-kh, w+1-kw, c],    dWd[c,kw] += x[n,h,w] di[n, h, w+1-kw, c]
+// Output columns outside [0, W) are the zero padding; conv1's output has H + 1 rows, so row h+1-kh always
+// exists. Lane = (input pixel, 8 channels): the four lanes of a pixel add their dx partials with two
+// xor-shuffles; each lane's 72 weight-gradient sums are reduced per block in LDS and written as one partial
+// row per block (the caller sums the rows: no same-address atomics across blocks).
+constexpr int B0_C = 32;
+constexpr int B0_TAPS = 9;  // conv1 taps kh * 3 + kw, then conv_downsample taps 6 + kw
+constexpr int B0_BLOCKS = 1024;
+
+__global__ __launch_bounds__(SN_THREADS) void b0_bwd_kernel(const __hip_bfloat16* __restrict__ x,
+                                                            const __hip_bfloat16* __restrict__ dc,
+                                                            const __hip_bfloat16* __restrict__ di,
+                                                            const float* __restrict__ w1, const float* __restrict__ wd,
+                                                            float* __restrict__ dx, float* __restrict__ part,
+                                                            int64_t npix, int H, int W) {
+  __shared__ float red[B0_C * B0_TAPS];
+  for (int i = threadIdx.x; i < B0_C * B0_TAPS; i += SN_THREADS) red[i] = 0.f;
+  const int cg = threadIdx.x & 3;  // channels 8 cg .. 8 cg + 7
+  float wt[SN_VEC][B0_TAPS], acc[SN_VEC][B0_TAPS];
+#pragma unroll
+  for (int k = 0; k < SN_VEC; ++k) {
+    const int c = SN_VEC * cg + k;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) wt[k][t] = w1[c * 6 + t];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) wt[k][6 + t] = wd[c * 3 + t];
+#pragma unroll
+    for (int t = 0; t < B0_TAPS; ++t) acc[k][t] = 0.f;
+  }
+  const int64_t step = (int64_t)gridDim.x * (SN_THREADS / 4);
+  for (int64_t q = (int64_t)blockIdx.x * (SN_THREADS / 4) + (threadIdx.x >> 2); q < npix; q += step) {
+    const int64_t nh = q / W;  // n * H + h
+    const int w = (int)(q - nh * W);
+    const int64_t n = nh / H;
+    const float xq = __bfloat162float(x[q]);
+    float pdx = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int64_t orow = (nh + n + 1 - kh) * W;  // conv1 output row (n, h + 1 - kh) of H + 1
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int wo = w + 1 - kw;
+        if (wo < 0 || wo >= W) continue;
+        float v[SN_VEC];
+        Vec8<__hip_bfloat16>::load(dc + (orow + wo) * B0_C + SN_VEC * cg, v);
+#pragma unroll
+        for (int k = 0; k < SN_VEC; ++k) {
+          pdx = fmaf(v[k], wt[k][kh * 3 + kw], pdx);
+          acc[k][kh * 3 + kw] = fmaf(xq, v[k], acc[k][kh * 3 + kw]);
+        }
+      }
+    }
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int wo = w + 1 - kw;
+      if (wo < 0 || wo >= W) continue;
+      float v[SN_VEC];
+      Vec8<__hip_bfloat16>::load(di + (nh * W + wo) * B0_C + SN_VEC * cg, v);
+#pragma unroll
+      for (int k = 0; k < SN_VEC; ++k) {
+        pdx = fmaf(v[k], wt[k][6 + kw], pdx);
+        acc[k][6 + kw] = fmaf(xq, v[k], acc[k][6 + kw]);
+      }
+    }
+    pdx += __shfl_xor(pdx, 1, 64);
+    pdx += __shfl_xor(pdx, 2, 64);
+    if (cg == 0) dx[q] = pdx;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SN_VEC; ++k)
+#pragma unroll
+    for (int t = 0; t < B0_TAPS; ++t) atomicAdd(&red[(SN_VEC * cg + k) * B0_TAPS + t], acc[k][t]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < B0_C * B0_TAPS; i += SN_THREADS)
+    part[(int64_t)blockIdx.x * B0_C * B0_TAPS + i] = red[i];
+}
+
 inline unsigned sn_grid(int64_t n, int cvec) {
   // enough blocks to fill 256 CUs several times; keeps gridDim*256 a multiple of cvec (256 % cvec == 0)
   int64_t blocks = (n + SN_THREADS - 1) / SN_THREADS;
@@ -317,6 +400,24 @@ extern "C" int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax
   const int64_t nout = rows * Wo * cvec;
   SN_DISPATCH(dtype, hipLaunchKernelGGL(tail_bwd_kernel<T>, dim3(sn_grid(nout, cvec)), dim3(SN_THREADS), 0,
                                         as_stream(stream), (const T*)dy, argmax, (T*)dx, dbias, nout, Wo, W, cvec, C));
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+extern "C" int rdx_sincnet_b0_nblk(int64_t npix) {
+  const int64_t b = (npix + SN_THREADS / 4 - 1) / (SN_THREADS / 4);
+  return (int)(b < 1 ? 1 : (b > B0_BLOCKS ? B0_BLOCKS : b));
+}
+
+extern "C" int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di, const float* w1, const float* wd,
+                                  float* dx, float* part, int N, int H, int W, int C, void* stream) {
+  RDX_REQUIRE(x && dc && di && w1 && wd && dx && part && N > 0 && H > 0 && W > 0);
+  RDX_REQUIRE(((uintptr_t)dc & 15) == 0 && ((uintptr_t)di & 15) == 0);
+  if (C != B0_C) return RDX_EUNSUPPORTED;
+  const int64_t npix = (int64_t)N * H * W;
+  hipLaunchKernelGGL(b0_bwd_kernel, dim3(rdx_sincnet_b0_nblk(npix)), dim3(SN_THREADS), 0, as_stream(stream),
+                     (const __hip_bfloat16*)x, (const __hip_bfloat16*)dc, (const __hip_bfloat16*)di, w1, wd, dx, part,
+                     npix, H, W);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

@@ -58,7 +58,8 @@ SIGNATURES = {
     "rdx_version": (ctypes.c_char_p, []),
     "rdx_strerror": (ctypes.c_char_p, [c_int]),
     "rdx_sincconv_absmaxpool_fwd": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
-    "rdx_sincconv_absmaxpool_fwd_devmask": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_vp, c_vp, c_vp]),
+    "rdx_sincconv_absmaxpool_fwd_devmask": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_vp, c_int, c_vp,
+                                                    c_vp]),
     "rdx_dwconv_bidir_fwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_dwconv_bidir_bwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                      c_int, c_int, c_int, c_int, c_int, c_vp]),
@@ -85,9 +86,13 @@ SIGNATURES = {
     "rdx_bnselu_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
     "rdx_res_tail_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_res_tail_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
-    "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp,
+    "rdx_sincnet_b0_nblk": (c_int, [c_i64]),
+    "rdx_sincnet_b0_bwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_posconv_fwd": (c_int, [c_vp] * 5 + [c_int, c_int, c_vp]),
+    "rdx_posconv_bwd": (c_int, [c_vp] * 4 + [c_int, c_int, c_vp]),
+    "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_f32, c_vp,
                              c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp]),
-    "rdx_attn_bwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp,
+    "rdx_attn_bwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_f32, c_vp,
                              c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int,
                              c_int, c_vp]),
     "rdx_attn_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_vp]),

@@ -23,14 +23,26 @@ CAPTURE_TIMING = None
 
 
 class GraphTimer:
-    """Per-launch-site accumulators [ticks, count] in device memory, filled by captured stamps."""
+    """Per-launch-site accumulators [ticks, count] in device memory, filled by captured stamps. Only the
+    first `per_graph` launch sites of each kernel in each captured graph are stamped: the sites of one
+    kernel in one graph have the same shape, and every stamp is itself a ~4.5 us graph node."""
 
-    def __init__(self, device, capacity=1024):
+    def __init__(self, device, capacity=1024, per_graph=2):
         self.device = torch.device(device)
         self.acc = torch.zeros(capacity, 2, dtype=torch.int64, device=self.device)
         self.sites = []                       # (name, work) per slot
+        self.per_graph = per_graph
+        self._in_graph = {}
+
+    def new_graph(self):
+        """Call before capturing each graph."""
+        self._in_graph = {}
 
     def slot(self, name, work):
+        n = self._in_graph.get(name, 0)
+        if n >= self.per_graph:
+            return None
+        self._in_graph[name] = n + 1
         if len(self.sites) >= self.acc.shape[0]:
             raise RuntimeError("GraphTimer: out of slots")
         self.sites.append((name, float(work)))
@@ -69,8 +81,9 @@ class _timed:
 
     def __enter__(self):
         if CAPTURE_TIMING is not None and torch.cuda.is_current_stream_capturing():
-            self.site = CAPTURE_TIMING.slot(self.name, self.work)
-            check(lib().rdx_timestamp_acc(_p(self.site), -1, _stream(self.t)), "timestamp")
+            self.site = CAPTURE_TIMING.slot(self.name, self.work)   # None: this site is not sampled
+            if self.site is not None:
+                check(lib().rdx_timestamp_acc(_p(self.site), -1, _stream(self.t)), "timestamp")
         elif TIMING is not None:
             self.reg = TIMING
             s = torch.cuda.current_stream(self.t.device)
@@ -138,9 +151,13 @@ def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
     out = torch.empty(B, C // 3, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
     with _timed("sincconv_absmaxpool", x, sinc_flops(B, C, K, L)):
         if mask_dev is not None:
-            assert mask_dev.dtype == torch.int32 and mask_dev.numel() >= 2 and mask_dev.is_cuda
-            check(lib().rdx_sincconv_absmaxpool_fwd_devmask(_p(x), B, L, _p(filters), C, K, _p(mask_dev), _p(out),
-                                                            _stream(x)), "sincconv_absmaxpool_fwd_devmask")
+            # int32 [2] (one mask for the batch) or [B, 2] (one per utterance)
+            per_utt = mask_dev.dim() == 2
+            assert mask_dev.dtype == torch.int32 and mask_dev.is_cuda and mask_dev.is_contiguous()
+            assert (mask_dev.shape == (B, 2)) if per_utt else mask_dev.numel() >= 2
+            check(lib().rdx_sincconv_absmaxpool_fwd_devmask(_p(x), B, L, _p(filters), C, K, _p(mask_dev),
+                                                            2 if per_utt else 0, _p(out), _stream(x)),
+                  "sincconv_absmaxpool_fwd_devmask")
         else:
             check(lib().rdx_sincconv_absmaxpool_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi),
                                                     _p(out), _stream(x)), "sincconv_absmaxpool_fwd")
@@ -470,12 +487,104 @@ class ResTail(torch.autograd.Function):
         return dx, dx, dbias
 
 
+class Block0Convs(torch.autograd.Function):
+    """conv1 (2x3, padding (1, 1)) and conv_downsample (1x3, padding (0, 1)) of SincNet block 0, whose input
+    has ONE channel (Residual_block.forward, src/models/DualStreamSEMamba.py:182-200): forward on MIOpen in
+    bf16 (as autocast runs them), backward (dx, d conv1.weight, d conv_downsample.weight) in one HIP pass
+    (rdx_sincnet_b0_bwd) instead of two single-output-channel backward-data and two weight-gradient
+    convolutions."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd):
+        _require_gpu(x)
+        xb = x.to(torch.bfloat16)
+        w1b, wdb = w1.to(torch.bfloat16), wd.to(torch.bfloat16)
+        c = torch.nn.functional.conv2d(xb, w1b, None, 1, (1, 1))
+        idn = torch.nn.functional.conv2d(xb, wdb, None, 1, (0, 1))
+        ctx.save_for_backward(xb, w1b, wdb)
+        ctx.meta = (w1.shape, wd.shape, x.dtype)
+        return c, idn
+
+    @staticmethod
+    def backward(ctx, dc, di):
+        xb, w1b, wdb = ctx.saved_tensors
+        w1_shape, wd_shape, x_dtype = ctx.meta
+        N, _, H, W = xb.shape
+        C = w1_shape[0]
+        dc = _nhwc(dc.to(torch.bfloat16))
+        di = _nhwc(di.to(torch.bfloat16))
+        xc = xb.contiguous(memory_format=torch.channels_last)      # one channel: [N, H, W] in memory
+        w1f = w1b.float().contiguous()                               # the bf16 weights the forward used
+        wdf = wdb.float().contiguous()
+        dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
+        part = torch.empty(lib().rdx_sincnet_b0_nblk(N * H * W), C * 9, device=xb.device, dtype=torch.float32)
+        with _timed("sincnet_b0_bwd", dc, 2 * (dc.numel() + di.numel()) + 4 * dx.numel() + 2 * xc.numel()):
+            check(lib().rdx_sincnet_b0_bwd(_p(xc), _p(dc), _p(di), _p(w1f), _p(wdf), _p(dx), _p(part), N, H, W, C,
+                                           _stream(dc)), "sincnet_b0_bwd")
+        dw = part.sum(0).view(C, 9)
+        return dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape)
+
+
+# ------------------------------------------------------------ WavLM positional convolution ----
+def posconv_weights(weight):
+    """Conv weight [1024, 64, 128] (weight_norm applied) -> the two bf16 operand layouts of csrc/posconv.hip:
+    wk [16][128][64 n][64 c] = W[g*64+n, c, k] (forward) and wkt [16][128][64 c][64 n] = W[g*64+n, c, 127-k]
+    (input gradient)."""
+    W = weight.detach().reshape(16, 64, 64, 128)                             # [g, n, c, k]
+    wk = W.permute(0, 3, 1, 2).contiguous().to(torch.bfloat16)
+    wkt = W.flip(-1).permute(0, 3, 2, 1).contiguous().to(torch.bfloat16)
+    return wk, wkt
+
+
+class PosConv(torch.autograd.Function):
+    """gelu(conv1d(h, W, bias, padding=64, groups=16)[..., :T]) on bf16 [B, T, 1024] token-major rows: the
+    WavLM positional embedding (HF WavLMPositionalConvEmbedding) with frozen W / bias, as one MFMA launch
+    (rdx_posconv_fwd); the backward returns the input gradient only (rdx_posconv_bwd)."""
+
+    @staticmethod
+    def forward(ctx, h, wk, wkt, bias):
+        _require_gpu(h)
+        B, T, E = h.shape
+        if E != 1024:
+            raise ValueError("radhip posconv: 1024 channels (16 groups of 64) required")
+        h = h.to(torch.bfloat16).contiguous()
+        bias = bias.detach().float().contiguous()
+        y = torch.empty_like(h)
+        u = torch.empty_like(h)
+        with _timed("posconv_fwd", h, 2.0 * B * T * E * 64 * 128):
+            check(lib().rdx_posconv_fwd(_p(h), _p(wk), _p(bias), _p(y), _p(u), B, T, _stream(h)), "posconv_fwd")
+        ctx.save_for_backward(u, wkt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        u, wkt = ctx.saved_tensors
+        B, T, E = u.shape
+        dy = dy.to(torch.bfloat16).contiguous()
+        dh = torch.empty_like(u)
+        with _timed("posconv_bwd", dy, 2.0 * B * T * E * 64 * 128):
+            check(lib().rdx_posconv_bwd(_p(dy), _p(u), _p(wkt), _p(dh), B, T, _stream(dy)), "posconv_bwd")
+        return dh, None, None, None
+
+
 # ---------------------------------------------------------------- WavLM gated attention -------
 def _ld(t):
     """Row stride of a [B, T, E] view whose last dim is contiguous (e.g. a column slice of q|k|v)."""
     if t.dim() != 3 or t.stride(2) != 1 or t.stride(0) != t.shape[1] * t.stride(1):
         raise ValueError("radhip attention: expected a [B, T, E] row view with unit column stride")
     return t.stride(1)
+
+
+def pad_position_bias(pb):
+    """[H, T, T] -> [H, T, 32*ceil(T/32)] fp32, zero-padded rows (the attention kernels read each key
+    tile's position bias with aligned float4 loads)."""
+    H, T, T2 = pb.shape
+    ld = -(-T2 // 32) * 32
+    if T2 == ld and pb.is_contiguous():
+        return pb
+    out = torch.zeros(H, T, ld, device=pb.device, dtype=torch.float32)
+    out[:, :, :T2] = pb
+    return out
 
 
 class GatedAttention(torch.autograd.Function):
@@ -493,12 +602,13 @@ class GatedAttention(torch.autograd.Function):
         if pos_bias.requires_grad:
             raise ValueError("radhip attention: the position bias must be frozen")
         gate = gate.contiguous().float()
-        pb = pos_bias.detach().contiguous().float()
+        pb = pad_position_bias(pos_bias.detach().float())
         o = torch.empty(B, T, E, device=q.device, dtype=q.dtype)
         lse = torch.empty(B, H, T, device=q.device, dtype=torch.float32)
         sd = seed if seed is not None else torch.zeros(1, dtype=torch.int64, device=q.device)
         with _timed("attn_fwd", q, 2.0 * 2 * B * H * T * T * 64):
-            check(lib().rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), _p(sd), int(salt),
+            check(lib().rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), pb.shape[2],
+                                     _p(sd), int(salt),
                                      float(p_drop), 0.125, _p(o), E, _p(lse), B, T, H, 64, _stream(q)), "attn_fwd")
         ctx.save_for_backward(q, k, v, gate, pb, sd, o, lse)
         ctx.p, ctx.salt = float(p_drop), int(salt)
@@ -515,7 +625,8 @@ class GatedAttention(torch.autograd.Function):
         dk, dv = torch.empty_like(dq), torch.empty_like(dq)
         dgate = torch.empty(B, T, H, device=q.device, dtype=torch.float32)
         with _timed("attn_bwd", q, 2.0 * 5 * B * H * T * T * 64):
-            check(lib().rdx_attn_bwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), _p(sd), ctx.salt,
+            check(lib().rdx_attn_bwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), pb.shape[2],
+                                     _p(sd), ctx.salt,
                                      ctx.p, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D), _p(dq), _p(dk), _p(dv), E,
                                      _p(dgate), B, T, H, 64, _stream(q)), "attn_bwd")
         return dq, dk, dv, dgate, None, None, None, None

@@ -11,7 +11,11 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import BnSelu, ResTail, sincconv_absmaxpool
+from .ops import Block0Convs, BnSelu, ResTail, sincconv_absmaxpool
+
+
+def _bf16_autocast(x):
+    return x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
 
 def mel_edges(out_channels, sample_rate, nfft=512):
@@ -115,13 +119,19 @@ class Residual_block(nn.Module):
             # NHWC fused epilogues (csrc/sincnet.hip): conv1's bias is folded into the frozen-BN+SELU pass,
             # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass
             bn = self.bn2
-            c = F.conv2d(x, self.conv1.weight, None, self.conv1.stride, self.conv1.padding)
+            idn = None
+            if self.first and self.downsample and x.shape[1] == 1 and _bf16_autocast(x):
+                # one input channel: both convs' backward in one HIP pass (radhip.ops.Block0Convs)
+                c, idn = Block0Convs.apply(x, self.conv1.weight, self.conv_downsample.weight)
+            else:
+                c = F.conv2d(x, self.conv1.weight, None, self.conv1.stride, self.conv1.padding)
             out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, torch.rsqrt(bn.running_var + bn.eps),
                                bn.weight, bn.bias)
             a = F.conv2d(out, self.conv2.weight, None, self.conv2.stride, self.conv2.padding)
             if self.downsample:
-                idn = F.conv2d(x, self.conv_downsample.weight, None, self.conv_downsample.stride,
-                               self.conv_downsample.padding)
+                if idn is None:
+                    idn = F.conv2d(x, self.conv_downsample.weight, None, self.conv_downsample.stride,
+                                   self.conv_downsample.padding)
                 bias = self.conv2.bias + self.conv_downsample.bias
             else:
                 idn, bias = x, self.conv2.bias

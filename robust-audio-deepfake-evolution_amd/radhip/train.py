@@ -617,7 +617,10 @@ class GraphedMicroStep:
         torch.cuda.current_stream(tr.device).wait_stream(side)
         torch.cuda.synchronize(tr.device)
         gs = []
+        from . import ops
         for k in ((0, 1) if self.adv else (0,)):
+            if ops.CAPTURE_TIMING is not None:
+                ops.CAPTURE_TIMING.new_graph()
             g = torch.cuda.CUDAGraph()
             # one private memory pool per graph (sharing one pool between the clean and the adversarial
             # graph corrupted bias-gradient reductions of the clean graph on ROCm 7 / torch 2.10)

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import wavlm_fused
-from .ops import GatedAttention
+from .ops import GatedAttention, PosConv, posconv_weights
 
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
 # restated, not verifiable offline: parity unpinned for those regularisers)
@@ -200,6 +200,7 @@ class PositionalConvEmbedding(nn.Module):
         self.conv = nn.utils.parametrizations.weight_norm(conv, name="weight", dim=2)
         self.remove = 1 if k % 2 == 0 else 0
         self.act = _act(cfg.feat_extract_activation)
+        self.act_name = cfg.feat_extract_activation
 
     def _weight(self):
         """weight_norm(v, g, dim=2). The WavLM encoder is frozen in Phase 6, so the normalised weight is
@@ -216,8 +217,25 @@ class PositionalConvEmbedding(nn.Module):
             self._wkey = key
         return self._w
 
+    def _fused_ok(self, x):
+        """bf16 CUDA step with the WavLM-Large geometry and frozen weights -> csrc/posconv.hip (one MFMA launch
+        each way instead of MIOpen's per-utterance im2col + GEMM + col2im)."""
+        c = self.conv
+        return (x.is_cuda and x.dim() == 3 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and c.in_channels == 1024
+                and c.out_channels == 1024 and c.groups == 16 and c.kernel_size[0] == 128 and self.remove == 1
+                and self.act_name == "gelu" and os.environ.get("RADHIP_FUSED_POSCONV", "1") != "0"
+                and not any(p.requires_grad for p in c.parameters()))
+
     def forward(self, x):
         c = self.conv
+        if self._fused_ok(x):
+            w = self._weight()
+            key = (w.data_ptr(), getattr(self, "_wkey", None))
+            if getattr(self, "_pc_key", None) != key:
+                self._pc = posconv_weights(w)
+                self._pc_key = key
+            return PosConv.apply(x, self._pc[0], self._pc[1], c.bias)
         y = F.conv1d(x.transpose(1, 2), self._weight(), c.bias, c.stride, c.padding, c.dilation, c.groups)
         if self.remove:
             y = y[:, :, :-self.remove]
@@ -397,7 +415,9 @@ class Encoder(nn.Module):
             states.append(h)
             if self.training and self.keep_dev is not None and i > 0 and p > 0:
                 hn, pos = run(i, layer, h, pos)
-                h = torch.where(self.keep_dev[i], hn, h)
+                # keep_dev: [num_layers] (one draw for the batch) or [B, num_layers] (one row per utterance)
+                kp = self.keep_dev[i] if self.keep_dev.dim() == 1 else self.keep_dev[:, i].view(-1, 1, 1)
+                h = torch.where(kp, hn, h)
                 continue
             # HF draws torch.rand([]) for EVERY layer (train or eval) and skips when training, i > 0 and
             # draw < layerdrop; the same CPU-RNG consumption is kept here
@@ -452,6 +472,12 @@ class WavLMEncoderModel(nn.Module):
         # features equal the clean pass's. cnn_reuse = "store" keeps them, "use" reuses them (exact).
         self.cnn_reuse = None
         self._cnn_feats = None
+        # window mode (radhip/window.py): a frozen-CNN feature tensor handed in for this call, and
+        # per-group leaf copies of the feature_projection parameters (K tuples (ln_w, ln_b, proj_w,
+        # proj_b)); group k of the batch goes through copy k, so the batched clean pass yields each
+        # micro-batch's own feature_projection gradient (the FGM attack needs the running sums)
+        self.cnn_feats_given = None
+        self.fp_groups = None
 
     def _cnn_frozen(self):
         return not self.feature_extractor.training and not any(p.requires_grad for p in self.feature_extractor.parameters())
@@ -459,7 +485,9 @@ class WavLMEncoderModel(nn.Module):
     def forward(self, input_values, output_hidden_states=True, layerdrop=None):
         x = input_values
         frozen = self._cnn_frozen()
-        if frozen and self.cnn_reuse == "use" and self._cnn_feats is not None:
+        if frozen and self.cnn_feats_given is not None:
+            feats = self.cnn_feats_given
+        elif frozen and self.cnn_reuse == "use" and self._cnn_feats is not None:
             if self._cnn_feats[0] != (x.data_ptr(), tuple(x.shape), x.dtype):
                 raise RuntimeError("WavLM CNN feature reuse: the adversarial pass got a different input")
             feats = self._cnn_feats[1]
@@ -471,7 +499,15 @@ class WavLMEncoderModel(nn.Module):
         else:
             feats = self.feature_extractor(x)
         feats = feats.transpose(1, 2)
-        h = self.feature_projection(feats)
+        if self.fp_groups is not None:
+            fp = self.feature_projection
+            K = len(self.fp_groups)
+            parts = []
+            for xk, (lw, lb, pw, pb) in zip(feats.chunk(K, dim=0), self.fp_groups):
+                parts.append(F.linear(F.layer_norm(xk, xk.shape[-1:], lw, lb, fp.layer_norm.eps), pw, pb))
+            h = fp.dropout(torch.cat(parts, dim=0))
+        else:
+            h = self.feature_projection(feats)
         c = self.config
         if self.training and getattr(c, "apply_spec_augment", True) and c.mask_time_prob > 0:
             B, T, _ = h.shape

@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from ._lib import check, lib
-from .ops import _p, _stream, _timed
+from .ops import _p, _stream, _timed, pad_position_bias
 
 E_FUSED = 1024
 
@@ -152,7 +152,7 @@ class WavLMLayerFn(torch.autograd.Function):
         zseed = sd if sd is not None else torch.zeros(1, dtype=torch.int64, device=dev)
         with _timed("attn_fwd", hf, 2.0 * 2 * B * H * T * T * 64):
             check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(pb),
-                                     _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse), B, T, H, 64, st),
+                                     pb.shape[2], _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse), B, T, H, 64, st),
                   "attn_fwd")
         aout = F.linear(o, cache.wo, cache.bo)
         h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -204,7 +204,7 @@ class WavLMLayerFn(torch.autograd.Function):
         dgate = torch.empty(M, H, device=dev, dtype=torch.float32)
         with _timed("attn_bwd", hf, 2.0 * 5 * B * H * T * T * 64):
             check(lib().rdx_attn_bwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(pb),
-                                     _p(zseed), int(index), p_attn, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D),
+                                     pb.shape[2], _p(zseed), int(index), p_attn, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D),
                                      _p(dqkv), _off(dqkv, E), _off(dqkv, 2 * E), 3 * E, _p(dgate), B, T, H, 64, st),
                   "attn_bwd")
         dx1 = torch.mm(dqkv, cache.wext)                                     # [M, E + 2r]
@@ -242,7 +242,7 @@ class FusedEncoderRunner:
         key = (T, emb.data_ptr(), emb._version)
         if key != self.pb_key:
             with torch.no_grad():
-                self.pb = self.encoder.layers[0].attention.compute_bias(T, device).float().contiguous()
+                self.pb = pad_position_bias(self.encoder.layers[0].attention.compute_bias(T, device).float())
             self.pb_key = key
         return self.pb
 

@@ -1,0 +1,251 @@
+"""Accumulation-window execution of the Phase-6 step (same math as train_epoch, src/main.py:998-1126).
+
+Within one gradient-accumulation window of K micro-batches the parameters do not change: FGM perturbs
+feature_projection and restores it before the next micro-batch, and the optimizer steps only at the
+end. So the K CLEAN passes are independent of each other and of the adversarial passes, and run here
+as ONE batched forward/backward over K*B utterances (every norm is per-utterance: BN frozen, LN/SE/
+Mamba per sample). What the FGM chain needs from them is each micro-batch's own feature_projection
+gradient: group k of the batch runs feature_projection through its own leaf copy of those four
+tensors, so after the batched backward the copies hold g_1..g_K. The K ADVERSARIAL passes stay
+sequential, exactly as the reference orders them:
+    for k: fp.grad += g_k; FGM.attack() (accumulated grad, incl. adversarial passes < k); adv pass k
+           (B utterances, the clean pass's frozen-CNN features of group k); FGM.restore()
+then one optimizer step. Per-call random decisions (SincConv band mask, SpecAugment, LayerDrop,
+mixup) are drawn on the host in the reference's per-micro-batch order and staged into device
+buffers; the clean pass reads them per utterance row. With HIP graphs the window is 1 + K replays.
+"""
+import numpy as np
+import torch
+
+from . import ops
+from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay
+from .wavlm import compute_time_mask
+
+
+class WindowStep:
+    def __init__(self, trainer, batch, K=None, graphs=True, max_len=MAX_LEN):
+        tr = trainer
+        m = tr.model
+        dev = tr.device
+        self.tr, self.B, self.K = tr, int(batch), int(K or tr.accum)
+        if self.K < 1:
+            raise ValueError("window needs K >= 1")
+        N = self.K * self.B
+        self.N = N
+        self.graphs_on = graphs
+        self.x = torch.zeros(N, max_len, device=dev)
+        self.ya = torch.zeros(N, dtype=torch.long, device=dev)
+        self.yb = torch.zeros(N, dtype=torch.long, device=dev)
+        self.lam = torch.ones(self.K, device=dev)
+        self.conv = m.sinc_stream.conv_time
+        self.core = m.wavlm_stream._core()
+        cfg = self.core.config
+        T = max_len
+        for k, st in zip(cfg.conv_kernel, cfg.conv_stride):
+            T = (T - k) // st + 1
+        self.T = T
+        nl = len(self.core.encoder.layers)
+        self.nl = nl
+        self.spec_on = bool(getattr(cfg, "apply_spec_augment", True)) and cfg.mask_time_prob > 0
+        # device draws: clean rows (one per utterance) and one set per adversarial pass
+        self.c_mask = torch.zeros(N, 2, dtype=torch.int32, device=dev)
+        self.c_tmask = torch.zeros(N, T, dtype=torch.bool, device=dev)
+        self.c_keep = torch.ones(N, nl, dtype=torch.bool, device=dev)
+        self.a_mask = torch.zeros(self.K, 2, dtype=torch.int32, device=dev)
+        self.a_tmask = torch.zeros(self.K, self.B, T, dtype=torch.bool, device=dev)
+        self.a_keep = torch.ones(self.K, nl, dtype=torch.bool, device=dev)
+        self.adv = tr.fgm is not None
+        # feature_projection: the real tensors and K leaf copies whose grads live in one flat buffer
+        fp = self.core.feature_projection
+        self.fp_real = [fp.layer_norm.weight, fp.layer_norm.bias, fp.projection.weight, fp.projection.bias]
+        n = sum(p.numel() for p in self.fp_real)
+        self.fp_grad = torch.zeros(self.K, n, device=dev)
+        self.fp_copies = []
+        for k in range(self.K):
+            group, off = [], 0
+            for p in self.fp_real:
+                c = torch.empty_like(p, requires_grad=True)
+                c.grad = self.fp_grad[k, off:off + p.numel()].view_as(p)
+                off += p.numel()
+                group.append(c)
+            self.fp_copies.append(tuple(group))
+        self._flat_copies = [c for g in self.fp_copies for c in g]
+        self._flat_real = [p for _ in range(self.K) for p in self.fp_real]
+        self.ring = _PinnedRing(8192 + 2 * N * 8 + N * (T + nl + 16) + self.K * (self.B * T + nl + 64))
+        self.graphs = None
+        self.feats = None
+        self._host = None
+        self.reset_host()
+
+    # ------------------------------------------------------------------ host staging ----------
+    def reset_host(self):
+        N, K, B, T, nl = self.N, self.K, self.B, self.T, self.nl
+        self._host = dict(ya=np.zeros(N, np.int64), yb=np.zeros(N, np.int64), lam=np.ones(K, np.float32),
+                          c_mask=np.zeros((N, 2), np.int32), c_tmask=np.zeros((N, T), bool),
+                          c_keep=np.ones((N, nl), bool), a_mask=np.zeros((K, 2), np.int32),
+                          a_tmask=np.zeros((K, B, T), bool), a_keep=np.ones((K, nl), bool))
+        self._added = 0
+
+    def _draw_pass(self):
+        """One forward's host draws in the reference order: SpecAugment (numpy), LayerDrop (torch CPU),
+        SincConv band mask (numpy + python random)."""
+        c = self.core.config
+        tm = (compute_time_mask(self.B, self.T, c.mask_time_prob, c.mask_time_length, c.mask_time_min_masks)
+              if self.spec_on else np.zeros((self.B, self.T), dtype=bool))
+        p = c.layerdrop
+        keep = np.ones(self.nl, dtype=bool)
+        r = np.array([float(torch.rand([])) for _ in range(self.nl)])
+        if p > 0:
+            keep[1:] = ~(r[1:] < p)
+        lo, hi = self.conv.draw_mask() if self.tr.freq_aug else (0, 0)
+        return tm, keep, np.array([lo, hi], dtype=np.int32)
+
+    def xslot(self, k):
+        """Row block of micro-batch k: Augmenter.run(..., out=window.xslot(k))."""
+        return self.x[k * self.B:(k + 1) * self.B]
+
+    def add(self, k, y, lam=1.0, perm=None):
+        """Register micro-batch k (already mixed into xslot(k)) and make its clean-pass and
+        adversarial-pass draws, in the order the reference makes them."""
+        h, B = self._host, self.B
+        y = np.asarray(y, dtype=np.int64).reshape(-1)
+        if y.shape[0] != B or k != self._added:
+            raise ValueError("window: micro-batches must be added in order with B labels each")
+        sl = slice(k * B, (k + 1) * B)
+        h["ya"][sl] = y
+        h["yb"][sl] = y[np.asarray(perm)] if perm is not None else y
+        h["lam"][k] = lam
+        tm, keep, mk = self._draw_pass()
+        h["c_tmask"][sl], h["c_keep"][sl], h["c_mask"][sl] = tm, keep[None, :], mk[None, :]
+        if self.adv:
+            tm, keep, mk = self._draw_pass()
+            h["a_tmask"][k], h["a_keep"][k], h["a_mask"][k] = tm, keep, mk
+        self._added += 1
+
+    def _stage(self):
+        h = self._host
+        self.ring.stage([(h["ya"], self.ya), (h["yb"], self.yb), (h["lam"], self.lam), (h["c_mask"], self.c_mask),
+                         (h["c_tmask"], self.c_tmask), (h["c_keep"], self.c_keep), (h["a_mask"], self.a_mask),
+                         (h["a_tmask"], self.a_tmask), (h["a_keep"], self.a_keep)])
+
+    # ------------------------------------------------------------------ passes ----------------
+    def _loss(self, out, k):
+        tr, B = self.tr, self.B
+        lam = self.lam[k]
+        ya, yb = self.ya[k * B:(k + 1) * B], self.yb[k * B:(k + 1) * B]
+        return lam * tr.criterion(out, ya) + (1.0 - lam) * tr.criterion(out, yb)
+
+    def _clean_pass(self):
+        tr, core, B = self.tr, self.core, self.B
+        with torch.no_grad():
+            torch._foreach_copy_(self._flat_copies, self._flat_real)
+            self.fp_grad.zero_()
+        core.fp_groups = self.fp_copies
+        core.cnn_reuse = "store"
+        self.conv.mask_dev = self.c_mask
+        core.time_mask_dev = self.c_tmask
+        core.encoder.keep_dev = self.c_keep
+        try:
+            with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32,
+                                cache_enabled=False):
+                _, out = tr.model(self.x, Freq_aug=tr.freq_aug)
+                loss = sum(self._loss(out[k * B:(k + 1) * B], k) for k in range(self.K)) / tr.accum
+            tr.scaler.scale(loss).backward()
+            tr.loss_sum.add_(loss.detach().double() * (tr.accum * B))
+        finally:
+            core.fp_groups = None
+            self.feats = core._cnn_feats[1] if core._cnn_feats is not None else None
+            core.cnn_reuse = None
+
+    def _adv_pass(self, k):
+        tr, core, B = self.tr, self.core, self.B
+        self.conv.mask_dev = self.a_mask[k]
+        core.time_mask_dev = self.a_tmask[k]
+        core.encoder.keep_dev = self.a_keep[k]
+        if self.feats is not None:
+            core.cnn_feats_given = self.feats[k * B:(k + 1) * B]
+        try:
+            with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32,
+                                cache_enabled=False):
+                _, out = tr.model(self.x[k * B:(k + 1) * B], Freq_aug=tr.freq_aug)
+                adv = self._loss(out, k) / tr.accum
+            tr.scaler.scale(adv).backward()
+        finally:
+            core.cnn_feats_given = None
+
+    def _unbind(self):
+        self.conv.mask_dev = None
+        self.core.time_mask_dev = None
+        self.core.encoder.keep_dev = None
+
+    def _prefix_grad(self, k):
+        """feature_projection.grad += g_k (micro-batch k's clean gradient)."""
+        torch._foreach_add_([p.grad for p in self.fp_real], list(self.fp_copies[k][i].grad for i in range(4)))
+
+    def _adv_chain(self, run_adv):
+        tr = self.tr
+        for k in range(self.K):
+            self._prefix_grad(k)
+            if self.adv:
+                tr.fgm.attack()
+                run_adv(k)
+                tr.fgm.restore()
+
+    # ------------------------------------------------------------------ driver ----------------
+    def capture(self, warmup=2):
+        tr = self.tr
+        check_graph_memset_replay(tr.device)
+        tr.train_mode()
+        saved_loss = tr.loss_sum.clone()
+        self._stage()
+        side = torch.cuda.Stream(device=tr.device)
+        side.wait_stream(torch.cuda.current_stream(tr.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._clean_pass()
+                self._adv_chain(self._adv_pass)
+        torch.cuda.current_stream(tr.device).wait_stream(side)
+        torch.cuda.synchronize(tr.device)
+
+        def new_graph():
+            if ops.CAPTURE_TIMING is not None:   # bench.py: stamp the first launch sites of each graph
+                ops.CAPTURE_TIMING.new_graph()
+            return torch.cuda.CUDAGraph()
+        g0 = new_graph()
+        with torch.cuda.graph(g0):
+            self._clean_pass()
+        gadv = []
+        if self.adv:
+            for k in range(self.K):
+                g = new_graph()
+                with torch.cuda.graph(g):
+                    self._adv_pass(k)
+                gadv.append(g)
+        torch.cuda.synchronize(tr.device)
+        self._unbind()
+        tr.grads.zero()
+        self.fp_grad.zero_()
+        tr.loss_sum.copy_(saved_loss)
+        self.graphs = (g0, gadv)
+
+    def run(self, last_in_epoch=False):
+        """Execute the window (every micro-batch added); ends with the optimizer step."""
+        if self._added != self.K:
+            raise RuntimeError(f"window has {self._added} of {self.K} micro-batches")
+        tr = self.tr
+        tr.train_mode()
+        self._stage()
+        if self.graphs_on:
+            if self.graphs is None:
+                self.capture()
+            g0, gadv = self.graphs
+            g0.replay()
+            self._adv_chain(lambda k: gadv[k].replay())
+        else:
+            self._clean_pass()
+            self._adv_chain(self._adv_pass)
+            self._unbind()
+        tr.micro += self.K
+        tr.n_seen += self.N
+        tr.optimizer_step()
+        self.reset_host()

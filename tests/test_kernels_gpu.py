@@ -362,3 +362,77 @@ def test_gated_attention_matches_torch(p_drop):
         assert torch.equal(o2, o)
         o3 = GatedAttention.apply(q, k, v, gate, pb, seed + 1, p_drop, 3)
         assert not torch.equal(o3, o)
+
+
+@pytest.mark.parametrize("B,T,H", [(1, 33, 2), (3, 64, 1), (1, 256, 2)])
+def test_gated_attention_ragged_lengths(B, T, H):
+    """Sequence lengths with a one-row last tile, an exact tile multiple and the 256-row maximum: forward and
+    gradients against the fp32 torch reference (no dropout)."""
+    from radhip.ops import GatedAttention
+    torch.manual_seed(T)
+    E = H * 64
+    q, k, v = ((0.5 * torch.randn(B, T, E, device=DEV)).to(torch.bfloat16).requires_grad_() for _ in range(3))
+    gate = (torch.rand(B, T, H, device=DEV) * 2).requires_grad_()
+    pb = torch.randn(H, T, T, device=DEV)
+    o = GatedAttention.apply(q, k, v, gate, pb, None, 0.0, 0)
+    go = torch.randn(B, T, E, device=DEV).to(torch.bfloat16)
+    o.backward(go)
+    qr, kr, vr = (t.detach().float().view(B, T, H, 64).transpose(1, 2).requires_grad_() for t in (q, k, v))
+    gr = gate.detach().clone().requires_grad_()
+    s = qr @ kr.transpose(-1, -2) * 0.125 + gr.permute(0, 2, 1).unsqueeze(-1) * pb.unsqueeze(0)
+    orf = (torch.softmax(s, -1) @ vr).transpose(1, 2).reshape(B, T, E)
+    orf.backward(go.float())
+
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+    assert rel(o, orf) < 1e-2
+    assert rel(q.grad, qr.grad.transpose(1, 2).reshape(B, T, E)) < 2e-2
+    assert rel(k.grad, kr.grad.transpose(1, 2).reshape(B, T, E)) < 2e-2
+    assert rel(v.grad, vr.grad.transpose(1, 2).reshape(B, T, E)) < 2e-2
+    assert rel(gate.grad, gr.grad) < 2e-2
+
+
+def test_posconv_matches_torch():
+    """WavLM positional conv (grouped conv1d 16 x 64 channels, 128 taps, padding 64, last frame dropped,
+    GELU; csrc/posconv.hip) vs torch fp32 on the same bf16 operands: output and input gradient."""
+    from radhip.ops import PosConv, posconv_weights
+    torch.manual_seed(0)
+    w = torch.randn(1024, 64, 128, device=DEV) * 0.01
+    bias = torch.randn(1024, device=DEV) * 0.1
+    wk, wkt = posconv_weights(w)
+    wr = w.to(torch.bfloat16).float()
+    for B, T in ((2, 201), (1, 37), (1, 129)):
+        h = torch.randn(B, T, 1024, device=DEV).to(torch.bfloat16).requires_grad_()
+        y = PosConv.apply(h, wk, wkt, bias)
+        go = torch.randn(B, T, 1024, device=DEV).to(torch.bfloat16)
+        y.backward(go)
+        hr = h.detach().float().requires_grad_()
+        yr = F.gelu(F.conv1d(hr.transpose(1, 2), wr, bias, padding=64, groups=16)[:, :, :-1]).transpose(1, 2)
+        yr.backward(go.float())
+        assert y.shape == yr.shape
+        assert ((y.float() - yr).norm() / yr.norm()).item() < 1e-2, (B, T)
+        assert ((h.grad.float() - hr.grad).norm() / hr.grad.norm()).item() < 2e-2, (B, T)
+
+
+def test_sincnet_block0_backward_kernel():
+    """SincNet block-0 convs (one input channel) through radhip.ops.Block0Convs vs torch autograd of the same
+    bf16-rounded convolutions in fp32: dx, d conv1.weight, d conv_downsample.weight."""
+    from radhip.ops import Block0Convs
+    torch.manual_seed(3)
+    N, H, W = 2, 23, 301
+    x = torch.randn(N, 1, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    w1 = (0.3 * torch.randn(32, 1, 2, 3, device=DEV)).requires_grad_()
+    wd = (0.3 * torch.randn(32, 1, 1, 3, device=DEV)).requires_grad_()
+    c, idn = Block0Convs.apply(x, w1, wd)
+    assert c.shape == (N, 32, H + 1, W) and idn.shape == (N, 32, H, W)
+    gc = torch.randn(c.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gi = torch.randn(idn.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    torch.autograd.backward([c, idn], [gc, gi])
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_()
+    w1r = w1.detach().to(torch.bfloat16).float().requires_grad_()
+    wdr = wd.detach().to(torch.bfloat16).float().requires_grad_()
+    cr = F.conv2d(xr, w1r, None, 1, (1, 1))
+    ir = F.conv2d(xr, wdr, None, 1, (0, 1))
+    torch.autograd.backward([cr, ir], [gc.float(), gi.float()])
+    for got, ref in ((x.grad, xr.grad), (w1.grad, w1r.grad), (wd.grad, wdr.grad)):
+        assert ((got.float() - ref).norm() / ref.norm()).item() < 1e-3
