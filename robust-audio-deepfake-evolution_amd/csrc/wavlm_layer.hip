@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
 //   dB_q[e, k] += s sum_m dq[m, e] a_q[m, k]        dA_q[k, e] += sum_m da_q[m, k] drop_q(x1)[m, e]
 // (same for v). Thread = one column e; a block walks WL_LG_ROWS rows, staging the rows' 32 per-row
 // factors (a_q, a_v, da_q, da_v) in LDS, then adds its 32 partial sums with fp32 atomics.
-constexpr int WL_LG_ROWS = 96;
+constexpr int WL_LG_ROWS = 48;
 
 struct LoraGradArgs {
   const __hip_bfloat16* dqkv;  // [M, ldq]: dq at column 0, dv at column 2E
@@ -527,6 +527,7 @@ __global__ __launch_bounds__(256) void wl_lora_grad_kernel(LoraGradArgs a) {
   for (int k = 0; k < R; ++k) bq[k] = bv[k] = aq[k] = av[k] = 0.f;
   const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
   const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
+#pragma unroll 4
   for (int rr = 0; rr < nrow; ++rr) {
     const int64_t m = m0 + rr;
     const float gq = __bfloat162float(a.dqkv[m * a.ldq + e]);

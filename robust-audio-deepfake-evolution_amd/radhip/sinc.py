@@ -3,6 +3,7 @@
 Reference: CONV (src/models/DualStreamSEMamba.py:49-138), Residual_block (:144-200) and
 SincNetEncoder (:206-270), themselves taken from AASIST (models/AASIST.py:325-466).
 """
+import os
 import random
 
 import numpy as np
@@ -120,7 +121,8 @@ class Residual_block(nn.Module):
             # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass
             bn = self.bn2
             idn = None
-            if self.first and self.downsample and x.shape[1] == 1 and _bf16_autocast(x):
+            if (self.first and self.downsample and x.shape[1] == 1 and _bf16_autocast(x)
+                    and os.environ.get("RADHIP_FUSED_B0", "1") != "0"):
                 # one input channel: both convs' backward in one HIP pass (radhip.ops.Block0Convs)
                 c, idn = Block0Convs.apply(x, self.conv1.weight, self.conv_downsample.weight)
             else:
