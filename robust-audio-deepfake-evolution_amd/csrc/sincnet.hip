@@ -247,26 +247,57 @@ __global__ __launch_bounds__(SN_THREADS) void tail_bwd_kernel(const T* __restric
 //   dx[n,h,w]      = sum_c [ sum_{kh,kw} dc[n, h+1-kh, w+1-kw, c] W1[c,kh,kw] + sum_kw di[n, h, w+1-kw, c] Wd[c,kw] ]
 //   dW1[c,kh,kw]  += x[n,h,w] dc[n, h+1-kh, w+1-kw, c],    dWd[c,kw] += x[n,h,w] di[n, h, w+1-kw, c]
 // Output columns outside [0, W) are the zero padding; conv1's output has H + 1 rows, so row h+1-kh always
-// exists. Lane = (input pixel, 8 channels): the four lanes of a pixel add their dx partials with two
-// xor-shuffles; each lane's 72 weight-gradient sums are reduced per block in LDS and written as one partial
-// row per block (the caller sums the rows: no same-address atomics across blocks).
+// exists. A work unit is one utterance x one strip of 64 columns, walked top-down: conv1 output row h+1
+// is loaded once (as the kh = 0 taps of input row h) and kept in registers as the kh = 1 taps of row
+// h+1, so every dc row comes from HBM once. Lane = (column, 4 channels): the eight lanes of a column add
+// their dx partials with three xor-shuffles; the three column taps are loaded from clamped addresses and
+// zeroed by a select (no divergent branch between the loads). Each lane's 36 weight-gradient sums are
+// reduced per block in LDS and written as one partial row per block (the caller sums the rows: no
+// same-address atomics across blocks); blocks without a unit write zeros.
 constexpr int B0_C = 32;
 constexpr int B0_TAPS = 9;  // conv1 taps kh * 3 + kw, then conv_downsample taps 6 + kw
-constexpr int B0_BLOCKS = 1024;
+constexpr int B0_BLOCKS = 4096;
+constexpr int B0_CPL = 4;                         // channels per lane
+constexpr int B0_LPC = B0_C / B0_CPL;             // lanes per column
+constexpr int B0_STRIP = SN_THREADS / B0_LPC;     // columns per unit
+
+__device__ __forceinline__ uint2 b0_tap(const __hip_bfloat16* __restrict__ row, int wo, int W, int cg) {
+  const int wc = wo < 0 ? 0 : (wo >= W ? W - 1 : wo);
+  const uint2 v = *reinterpret_cast<const uint2*>(row + (int64_t)wc * B0_C + B0_CPL * cg);
+  const bool ok = wo >= 0 && wo < W;
+  return ok ? v : make_uint2(0u, 0u);
+}
+
+__device__ __forceinline__ float b0_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float b0_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+// pdx += sum_k v[k] wt[k][t];  acc[k][t] += xq v[k]
+__device__ __forceinline__ void b0_fma(const uint2 v, int t, float xq, const float (&wt)[B0_CPL][B0_TAPS],
+                                       float (&acc)[B0_CPL][B0_TAPS], float& pdx) {
+  const unsigned u[2] = {v.x, v.y};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float a = b0_lo(u[j]), b = b0_hi(u[j]);
+    pdx = fmaf(a, wt[2 * j][t], pdx);
+    pdx = fmaf(b, wt[2 * j + 1][t], pdx);
+    acc[2 * j][t] = fmaf(xq, a, acc[2 * j][t]);
+    acc[2 * j + 1][t] = fmaf(xq, b, acc[2 * j + 1][t]);
+  }
+}
 
 __global__ __launch_bounds__(SN_THREADS) void b0_bwd_kernel(const __hip_bfloat16* __restrict__ x,
                                                             const __hip_bfloat16* __restrict__ dc,
                                                             const __hip_bfloat16* __restrict__ di,
                                                             const float* __restrict__ w1, const float* __restrict__ wd,
-                                                            float* __restrict__ dx, float* __restrict__ part,
-                                                            int64_t npix, int H, int W) {
+                                                            float* __restrict__ dx, float* __restrict__ part, int N,
+                                                            int H, int W) {
   __shared__ float red[B0_C * B0_TAPS];
   for (int i = threadIdx.x; i < B0_C * B0_TAPS; i += SN_THREADS) red[i] = 0.f;
-  const int cg = threadIdx.x & 3;  // channels 8 cg .. 8 cg + 7
-  float wt[SN_VEC][B0_TAPS], acc[SN_VEC][B0_TAPS];
+  const int cg = threadIdx.x & (B0_LPC - 1);  // channels 4 cg .. 4 cg + 3
+  float wt[B0_CPL][B0_TAPS], acc[B0_CPL][B0_TAPS];
 #pragma unroll
-  for (int k = 0; k < SN_VEC; ++k) {
-    const int c = SN_VEC * cg + k;
+  for (int k = 0; k < B0_CPL; ++k) {
+    const int c = B0_CPL * cg + k;
 #pragma unroll
     for (int t = 0; t < 6; ++t) wt[k][t] = w1[c * 6 + t];
 #pragma unroll
@@ -274,50 +305,48 @@ __global__ __launch_bounds__(SN_THREADS) void b0_bwd_kernel(const __hip_bfloat16
 #pragma unroll
     for (int t = 0; t < B0_TAPS; ++t) acc[k][t] = 0.f;
   }
-  const int64_t step = (int64_t)gridDim.x * (SN_THREADS / 4);
-  for (int64_t q = (int64_t)blockIdx.x * (SN_THREADS / 4) + (threadIdx.x >> 2); q < npix; q += step) {
-    const int64_t nh = q / W;  // n * H + h
-    const int w = (int)(q - nh * W);
-    const int64_t n = nh / H;
-    const float xq = __bfloat162float(x[q]);
-    float pdx = 0.f;
+  const int strips = (W + B0_STRIP - 1) / B0_STRIP;
+  const int units = N * strips;
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int n = u / strips;
+    const int w = (u - n * strips) * B0_STRIP + threadIdx.x / B0_LPC;
+    const bool live = w < W;
+    const int wl = live ? w : W - 1;  // dead lanes load a valid column and contribute nothing
+    const __hip_bfloat16* dcn = dc + (int64_t)n * (H + 1) * W * B0_C;
+    const __hip_bfloat16* din = di + (int64_t)n * H * W * B0_C;
+    const int64_t xrow0 = (int64_t)n * H * W;
+    uint2 cur[3];  // conv1 output row h: the kh = 1 taps of input row h
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int64_t orow = (nh + n + 1 - kh) * W;  // conv1 output row (n, h + 1 - kh) of H + 1
+    for (int kw = 0; kw < 3; ++kw) cur[kw] = b0_tap(dcn, wl + 1 - kw, W, cg);
+    for (int h = 0; h < H; ++h) {
+      uint2 nxt[3], dv[3];
+      const __hip_bfloat16* rn = dcn + (int64_t)(h + 1) * W * B0_C;
+      const __hip_bfloat16* ri = din + (int64_t)h * W * B0_C;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) nxt[kw] = b0_tap(rn, wl + 1 - kw, W, cg);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) dv[kw] = b0_tap(ri, wl + 1 - kw, W, cg);
+      const float xq = live ? __bfloat162float(x[xrow0 + (int64_t)h * W + wl]) : 0.f;
+      float pdx = 0.f;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int wo = w + 1 - kw;
-        if (wo < 0 || wo >= W) continue;
-        float v[SN_VEC];
-        Vec8<__hip_bfloat16>::load(dc + (orow + wo) * B0_C + SN_VEC * cg, v);
-#pragma unroll
-        for (int k = 0; k < SN_VEC; ++k) {
-          pdx = fmaf(v[k], wt[k][kh * 3 + kw], pdx);
-          acc[k][kh * 3 + kw] = fmaf(xq, v[k], acc[k][kh * 3 + kw]);
-        }
+        b0_fma(nxt[kw], kw, xq, wt, acc, pdx);     // kh = 0: conv1 output row h + 1
+        b0_fma(cur[kw], 3 + kw, xq, wt, acc, pdx); // kh = 1: conv1 output row h
+        b0_fma(dv[kw], 6 + kw, xq, wt, acc, pdx);  // conv_downsample output row h
       }
-    }
+      pdx += __shfl_xor(pdx, 1, 64);
+      pdx += __shfl_xor(pdx, 2, 64);
+      pdx += __shfl_xor(pdx, 4, 64);
+      if (cg == 0 && live) dx[xrow0 + (int64_t)h * W + w] = pdx;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int wo = w + 1 - kw;
-      if (wo < 0 || wo >= W) continue;
-      float v[SN_VEC];
-      Vec8<__hip_bfloat16>::load(di + (nh * W + wo) * B0_C + SN_VEC * cg, v);
-#pragma unroll
-      for (int k = 0; k < SN_VEC; ++k) {
-        pdx = fmaf(v[k], wt[k][6 + kw], pdx);
-        acc[k][6 + kw] = fmaf(xq, v[k], acc[k][6 + kw]);
-      }
+      for (int kw = 0; kw < 3; ++kw) cur[kw] = nxt[kw];
     }
-    pdx += __shfl_xor(pdx, 1, 64);
-    pdx += __shfl_xor(pdx, 2, 64);
-    if (cg == 0) dx[q] = pdx;
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < SN_VEC; ++k)
+  for (int k = 0; k < B0_CPL; ++k)
 #pragma unroll
-    for (int t = 0; t < B0_TAPS; ++t) atomicAdd(&red[(SN_VEC * cg + k) * B0_TAPS + t], acc[k][t]);
+    for (int t = 0; t < B0_TAPS; ++t) atomicAdd(&red[(B0_CPL * cg + k) * B0_TAPS + t], acc[k][t]);
   __syncthreads();
   for (int i = threadIdx.x; i < B0_C * B0_TAPS; i += SN_THREADS)
     part[(int64_t)blockIdx.x * B0_C * B0_TAPS + i] = red[i];
@@ -405,7 +434,8 @@ extern "C" int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax
 }
 
 extern "C" int rdx_sincnet_b0_nblk(int64_t npix) {
-  const int64_t b = (npix + SN_THREADS / 4 - 1) / (SN_THREADS / 4);
+  // about one block per (utterance, 32-column strip) unit at the bench shapes; the kernel grid-strides over units
+  const int64_t b = (npix + B0_STRIP - 1) / B0_STRIP;
   return (int)(b < 1 ? 1 : (b > B0_BLOCKS ? B0_BLOCKS : b));
 }
 
@@ -417,7 +447,7 @@ extern "C" int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di,
   const int64_t npix = (int64_t)N * H * W;
   hipLaunchKernelGGL(b0_bwd_kernel, dim3(rdx_sincnet_b0_nblk(npix)), dim3(SN_THREADS), 0, as_stream(stream),
                      (const __hip_bfloat16*)x, (const __hip_bfloat16*)dc, (const __hip_bfloat16*)di, w1, wd, dx, part,
-                     npix, H, W);
+                     N, H, W);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

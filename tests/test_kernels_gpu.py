@@ -414,12 +414,13 @@ def test_posconv_matches_torch():
         assert ((h.grad.float() - hr.grad).norm() / hr.grad.norm()).item() < 2e-2, (B, T)
 
 
-def test_sincnet_block0_backward_kernel():
+@pytest.mark.parametrize("N,H,W", [(2, 23, 301), (5, 1, 33), (1, 3, 2)])
+def test_sincnet_block0_backward_kernel(N, H, W):
     """SincNet block-0 convs (one input channel) through radhip.ops.Block0Convs vs torch autograd of the same
-    bf16-rounded convolutions in fp32: dx, d conv1.weight, d conv_downsample.weight."""
+    bf16-rounded convolutions in fp32: dx, d conv1.weight, d conv_downsample.weight. (5, 1, 33) has more
+    (utterance, 32-column strip) units than blocks (the grid-stride path); (1, 3, 2) a strip of 2 columns."""
     from radhip.ops import Block0Convs
     torch.manual_seed(3)
-    N, H, W = 2, 23, 301
     x = torch.randn(N, 1, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
     w1 = (0.3 * torch.randn(32, 1, 2, 3, device=DEV)).requires_grad_()
     wd = (0.3 * torch.randn(32, 1, 1, 3, device=DEV)).requires_grad_()

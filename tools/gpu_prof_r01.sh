@@ -1,6 +1,6 @@
 # Evidence for the bench line: rocprofv3 kernel-trace stats of a short bench run (the same command as the
 # driver's, fewer steps), then HBM traffic of the attention kernels from separate PMC passes (FETCH_SIZE,
-# WRITE_SIZE; one counter group per run) over tools/bench_attn.py at the window's two batch shapes.
+# WRITE_SIZE; one counter group per run) over tools/bench_kernels.py at the window's two batch shapes.
 # Outputs under gpurun_out/$TAG; tools/pmc_traffic.py turns the PMC CSVs into profiles/pmc_traffic.json.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -18,7 +18,7 @@ if [ -z "$NOTRACE" ]; then
 fi
 for B in 8 32; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    B=$B timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d /tmp/pmc_${c}_$B -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_attn.py > $O/attn_${c}_$B.out 2>&1
+    B=$B timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d /tmp/pmc_${c}_$B -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_kernels.py > $O/attn_${c}_$B.out 2>&1
     rc=$?
     echo "PMC $c B=$B EXIT $rc"
     [ $rc -eq 0 ] || exit $rc
