@@ -91,11 +91,13 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
 
 
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_layers_match_fp32_restatement(p):
+@pytest.mark.parametrize("p,B", [(0.0, 2), (0.1, 2), (0.1, 21)])
+def test_fused_layers_match_fp32_restatement(p, B):
+    """B = 21 (M = 4221 rows) takes the LoRA weight-grad kernel's multi-chunk path (2 chunks of 32
+    rows per block, ragged last block); B = 2 the single-chunk path with a ragged last chunk."""
     from radhip import wavlm_fused
     enc = _encoder(p=p).train()
-    B, T, E = 2, 201, 1024
+    T, E = 201, 1024
     torch.manual_seed(1)
     h0 = (0.5 * torch.randn(B, T, E, device=DEV)).requires_grad_(True)
     seed = torch.tensor([12345], dtype=torch.int64, device=DEV)
