@@ -492,9 +492,13 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
 
 // LoRA weight gradients of one layer, ACCUMULATED into the fp32 .grad buffers:
 //   dB_q[e, k] += s sum_m dq[m, e] a_q[m, k]        dA_q[k, e] += sum_m da_q[m, k] drop_q(x1)[m, e]
-// (same for v). Thread = one column e; a block walks WL_LG_ROWS rows, staging the rows' 32 per-row
-// factors (a_q, a_v, da_q, da_v) in LDS, then adds its 32 partial sums with fp32 atomics.
-constexpr int WL_LG_ROWS = 48;
+// (same for v). A block owns 128 columns and 4 * RPW rows: lane = 2 adjacent columns (bf16x2 loads,
+// 256 B per wave-instruction), wave w = RPW consecutive rows whose loads are all issued before the
+// FMAs (no per-row branch: rows past M read row M-1 against zeroed per-row factors). The 4 waves'
+// 32 x 128 partial sums are reduced through LDS, then the block adds 4096 fp32 atomics laid out so
+// each wave-instruction covers 64 consecutive dwords of dA ([r, E]) or dB ([E, r]).
+constexpr int WL_LG_COLS = 128;
+constexpr int WL_LG_PAD = WL_LG_COLS + 1;  // LDS row stride (floats): the dB read walks k
 
 struct LoraGradArgs {
   const __hip_bfloat16* dqkv;  // [M, ldq]: dq at column 0, dv at column 2E
@@ -509,47 +513,100 @@ struct LoraGradArgs {
   int64_t M;
 };
 
-__global__ __launch_bounds__(256) void wl_lora_grad_kernel(LoraGradArgs a) {
-  __shared__ float s_row[WL_LG_ROWS][WL_R2 * 2];
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  const int64_t m0 = (int64_t)blockIdx.y * WL_LG_ROWS;
-  const int nrow = (int)min((int64_t)WL_LG_ROWS, a.M - m0);
-  for (int t = threadIdx.x; t < nrow * 2 * WL_R2; t += 256) {
-    const int rr = t / (2 * WL_R2), c = t % (2 * WL_R2);
-    const int64_t m = m0 + rr;
-    s_row[rr][c] = c < WL_R2 ? __bfloat162float(a.x1[m * a.ldx + WL_E + c])
-                             : __bfloat162float(a.dx1[m * a.ldd + WL_E + c - WL_R2]);
-  }
-  __syncthreads();
+__device__ __forceinline__ float2 bf16x2_at(const __hip_bfloat16* p) {
+  const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+}
+
+template <int RPW>
+__global__ __launch_bounds__(256) void wl_lora_grad_kernel(LoraGradArgs a, int nch) {
+  constexpr int ROWS = 4 * RPW;  // rows per chunk; a block walks nch chunks
+  __shared__ float s_row[2][ROWS][2 * WL_R2];
+  __shared__ float s_part[4][2 * WL_R2][WL_LG_PAD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e0 = blockIdx.x * WL_LG_COLS;
+  const int e = e0 + 2 * lane;
   constexpr int R = WL_R2 / 2;
-  float bq[R], bv[R], aq[R], av[R];
+  float bq[2][R], bv[2][R], aq[2][R], av[2][R];
 #pragma unroll
-  for (int k = 0; k < R; ++k) bq[k] = bv[k] = aq[k] = av[k] = 0.f;
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < R; ++k) bq[c][k] = bv[c][k] = aq[c][k] = av[c][k] = 0.f;
   const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
   const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
-#pragma unroll 4
-  for (int rr = 0; rr < nrow; ++rr) {
-    const int64_t m = m0 + rr;
-    const float gq = __bfloat162float(a.dqkv[m * a.ldq + e]);
-    const float gv = __bfloat162float(a.dqkv[m * a.ldq + 2 * WL_E + e]);
-    const float x = __bfloat162float(a.x1[m * a.ldx + e]);
-    const uint64_t idx = (uint64_t)m * WL_E + e;
-    const float xq = x * drop_scale(a.dq, sq, idx), xv = x * drop_scale(a.dv, sv, idx);
-    const float* f = s_row[rr];
+  for (int ch = 0; ch < nch; ++ch) {
+    const int64_t m0 = ((int64_t)blockIdx.y * nch + ch) * ROWS;
+    float(*srow)[2 * WL_R2] = s_row[ch & 1];
+    for (int t = threadIdx.x; t < ROWS * 2 * WL_R2; t += 256) {
+      const int rr = t / (2 * WL_R2), c = t % (2 * WL_R2);
+      const int64_t m = m0 + rr;
+      float v = 0.f;
+      if (m < a.M)
+        v = c < WL_R2 ? __bfloat162float(a.x1[m * a.ldx + WL_E + c])
+                      : __bfloat162float(a.dx1[m * a.ldd + WL_E + c - WL_R2]);
+      srow[rr][c] = v;
+    }
+    float2 gq[RPW], gv[RPW], xx[RPW];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      bq[k] = fmaf(gq, f[k], bq[k]);
-      bv[k] = fmaf(gv, f[R + k], bv[k]);
-      aq[k] = fmaf(f[2 * R + k], xq, aq[k]);
-      av[k] = fmaf(f[3 * R + k], xv, av[k]);
+    for (int j = 0; j < RPW; ++j) {
+      const int64_t m = min(m0 + w * RPW + j, a.M - 1);
+      gq[j] = bf16x2_at(a.dqkv + m * a.ldq + e);
+      gv[j] = bf16x2_at(a.dqkv + m * a.ldq + 2 * WL_E + e);
+      xx[j] = bf16x2_at(a.x1 + m * a.ldx + e);
+    }
+    __syncthreads();  // srow staged (the other buffer is still read by nobody: one barrier per chunk)
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int rr = w * RPW + j;
+      const uint64_t idx = (uint64_t)min(m0 + rr, a.M - 1) * WL_E + e;
+      const float g_q[2] = {gq[j].x, gq[j].y}, g_v[2] = {gv[j].x, gv[j].y};
+      const float xq[2] = {xx[j].x * drop_scale(a.dq, sq, idx), xx[j].y * drop_scale(a.dq, sq, idx + 1)};
+      const float xv[2] = {xx[j].x * drop_scale(a.dv, sv, idx), xx[j].y * drop_scale(a.dv, sv, idx + 1)};
+      const float* f = srow[rr];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          bq[c][k] = fmaf(g_q[c], f[k], bq[c][k]);
+          bv[c][k] = fmaf(g_v[c], f[R + k], bv[c][k]);
+          aq[c][k] = fmaf(f[2 * R + k], xq[c], aq[c][k]);
+          av[c][k] = fmaf(f[3 * R + k], xv[c], av[c][k]);
+        }
     }
   }
 #pragma unroll
-  for (int k = 0; k < R; ++k) {
-    atomicAdd(a.dBq + (int64_t)e * R + k, a.scale * bq[k]);
-    atomicAdd(a.dBv + (int64_t)e * R + k, a.scale * bv[k]);
-    atomicAdd(a.dAq + (int64_t)k * WL_E + e, aq[k]);
-    atomicAdd(a.dAv + (int64_t)k * WL_E + e, av[k]);
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      s_part[w][k][2 * lane + c] = bq[c][k];
+      s_part[w][R + k][2 * lane + c] = bv[c][k];
+      s_part[w][2 * R + k][2 * lane + c] = aq[c][k];
+      s_part[w][3 * R + k][2 * lane + c] = av[c][k];
+    }
+  __syncthreads();
+  // 4096 outputs: o < 2048 -> dA (kk = o / 128 over aq then av, col = o % 128: lanes contiguous in e);
+  // o >= 2048 -> dB (which = q/v, col = rem / 8, k = rem % 8: lanes contiguous in e * r + k).
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int o = i * 256 + threadIdx.x;
+    int row, col;
+    float* dst;
+    float mul = 1.f;
+    if (o < 2048) {
+      const int kk = o / WL_LG_COLS;
+      col = o % WL_LG_COLS;
+      row = 2 * R + kk;
+      dst = kk < R ? a.dAq + (int64_t)kk * WL_E + e0 + col : a.dAv + (int64_t)(kk - R) * WL_E + e0 + col;
+    } else {
+      const int o2 = o - 2048, which = o2 / (WL_LG_COLS * R), rem = o2 % (WL_LG_COLS * R);
+      col = rem / R;
+      const int k = rem % R;
+      row = which * R + k;
+      dst = (which ? a.dBv : a.dBq) + (int64_t)(e0 + col) * R + k;
+      mul = a.scale;
+    }
+    const float v = s_part[0][row][col] + s_part[1][row][col] + s_part[2][row][col] + s_part[3][row][col];
+    atomicAdd(dst, mul * v);
   }
 }
 
@@ -683,11 +740,16 @@ int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx,
                      float* dbq, float* dav, float* dbv, int64_t M, int E, int r, void* stream) {
   RDX_REQUIRE(dqkv && x1 && dx1 && daq && dbq && dav && dbv && M > 0 && E == WL_E && 2 * r == WL_R2);
   RDX_REQUIRE(ldq >= 3 * (int64_t)E && ldx >= E + 2 * r && ldd >= E + 2 * r);
+  RDX_REQUIRE(ldq % 2 == 0 && ldx % 2 == 0 && ((uintptr_t)dqkv & 3) == 0 && ((uintptr_t)x1 & 3) == 0);
   LoraGradArgs a{reinterpret_cast<const __hip_bfloat16*>(dqkv), ldq, reinterpret_cast<const __hip_bfloat16*>(x1), ldx,
                  reinterpret_cast<const __hip_bfloat16*>(dx1), ldd, mk_drop(seed_dev, salt_q, p_lora),
                  mk_drop(seed_dev, salt_v, p_lora), scale, daq, dbq, dav, dbv, M};
-  const dim3 grid(WL_E / 256, (unsigned)((M + WL_LG_ROWS - 1) / WL_LG_ROWS));
-  hipLaunchKernelGGL(wl_lora_grad_kernel, grid, dim3(256), 0, as_stream(stream), a);
+  // 32-row chunks; a block walks nch of them so the 4096 fp32 atomics it ends with are amortised over
+  // >= 64 rows once M allows (atomics run at ~1.3 TB/s of added bytes chip-wide), keeping >= 400 blocks.
+  const int64_t nchunk = (M + 31) / 32;
+  const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(8, M / 2048));
+  const dim3 grid(WL_E / WL_LG_COLS, (unsigned)((nchunk + nch - 1) / nch));
+  hipLaunchKernelGGL(wl_lora_grad_kernel<8>, grid, dim3(256), 0, as_stream(stream), a, nch);
   RDX_LAUNCH_CHECK();
   return 0;
 }

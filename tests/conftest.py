@@ -53,3 +53,42 @@ REFERENCE = "/root/reference"
 
 def reference_present():
     return os.path.isdir(REFERENCE)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_heartbeat(request):
+    """Long GPU tests (the fp32 accumulation-window test spends minutes in MIOpen's fp32 solver search
+    and three model builds) print nothing while they run; a runner that takes 3 silent minutes for a
+    hang would kill them. Every 45 s this writes one progress line naming the running test to the real
+    stdout (capture suspended) and, on the GPU box, to gpurun_out/pytest_heartbeat.log."""
+    if "gpu" not in request.keywords:
+        yield
+        return
+    import threading
+    import time
+    capman = request.config.pluginmanager.getplugin("capturemanager")
+    stop = threading.Event()
+    t0 = time.time()
+    out_dir = os.path.join(os.environ.get("GRAFT_REPO_ROOT", ROOT), "gpurun_out")
+
+    def beat():
+        while not stop.wait(45.0):
+            line = f"[heartbeat] {request.node.nodeid} running {time.time() - t0:.0f} s\n"
+            try:
+                if os.path.isdir(out_dir):
+                    with open(os.path.join(out_dir, "pytest_heartbeat.log"), "a") as f:
+                        f.write(line)
+                if capman is not None:
+                    with capman.global_and_fixture_disabled():
+                        sys.stdout.write(line)
+                        sys.stdout.flush()
+            except Exception:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        stop.set()
+        th.join()
