@@ -519,7 +519,7 @@ __device__ __forceinline__ float2 bf16x2_at(const __hip_bfloat16* p) {
 }
 
 template <int RPW>
-__global__ __launch_bounds__(256) void wl_lora_grad_kernel(LoraGradArgs a, int nch) {
+__global__ __launch_bounds__(256, 2) void wl_lora_grad_kernel(LoraGradArgs a, int nch) {
   constexpr int ROWS = 4 * RPW;  // rows per chunk; a block walks nch chunks
   __shared__ float s_row[2][ROWS][2 * WL_R2];
   __shared__ float s_part[4][2 * WL_R2][WL_LG_PAD];
