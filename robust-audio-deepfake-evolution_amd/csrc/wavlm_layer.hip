@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
   const float c = a.g.gconst[head], dg = a.dgate[m * (WL_E / 64) + head];
   const float dza = dg * (gb * c - 1.0f) * ga * (1.0f - ga);
   const float dzb = dg * ga * c * gb * (1.0f - gb);
-#pragma unroll
+#pragma unroll 2
   for (int j = 0; j < 8; ++j) {
     const float dz = j < 4 ? dza : dzb;
     const float4* w = reinterpret_cast<const float4*>(a.g.wg + j * 64 + part * 16);
@@ -464,19 +464,24 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
       store16_bf(a.xd + m * WL_E + e0, xq);
       store16_bf(a.xd + (a.M + m) * WL_E + e0, xv);
     }
+    // q and v adapters in separate loops unrolled by 2: a full unroll hoists all 16 A rows (256 floats)
+    // into registers and leaves this memory-bound kernel at one wave per SIMD
 #pragma unroll
-    for (int k = 0; k < WL_R2; ++k) {
-      const float da = __bfloat162float(a.dx1[m * a.ldx + WL_E + k]);
-      const float* arow = k < WL_R2 / 2 ? a.Aq + (int64_t)k * WL_E : a.Av + (int64_t)(k - WL_R2 / 2) * WL_E;
-      const float4* w = reinterpret_cast<const float4*>(arow + e0);
-      float* acc = k < WL_R2 / 2 ? bq : bv;
+    for (int which = 0; which < 2; ++which) {
+      float* acc = which ? bv : bq;
+      const float* A = which ? a.Av : a.Aq;
+#pragma unroll 2
+      for (int k = 0; k < WL_R2 / 2; ++k) {
+        const float da = __bfloat162float(a.dx1[m * a.ldx + WL_E + which * (WL_R2 / 2) + k]);
+        const float4* w = reinterpret_cast<const float4*>(A + (int64_t)k * WL_E + e0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float4 t = w[i];
-        acc[4 * i] += t.x * da;
-        acc[4 * i + 1] += t.y * da;
-        acc[4 * i + 2] += t.z * da;
-        acc[4 * i + 3] += t.w * da;
+        for (int i = 0; i < 4; ++i) {
+          float4 t = w[i];
+          acc[4 * i] += t.x * da;
+          acc[4 * i + 1] += t.y * da;
+          acc[4 * i + 2] += t.z * da;
+          acc[4 * i + 3] += t.w * da;
+        }
       }
     }
 #pragma unroll
