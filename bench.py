@@ -79,7 +79,10 @@ def parse():
     ap.add_argument("--pool", type=int, default=64, help="synthetic utterances resident in HBM per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-microsteps", type=int, default=1)
+    ap.add_argument("--cpu-protocol", default="bounded", choices=["bounded", "full"],
+                    help="bounded: B=2, 1 warm-up + 2 timed steps (~20 s); full: BASELINE.md §3, B=2 and B=8, "
+                         "3 warm-up + 10 timed steps each (~8 min on 16 threads)")
+    ap.add_argument("--cpu-only", action="store_true", help="run only the CPU baseline leg (no GPU)")
     ap.add_argument("--config", default="Phase6_Proposed.conf")
     ap.add_argument("--eager", action="store_true",
                     help="launch the micro-step kernel by kernel instead of replaying it as HIP graphs")
@@ -120,9 +123,14 @@ def build(config, device, layerdrop):
     return model
 
 
-def roofline_from_rows(rows, graphed=False):
+def roofline_from_rows(rows, steps, graphed=False):
+    """The dominant hand-written kernel = largest total time over the timed region (every launch site
+    counted: GraphTimer scales its sampled sites), with its achieved rate over its average launch."""
     if not rows:
         return None, rows
+    for r in rows.values():
+        r["launches_per_step"] = round(r["launches"] / steps, 2)
+        r["ms_per_step"] = r["total_ms"] / steps
     dom = max(rows, key=lambda k: rows[k]["total_ms"])
     r = rows[dom]
     bound, kind = KERNEL_BOUND.get(dom, ("hbm", None))
@@ -143,16 +151,50 @@ def roofline_from_rows(rows, graphed=False):
             "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": dom,
             "avg_launch_ms": round(r["avg_ms"], 5), "work_per_launch": r["avg_work"],
             "work_unit": "FLOP" if bound == "mfma" else "bytes",
+            "launches_per_step": r["launches_per_step"], "ms_per_step": round(r["ms_per_step"], 4),
             "timing": ("device wall-clock stamps (rdx_timestamp_acc) captured around the first 2 launch sites of each "
-                       "kernel in each replayed HIP graph, accumulated over every replay of the timed region") if graphed else
+                       "kernel in each replayed HIP graph (each standing for the graph's same-shape sites of that "
+                       "kernel), accumulated over every replay of the timed region; HIP events on the launch "
+                       "stream for eager launches") if graphed else
                       "HIP events on the launch stream around every launch of the timed region"}
     return roof, rows
 
 
-def cpu_baseline(config, threads, microsteps):
-    """Oracle (CPU restatement, fp32) Phase-6 FGM micro-batch at B=2: RawBoost/codec (numpy), full
-    WavLM-Large (transformers, random init) + SincNet + sequential Bi-Mamba, focal loss, backward,
-    FGM attack + adversarial fwd/bwd + restore, AdamW step."""
+def host_cpu():
+    """(CPU model, physical cores of the machine, logical CPUs this process may run on)."""
+    model, cores = None, set()
+    try:
+        phys = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    cores.add((phys, v))
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, (len(cores) or None), avail
+
+
+def cpu_baseline(config, threads, protocol):
+    """The oracle (CPU restatement, fp32; pinned to the reference by tests/golden) running the Phase-6
+    train step of BASELINE.md §3 on the host cores: per micro-batch RawBoost algo 5 (p 0.8) + codec
+    (p 0.3 x 0.5) in numpy, pad_random to 64 600, mixup, full WavLM-Large (random init) + SincNet +
+    sequential Bi-Mamba, focal loss (alpha 0.9, gamma 2.5), backward, FGM attack (eps 0.5) + adversarial
+    forward/backward + restore; clip 3.0 + AdamW every 4th micro-batch (accumulation 4).
+
+    protocol "full" = BASELINE.md §3: 3 warm-up + 10 timed steps at micro-batch 2 and at 8, a step being
+    one FGM micro-batch step (an optimizer step is 4 of them: the per-utterance rate is the same, and the
+    optimizer-step reading at B = 8 would take ~25 min, past one GPU-box call).
+    protocol "bounded" (bench default): 1 warm-up + 2 timed steps at micro-batch 2 (~20 s)."""
     from oracle import rawboost as orb
     from oracle.data import pad_random
     from oracle.model import OracleModel
@@ -171,30 +213,35 @@ def cpu_baseline(config, threads, microsteps):
     for mod in m.modules():
         if isinstance(mod, torch.nn.BatchNorm2d):
             mod.eval()
-    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5)
-    rng = np.random.default_rng(7)
-    B = 2
-    xs = [np.clip(0.1 * rng.standard_normal(64000), -1, 1) for _ in range(B)]
-    ys = torch.tensor([0, 1])
+    train_params = [p for p in m.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW(train_params, lr=1e-5)
+    rng = np.random.default_rng(1234)
+    pool = np.clip(0.1 * rng.standard_normal((16, 64000)), -1, 1)
+    labels = (rng.random(16) < 0.102).astype(np.int64)
 
     def focal(logits, y, a=0.9, g=2.5):
         lp = torch.log_softmax(logits, 1).gather(1, y[:, None]).squeeze(1)
-        return (-torch.where(y == 0, 1 - a, a) * (1 - lp.exp()) ** g * lp).mean()
+        return (-torch.where(y == 0, 1 - a, a) * (1 - lp.exp()) ** g * lp).sum() / (2 * y.shape[0])
 
-    def one():
+    state = {"micro": 0}
+
+    def step(B):
+        idx = rng.integers(0, len(pool), B)
         batch = []
-        for x in xs:
+        for i in idx:
+            x = pool[i]
             if pyrandom.random() < 0.8:
                 x = orb.process(x, [1, 2, 3, 4])
             if pyrandom.random() < 0.3 and pyrandom.random() < 0.5:
                 x = codec_roundtrip(x, pyrandom.choice([8000, 6000, 4000]))
             batch.append(pad_random(x))
         xb = torch.tensor(np.stack(batch), dtype=torch.float32)
+        ys = torch.from_numpy(labels[idx])
         lam = float(np.random.beta(1, 1))
         perm = torch.randperm(B)
         xb = lam * xb + (1 - lam) * xb[perm]
         _, out = m(xb)
-        loss = lam * focal(out, ys) + (1 - lam) * focal(out, ys[perm])
+        loss = (lam * focal(out, ys) + (1 - lam) * focal(out, ys[perm])) / 4
         loss.backward()
         fp = [p for n, p in m.named_parameters() if "feature_projection" in n]
         bk = [p.data.clone() for p in fp]
@@ -204,24 +251,52 @@ def cpu_baseline(config, threads, microsteps):
                 if nrm != 0 and not torch.isnan(nrm):
                     p.add_(0.5 * p.grad / nrm)
         _, out = m(xb)
-        (lam * focal(out, ys) + (1 - lam) * focal(out, ys[perm])).backward()
+        ((lam * focal(out, ys) + (1 - lam) * focal(out, ys[perm])) / 4).backward()
         with torch.no_grad():
             for p, b in zip(fp, bk):
                 p.copy_(b)
-        torch.nn.utils.clip_grad_norm_([p for p in m.parameters() if p.requires_grad], 3.0)
-        opt.step()
-        opt.zero_grad()
-    t0 = time.perf_counter()
-    for _ in range(microsteps):
-        one()
-    dt = time.perf_counter() - t0
-    return {"value": round(B * microsteps / dt, 4), "unit": "utt/s", "cores": threads, "kind": "port",
-            "sample": f"{microsteps} Phase-6 FGM micro-batch(es) of B={B} (RawBoost/codec numpy, fwd+bwd x2, "
-                      f"AdamW) through the fp32 CPU oracle, {dt:.1f} s on {threads} threads"}
+        state["micro"] += 1
+        if state["micro"] % 4 == 0:
+            torch.nn.utils.clip_grad_norm_(train_params, 3.0)
+            opt.step()
+            opt.zero_grad()
+
+    plan = [(2, 3, 10), (8, 3, 10)] if protocol == "full" else [(2, 1, 2)]
+    runs = []
+    for B, warm, timed in plan:
+        for _ in range(warm):
+            step(B)
+        t0 = time.perf_counter()
+        for _ in range(timed):
+            step(B)
+        dt = time.perf_counter() - t0
+        runs.append({"micro_batch": B, "warmup_steps": warm, "timed_steps": timed, "seconds": round(dt, 2),
+                     "utt_s": round(B * timed / dt, 4)})
+    model_name, phys, avail = host_cpu()
+    best = runs[-1]
+    return {"value": best["utt_s"], "unit": "utt/s", "cores": threads, "kind": "port",
+            "sample": (f"{protocol} protocol: " + "; ".join(
+                f"B={r['micro_batch']}: {r['warmup_steps']} warm-up + {r['timed_steps']} timed FGM micro-batch "
+                f"steps, {r['seconds']} s" for r in runs)
+                + " (fp32 CPU oracle: numpy RawBoost/codec, WavLM-Large + SincNet + Bi-Mamba fwd+bwd x2, "
+                  "AdamW every 4th step)"),
+            "runs": runs, "threads": threads, "cpu_model": model_name, "physical_cores_machine": phys,
+            "logical_cpus_available": avail}
+
+
+def cpu_threads(args):
+    """Threads for the CPU leg: --cpu-threads, else the CPUs this process may use, capped at the GPU box's
+    16-CPU share (OMP_NUM_THREADS is 16 there)."""
+    return args.cpu_threads or min(16, host_cpu()[2])
 
 
 def main():
     args = parse()
+    if args.cpu_only:
+        from radhip.build import load_config
+        res = cpu_baseline(load_config(args.config), cpu_threads(args), args.cpu_protocol)
+        print(json.dumps({"cpu_baseline": res}), flush=True)
+        return
     hb = Heartbeat()
     ws, rank, local = dist_setup()
     dev = torch.device("cuda", local)
@@ -326,7 +401,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
     loss = trainer.epoch_loss()
-    roof, rows = roofline_from_rows(rows, graphed=not args.eager)
+    roof, rows = roofline_from_rows(rows, args.steps, graphed=not args.eager)
     utts = ws * args.steps * args.accum * B
     value = utts / wall_max
     if rank == 0:
@@ -349,9 +424,8 @@ def main():
             "final_loss": round(loss, 6),
         }
         if ws == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 8)
             hb.set("cpu baseline")
-            line["cpu_baseline"] = cpu_baseline(config, threads, args.cpu_microsteps)
+            line["cpu_baseline"] = cpu_baseline(config, cpu_threads(args), args.cpu_protocol)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -19,9 +19,13 @@ Differences, all documented in DESIGN.md:
     per-rank micro-batch is `batch_size`, and eval shards the protocol and all-gathers the scores;
   * the train dataset is decoded natively and augmented on the GPU (radhip.data.TrainFeeder), with
     the reference's per-utterance host RNG order;
-  * torchcontrib SWA: the snapshot average is kept (swa.pth) but bn_update is not run (every BN is
-    frozen in the Phase-5/6 recipe);
-  * checkpoints load with torch.load(weights_only=True); tensorboard scalars are not written.
+  * the optimizer window of `accumulation_steps` micro-batches runs as one batched clean pass plus the
+    sequential FGM passes (radhip/window.py, same math; needs frozen BN) unless --no-window or --eager;
+  * checkpoints load with torch.load(weights_only=True), strictly for --eval / --resume / auto 2021 DF
+    (the reference's strict=False silently drops mismatched keys); tensorboard scalars are not written;
+  * --save_train_state additionally writes weights/train_state_epoch_XXX.pt (last 2 kept) after every
+    epoch: weights, optimizer, scheduler, scaler, EMA, SWA, best metrics, loader generator, host/device
+    RNG states; --resume on such a file continues the run where it stopped.
 """
 import argparse
 import json
@@ -47,9 +51,11 @@ from radhip.data import (Dataset_ASVspoof2019_devNeval, Dataset_ASVspoof2021_eva
 from radhip.evaluation import calculate_EER_2021, calculate_tDCF_EER  # noqa: E402
 from radhip.infer import produce_evaluation_file_sharded  # noqa: E402
 from radhip.train import (Augmenter, GraphedMicroStep, Trainer, build_criterion,  # noqa: E402
-                          total_optimizer_steps)
+                          swa_bn_update, total_optimizer_steps)
+from radhip.window import WindowStep, window_eligible  # noqa: E402
 
 AMP = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+TRAIN_STATE_FORMAT = "radhip-train-state-v1"
 
 
 def set_seed(seed, config):
@@ -105,6 +111,13 @@ class SWA:
             tmp = p.detach().clone()
             p.copy_(b)
             b.copy_(tmp)
+
+    def state_dict(self):
+        return {"n": self.n, "buf": None if self.buf is None else [b.detach().clone() for b in self.buf]}
+
+    def load_state_dict(self, st):
+        self.n = int(st["n"])
+        self.buf = None if st["buf"] is None else [b.to(p.device) for b, p in zip(st["buf"], self.params)]
 
 
 class Runner:
@@ -163,9 +176,14 @@ class Runner:
         if args.pretrained_weights:
             self.log(f"Loading pretrained weights for fine-tuning: {args.pretrained_weights}")
             load_weights(model, args.pretrained_weights, self.device, strict=False)
+        self.resume_state = None
         if args.resume:
             self.log("Resuming from checkpoint: {}".format(args.resume))
-            load_weights(model, args.resume, self.device, strict=True)
+            ck = torch.load(args.resume, map_location=self.device, weights_only=True)
+            if isinstance(ck, dict) and ck.get("format") == TRAIN_STATE_FORMAT:
+                self.resume_state = ck      # full state: restored once the trainer exists (run())
+            else:
+                load_weights(model, args.resume, self.device, strict=True)
         return model
 
     # ------------------------------------------------------------------- eval ------------------
@@ -193,7 +211,7 @@ class Runner:
     def run_eval(self, model):
         args, config = self.args, self.config
         model_path = args.eval_model_weights if args.eval_model_weights is not None else config["model_path"]
-        load_weights(model, model_path, self.device, strict=False)
+        load_weights(model, model_path, self.device, strict=True)
         self.log("Model loaded : {}".format(model_path))
         self.log("Start evaluation...")
         if config.get("is_eval_2021", False):
@@ -219,6 +237,77 @@ class Runner:
         self.tdcf(self.eval_score_path, self.tag / "loaded_model_t-DCF_EER.txt")
 
     # ------------------------------------------------------------------ train ------------------
+    def make_stepper(self, trainer, B):
+        """How micro-batches execute: the accumulation window (HIP graphs, radhip/window.py), the
+        per-micro-batch graphs (GraphedMicroStep), or eager launches."""
+        if self.args.eager:
+            return "eager", None
+        if not self.args.no_window and window_eligible(trainer):
+            w = WindowStep(trainer, B)
+            for k in range(w.K):            # capture needs one staged window of draws
+                w.add(k, np.zeros(B, dtype=np.int64))
+            w.capture()
+            w.reset_host()
+            return "window", w
+        g = GraphedMicroStep(trainer, B)
+        g.capture()
+        return "graph", g
+
+    def train_epoch(self, trainer, stepper, feeder, aug):
+        """One pass of train_epoch (src/main.py:998-1126) over this rank's micro-batches."""
+        kind, st = stepper
+        n_micro = len(feeder)
+        K = st.K if kind == "window" else 1
+        full = (n_micro // K) * K                  # micro-batches that fill whole windows
+        for i, keys in enumerate(feeder.epoch()):
+            flat, offs, lens, y = feeder.load(keys, self.device)
+            plan = aug.draw(lens)
+            lam, perm = trainer.mixup_draw(len(keys))
+            last = i + 1 == n_micro
+            if kind == "window" and i < full:
+                k = i % K
+                aug.run(flat, offs, lens, plan, perm, lam, out=st.xslot(k))
+                st.add(k, y.numpy(), lam, perm)
+                if k == K - 1:
+                    st.run()
+            elif kind == "graph":
+                aug.run(flat, offs, lens, plan, perm, lam, out=st.x)
+                st.run(y.numpy(), lam, perm, last_in_epoch=last)
+            else:                                  # eager, or a trailing partial window
+                x = aug.run(flat, offs, lens, plan, perm, lam)
+                trainer.micro_step(x, y, lam, perm, last_in_epoch=last)
+
+    def save_train_state(self, path, epoch, model, trainer, swa, feeder, best):
+        """Full resume state (opt-in, --save_train_state): the reference keeps weights only."""
+        nst = np.random.get_state()
+        py = random.getstate()
+        torch.save({"format": TRAIN_STATE_FORMAT, "epoch": epoch, "model": model.state_dict(),
+                    "buffers": {n: b.detach().clone() for n, b in model.named_buffers()},
+                    "trainer": trainer.state_dict(), "swa": swa.state_dict(), "best": dict(best),
+                    "loader_gen": feeder.gen.get_state(),
+                    "rng": {"python": [py[0], list(py[1]), py[2]],
+                            "numpy": [nst[0], torch.from_numpy(nst[1].astype(np.int64)), int(nst[2]), int(nst[3]),
+                                      float(nst[4])],
+                            "torch": torch.get_rng_state(), "cuda": torch.cuda.get_rng_state(self.device)}},
+                   path)
+
+    def restore_train_state(self, st, model, trainer, swa, feeder, best):
+        model.load_state_dict(st["model"], strict=True)
+        with torch.no_grad():       # non-persistent buffers too (the encoder's device dropout seed), in place
+            for n, b in model.named_buffers():
+                b.copy_(st["buffers"][n])
+        trainer.load_state_dict(st["trainer"])
+        swa.load_state_dict(st["swa"])
+        best.update(st["best"])
+        feeder.gen.set_state(st["loader_gen"])
+        r = st["rng"]
+        random.setstate((r["python"][0], tuple(r["python"][1]), r["python"][2]))
+        npk = r["numpy"]
+        np.random.set_state((npk[0], npk[1].numpy().astype(np.uint32), npk[2], npk[3], npk[4]))
+        torch.set_rng_state(r["torch"])
+        torch.cuda.set_rng_state(r["cuda"], self.device)
+        return int(st["epoch"]) + 1
+
     def run(self):
         args, config = self.args, self.config
         model = self.build_model()
@@ -247,49 +336,42 @@ class Runner:
         accum = max(1, int(self.tc.get("accumulation_steps", 1)))
         steps_per_epoch = math.ceil(len(feeder) / accum)
         total = config["num_epochs"] * steps_per_epoch
-        group = None
-        trainer = Trainer(model, config, self.device, total, self.amp, world_group=group, criterion=self.criterion)
+        trainer = Trainer(model, config, self.device, total, self.amp, world_group=None, criterion=self.criterion)
         self.log(f"[Schedule] micro-batches/epoch={len(feeder)}, accumulation_steps={accum} -> "
                  f"optimizer_steps/epoch={steps_per_epoch}, total_steps={total}")
-        graph = None
-        if not args.eager:
-            graph = GraphedMicroStep(trainer, B)
-            graph.capture()
         swa = SWA(trainer.params)
-        eval_model_state = (lambda: trainer.ema.state_dict()) if trainer.ema is not None else (lambda: model.state_dict())
-        best_dev_eer, best_eval_eer, best_dev_tdcf, best_eval_tdcf = 100.0, 100.0, 100.0, 100.0
+        best = {"dev_eer": 100.0, "eval_eer": 100.0, "dev_tdcf": 100.0, "eval_tdcf": 100.0}
+        start = args.start_epoch
+        # graph capture consumes host RNG draws and runs warm-up passes, so it happens before a full
+        # resume restores the RNG / device-seed / optimizer state of the interrupted run
+        stepper = self.make_stepper(trainer, B)
+        self.log(f"[Step] micro-batches execute as: {stepper[0]}")
+        if self.resume_state is not None:
+            start = self.restore_train_state(self.resume_state, model, trainer, swa, feeder, best)
+            self.log(f"Resumed the full training state; continuing at epoch {start}")
+            self.resume_state = None
         metric_path = self.tag / "metrics"
         if self.rank == 0:
             os.makedirs(metric_path, exist_ok=True)
             with open(self.tag / "metric_log.txt", "a") as f_log:
                 f_log.write("=" * 5 + "\n")
-        epoch = args.start_epoch
-        for epoch in range(args.start_epoch, config["num_epochs"]):
+        for epoch in range(start, config["num_epochs"]):
             self.log("Start training epoch{:03d}".format(epoch))
-            n_micro = len(feeder)
-            for i, keys in enumerate(feeder.epoch()):
-                flat, offs, lens, y = feeder.load(keys, self.device)
-                plan = aug.draw(lens)
-                lam, perm = trainer.mixup_draw(len(keys))
-                last = i + 1 == n_micro
-                if graph is not None:
-                    aug.run(flat, offs, lens, plan, perm, lam, out=graph.x)
-                    graph.run(y.numpy(), lam, perm, last_in_epoch=last)
-                else:
-                    x = aug.run(flat, offs, lens, plan, perm, lam)
-                    trainer.micro_step(x, y, lam, perm, last_in_epoch=last)
+            self.train_epoch(trainer, stepper, feeder, aug)
             running_loss = trainer.epoch_loss()
-            # dev scoring with the EMA weights when enabled (the reference scores ema_model)
+            # dev / eval scoring and best-model files with the EMA weights when enabled (the reference's
+            # eval_model = ema_model); SWA averages the live optimizer parameters afterwards
             if trainer.ema is not None:
                 trainer.ema.swap()
             self.score(model, file_dev, dev_base, metric_path / "dev_score.txt", dev_trial)
             dev_eer, dev_tdcf = self.tdcf(metric_path / "dev_score.txt",
                                           metric_path / "dev_t-DCF_EER_{}epo.txt".format(epoch), printout=False)
             self.log("DONE.\nLoss:{:.5f}, dev_eer: {:.3f}, dev_tdcf:{:.5f}".format(running_loss, dev_eer, dev_tdcf))
-            best_dev_tdcf = min(dev_tdcf, best_dev_tdcf)
-            if best_dev_eer >= dev_eer:
+            best["dev_tdcf"] = min(dev_tdcf, best["dev_tdcf"])
+            improved = best["dev_eer"] >= dev_eer
+            if improved:
                 self.log("best model find at epoch", epoch)
-                best_dev_eer = dev_eer
+                best["dev_eer"] = dev_eer
                 name = "epoch_{}_{:03.3f}.pth".format(epoch, dev_eer)
                 if self.rank == 0:
                     for old in self.weights_dir.glob("epoch_*_*.pth"):
@@ -301,50 +383,66 @@ class Runner:
                     eval_eer, eval_tdcf = self.tdcf(self.eval_score_path,
                                                     metric_path / "t-DCF_EER_{:03d}epo.txt".format(epoch))
                     log_text = "epoch{:03d}, ".format(epoch)
-                    if eval_eer < best_eval_eer:
+                    if eval_eer < best["eval_eer"]:
                         log_text += "best eer, {:.4f}%".format(eval_eer)
-                        best_eval_eer = eval_eer
-                    if eval_tdcf < best_eval_tdcf:
+                        best["eval_eer"] = eval_eer
+                    if eval_tdcf < best["eval_tdcf"]:
                         log_text += "best tdcf, {:.4f}".format(eval_tdcf)
-                        best_eval_tdcf = eval_tdcf
+                        best["eval_tdcf"] = eval_tdcf
                         if self.rank == 0:
                             torch.save(model.state_dict(), self.weights_dir / "best.pth")
                     self.log(log_text)
                     if self.rank == 0:
                         with open(self.tag / "metric_log.txt", "a") as f_log:
                             f_log.write(log_text + "\n")
-                swa.update()
             if trainer.ema is not None:
                 trainer.ema.swap()
+            if improved:
+                self.log("Saving epoch {} for swa".format(epoch))
+                swa.update()
             if ((epoch + 1) % 10 == 0 or epoch == config["num_epochs"] - 1) and self.rank == 0:
                 ck = self.weights_dir / "checkpoint_epoch_{:03d}.pth".format(epoch)
                 torch.save(model.state_dict(), ck)
                 cks = sorted(self.weights_dir.glob("checkpoint_epoch_*.pth"), key=lambda x: int(x.stem.split("_")[-1]))
                 for old in cks[:-3]:
                     old.unlink(missing_ok=True)
+            if args.save_train_state and self.rank == 0:
+                self.save_train_state(self.weights_dir / "train_state_epoch_{:03d}.pt".format(epoch), epoch, model,
+                                      trainer, swa, feeder, best)
+                sts = sorted(self.weights_dir.glob("train_state_epoch_*.pt"), key=lambda x: int(x.stem.split("_")[-1]))
+                for old in sts[:-2]:
+                    old.unlink(missing_ok=True)
         self.log("Start final evaluation")
+        # reference order (src/main.py:669-690): swap the SWA average into the live model, bn_update over
+        # the train loader, evaluate the EMA model if enabled (its own weights and construction-time
+        # buffers, which bn_update does not touch) else the live model, save swa.pth = live model.
+        final_state = None
         if trainer.ema is not None:
             trainer.ema.swap()
-        self.score(model, file_eval, eval_base, self.eval_score_path, eval_trial)
-        eval_eer, eval_tdcf = self.tdcf(self.eval_score_path, self.tag / "t-DCF_EER.txt")
-        final_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
-        if trainer.ema is not None:
+            self.score(model, file_eval, eval_base, self.eval_score_path, eval_trial)
+            eval_eer, eval_tdcf = self.tdcf(self.eval_score_path, self.tag / "t-DCF_EER.txt")
+            final_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
             trainer.ema.swap()
+        if swa.n > 0:
+            swa.swap()
+            n_bn = swa_bn_update(model, feeder, aug, self.device)
+            self.log(f"[SWA] averaged {swa.n} snapshots; BatchNorm statistics recomputed over {n_bn} utterances")
+        if trainer.ema is None:
+            self.score(model, file_eval, eval_base, self.eval_score_path, eval_trial)
+            eval_eer, eval_tdcf = self.tdcf(self.eval_score_path, self.tag / "t-DCF_EER.txt")
+            final_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
         if self.rank == 0:
             with open(self.tag / "metric_log.txt", "a") as f_log:
                 f_log.write("=" * 5 + "\n")
                 f_log.write("EER: {:.3f}, min t-DCF: {:.5f}".format(eval_eer, eval_tdcf))
-        swa.swap()
-        if self.rank == 0:
             torch.save(model.state_dict(), self.weights_dir / "swa.pth")
-        swa.swap()
-        if eval_eer <= best_eval_eer:
-            best_eval_eer = eval_eer
-        if eval_tdcf <= best_eval_tdcf:
-            best_eval_tdcf = eval_tdcf
+        if eval_eer <= best["eval_eer"]:
+            best["eval_eer"] = eval_eer
+        if eval_tdcf <= best["eval_tdcf"]:
+            best["eval_tdcf"] = eval_tdcf
             if self.rank == 0:
                 torch.save(final_state, self.weights_dir / "best.pth")
-        self.log("Exp FIN. EER: {:.3f}, min t-DCF: {:.5f}".format(best_eval_eer, best_eval_tdcf))
+        self.log("Exp FIN. EER: {:.3f}, min t-DCF: {:.5f}".format(best["eval_eer"], best["eval_tdcf"]))
         if config.get("auto_eval_2021_df", False):
             self.auto_eval_2021(model)
         if self.world > 1:
@@ -369,7 +467,7 @@ class Runner:
                 self.log("Error: No model found for 2021 evaluation.")
                 return
             best = eps[-1]
-        load_weights(model, best, self.device, strict=False)
+        load_weights(model, best, self.device, strict=True)
         keys = genSpoof_list(trial, is_train=False, is_eval=True, is_2021=True)
         out = self.tag / "eval_scores_2021DF.txt"
         self.score(model, keys, Path(root), out, trial, fmt="2021", zero_on_error=True)
@@ -398,6 +496,11 @@ def parse_args(argv=None):
     parser.add_argument("--model", type=str, default=None, help="override the model architecture")
     parser.add_argument("--amp", default="bf16", choices=sorted(AMP), help="autocast dtype (reference: fp16)")
     parser.add_argument("--eager", action="store_true", help="launch kernel by kernel (no HIP graphs)")
+    parser.add_argument("--no-window", dest="no_window", action="store_true",
+                        help="replay one graph pair per micro-batch instead of the batched accumulation window")
+    parser.add_argument("--save_train_state", action="store_true",
+                        help="also write weights/train_state_epoch_XXX.pt (optimizer, scheduler, EMA, SWA, RNG) for an "
+                             "exact --resume")
     parser.add_argument("--loader-threads", dest="loader_threads", type=int, default=8,
                         help="host threads of the native FLAC batch decoder")
     return parser.parse_args(argv)

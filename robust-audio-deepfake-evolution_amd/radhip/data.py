@@ -198,8 +198,11 @@ class _PinnedBuf:
 class TrainFeeder:
     """Shuffled micro-batches of the train list (drop_last=True), augmented on the GPU.
 
-    Order: torch.randperm(n, generator=gen) once per epoch with gen = Generator().manual_seed(seed),
-    which is what the reference's DataLoader(shuffle=True, generator=gen) draws (main.py:909-920).
+    Order: what the reference's DataLoader(shuffle=True, drop_last=True, generator=gen) draws from
+    gen = Generator().manual_seed(seed) (main.py:909-920) on torch 2.x, per epoch: the iterator's base
+    seed (one int64 random_), RandomSampler's torch.randperm(n) (the order used), and the sampler's
+    trailing randperm(n)[:n % n] that runs when the exhausted sampler is polled once more
+    (tests/test_data_cpu.py compares against a real DataLoader over several epochs).
     Per micro-batch: native batch decode -> Augmenter.draw (python/numpy RNG in __getitem__ order) ->
     mixup draw (np.random.beta, torch.randperm) -> Augmenter.run (RawBoost, codec, pad_random, mixup)."""
 
@@ -215,8 +218,17 @@ class TrainFeeder:
         """Micro-batches per epoch on this rank (global batches = world * B utterances)."""
         return len(self.keys) // (self.B * self.world)
 
+    def epoch_order(self):
+        """This epoch's shuffled index order, consuming the generator exactly as one full pass of the
+        reference's DataLoader does."""
+        n = len(self.keys)
+        torch.empty((), dtype=torch.int64).random_(generator=self.gen)    # _BaseDataLoaderIter base seed
+        order = torch.randperm(n, generator=self.gen).tolist()              # RandomSampler.__iter__
+        torch.randperm(n, generator=self.gen)                               # its trailing [:n % n] draw
+        return order
+
     def epoch(self):
-        order = torch.randperm(len(self.keys), generator=self.gen).tolist()
+        order = self.epoch_order()
         gb = self.B * self.world
         for i in range(len(self)):
             chunk = order[i * gb:(i + 1) * gb][self.rank * self.B:(self.rank + 1) * self.B]

@@ -24,51 +24,58 @@ CAPTURE_TIMING = None
 
 class GraphTimer:
     """Per-launch-site accumulators [ticks, count] in device memory, filled by captured stamps. Only the
-    first `per_graph` launch sites of each kernel in each captured graph are stamped: the sites of one
-    kernel in one graph have the same shape, and every stamp is itself a ~4.5 us graph node."""
+    first `per_graph` launch sites of each kernel in each captured graph are stamped (every stamp is
+    itself a ~4.5 us graph node); the sites of one kernel in one graph have the same shape (e.g. the 24
+    WavLM layers), so each sampled site stands for total / sampled of them and rows() scales its count
+    and time by that factor: launches and total_ms are per-replay totals over ALL sites."""
 
     def __init__(self, device, capacity=1024, per_graph=2):
         self.device = torch.device(device)
         self.acc = torch.zeros(capacity, 2, dtype=torch.int64, device=self.device)
-        self.sites = []                       # (name, work) per slot
+        self.sites = []                       # (name, work, group) per slot
         self.per_graph = per_graph
-        self._in_graph = {}
+        self._in_graph = {}                   # name -> group record {"total", "sampled"} of this graph
 
     def new_graph(self):
         """Call before capturing each graph."""
         self._in_graph = {}
 
     def slot(self, name, work):
-        n = self._in_graph.get(name, 0)
-        if n >= self.per_graph:
+        grp = self._in_graph.setdefault(name, {"total": 0, "sampled": 0})
+        grp["total"] += 1
+        if grp["sampled"] >= self.per_graph:
             return None
-        self._in_graph[name] = n + 1
+        grp["sampled"] += 1
         if len(self.sites) >= self.acc.shape[0]:
             raise RuntimeError("GraphTimer: out of slots")
-        self.sites.append((name, float(work)))
+        self.sites.append((name, float(work), grp))
         return self.acc[len(self.sites) - 1]
 
     def reset(self):
         self.acc.zero_()
 
     def rows(self):
-        """{name: {launches, total_ms, avg_ms, avg_work}} over everything replayed since reset()."""
+        """{name: {launches, total_ms, avg_ms, avg_work, sampled_launches}} over everything replayed since
+        reset(): launches / total_ms count every launch site of the graphs (sampled sites scaled)."""
         khz = lib().rdx_wallclock_khz(self.device.index or 0)
         if khz <= 0:
             raise RuntimeError("rdx_wallclock_khz failed")
         acc = self.acc.cpu().numpy()
         out = {}
-        for i, (name, work) in enumerate(self.sites):
+        for i, (name, work, grp) in enumerate(self.sites):
             ticks, cnt = int(acc[i, 0]), int(acc[i, 1])
             if cnt == 0:
                 continue
-            r = out.setdefault(name, {"launches": 0, "total_ms": 0.0, "work_sum": 0.0})
-            r["launches"] += cnt
-            r["total_ms"] += ticks / khz
-            r["work_sum"] += work * cnt
+            mult = grp["total"] / grp["sampled"]
+            r = out.setdefault(name, {"launches": 0.0, "total_ms": 0.0, "work_sum": 0.0, "sampled_launches": 0})
+            r["launches"] += cnt * mult
+            r["total_ms"] += ticks / khz * mult
+            r["work_sum"] += work * cnt * mult
+            r["sampled_launches"] += cnt
         for r in out.values():
             r["avg_ms"] = r["total_ms"] / r["launches"]
             r["avg_work"] = r.pop("work_sum") / r["launches"]
+            r["launches"] = int(round(r["launches"]))
         return out
 
 

@@ -30,14 +30,20 @@ CODEC_RATES = (8000, 6000, 4000)
 
 # ------------------------------------------------------------------------------- losses ------
 class FocalLoss(nn.Module):
-    """kornia.losses.FocalLoss(alpha, gamma, reduction='mean') for 2-class logits.
+    """kornia.losses.FocalLoss(alpha, gamma, reduction='mean') (src/main.py:297-305) for [B, C] logits.
 
-    alpha_mode 'per_class' (kornia >= 0.7: weight [1-alpha, alpha, ...] by target class) or 'scalar'
-    (older kornia: alpha for every class). kornia is absent from the image and the reference pins no
-    version: parity unpinned; default per_class."""
+    kornia is absent from the image and from the reference's requirements, and the two kornia
+    generations differ, so both are restated (parity unpinned):
+      'per_class' (kornia >= 0.7, default): loss_tmp[b, c] = -alpha_c (1 - p_bc)^gamma log p_bc onehot[b, c]
+                  with alpha_c = [1 - alpha, alpha, alpha, ...]; 'mean' averages loss_tmp over all B*C
+                  elements (the class axis is kept, so the mean divides by C as well).
+      'scalar'    (kornia < 0.7): loss[b] = -alpha (1 - p_b,y)^gamma log p_b,y, mean over B.
+    alpha None drops the factor. (1 - p)^gamma uses p = exp(log_softmax), so p -> 1 gives 0, not NaN."""
 
     def __init__(self, alpha=0.25, gamma=2.0, alpha_mode="per_class"):
         super().__init__()
+        if alpha_mode not in ("per_class", "scalar"):
+            raise ValueError(f"focal alpha_mode must be 'per_class' or 'scalar', got {alpha_mode!r}")
         self.alpha, self.gamma, self.alpha_mode = alpha, gamma, alpha_mode
 
     def forward(self, logits, target):
@@ -50,7 +56,10 @@ class FocalLoss(nn.Module):
             a = torch.where(target == 0, 1.0 - self.alpha, self.alpha).to(lp.dtype)
         else:
             a = self.alpha
-        return (-a * w * lp).mean()
+        per_utt = -a * w * lp
+        if self.alpha_mode == "per_class":
+            return per_utt.sum() / (logits.shape[0] * logits.shape[1])
+        return per_utt.mean()
 
 
 def build_criterion(config, device):
@@ -104,13 +113,17 @@ class FGM:
 class EMA:
     """AveragedModel(model, multi_avg_fn=get_ema_multi_avg_fn(decay)) restricted to the tensors that
     can change (lerp(a, a, w) == a, so frozen tensors are unaffected in the reference as well).
-    First update copies; buffers are not averaged (use_buffers=False)."""
+    First update copies. Buffers are not averaged (use_buffers=False): like the reference's deep copy,
+    the EMA model keeps the BatchNorm buffers it was constructed with (identical to the live ones
+    whenever BN is frozen), and swap() exchanges those too."""
 
     def __init__(self, model, decay=0.999):
         self.model, self.decay = model, decay
         self.names = [n for n, p in model.named_parameters() if p.requires_grad]
         self.shadow = None
         self.n_averaged = 0
+        self.buf_names = [n for n, _ in model.named_buffers()]
+        self.buffers = [b.detach().clone() for _, b in model.named_buffers()]
 
     def refresh_names(self):
         self.names = [n for n, p in self.model.named_parameters() if p.requires_grad]
@@ -132,18 +145,41 @@ class EMA:
         if self.shadow is None:
             return
         params = dict(self.model.named_parameters())
-        for n, s in zip(self.names, self.shadow):
-            tmp = params[n].data.clone()
-            params[n].data.copy_(s)
+        bufs = dict(self.model.named_buffers())
+        for n, s in list(zip(self.names, self.shadow)) + list(zip(self.buf_names, self.buffers)):
+            live = params[n].data if n in params else bufs[n]
+            tmp = live.clone()
+            live.copy_(s)
             s.copy_(tmp)
 
     def state_dict(self):
-        """Full model state dict with EMA values (the reference saves ema_model.state_dict())."""
+        """Full model state dict with EMA values (the reference saves ema_model.state_dict()): EMA
+        parameters, the construction-time buffers, live values for everything never averaged."""
         sd = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+        for n, b in zip(self.buf_names, self.buffers):
+            if n in sd:
+                sd[n] = b.detach().clone()
         if self.shadow is not None:
             for n, s in zip(self.names, self.shadow):
                 sd[n] = s.detach().clone()
         return sd
+
+    def train_state(self):
+        return {"names": list(self.names), "n_averaged": self.n_averaged,
+                "shadow": None if self.shadow is None else [s.detach().clone() for s in self.shadow],
+                "buf_names": list(self.buf_names), "buffers": [b.detach().clone() for b in self.buffers]}
+
+    def load_train_state(self, st):
+        if list(st["names"]) != self.names or list(st["buf_names"]) != self.buf_names:
+            raise ValueError("EMA state was saved for a different set of tensors")
+        self.n_averaged = int(st["n_averaged"])
+        self.shadow = None if st["shadow"] is None else [s.to(b.device) for s, b in
+                                                         zip(st["shadow"], self._live_params())]
+        self.buffers = [b.to(l.device) for b, l in zip(st["buffers"], self.model.buffers())]
+
+    def _live_params(self):
+        params = dict(self.model.named_parameters())
+        return [params[n] for n in self.names]
 
 
 # ---------------------------------------------------------------------- flat gradients -------
@@ -454,13 +490,66 @@ class Trainer:
         self.n_seen = 0
         return v
 
+    # ---------------------------------------------------------------- full resume state -------
+    def state_dict(self):
+        """Everything an exact resume needs beyond the model weights (the reference saves weights only,
+        src/main.py:649-664): optimizer moments, LR schedule position, grad scaler, EMA."""
+        return {"optimizer": self.opt.state_dict(), "scheduler": self.sched.state_dict(),
+                "scaler": self.scaler.state_dict(), "micro": self.micro,
+                "ema": self.ema.train_state() if self.ema is not None else None}
+
+    def load_state_dict(self, st):
+        self.opt.load_state_dict(st["optimizer"])
+        self.sched.load_state_dict(st["scheduler"])
+        self.scaler.load_state_dict(st["scaler"])
+        self.micro = int(st["micro"])
+        if (st["ema"] is None) != (self.ema is None):
+            raise ValueError("train state and config disagree on use_ema")
+        if self.ema is not None:
+            self.ema.load_train_state(st["ema"])
+
+
+@torch.no_grad()
+def swa_bn_update(model, feeder, augmenter, device):
+    """torchcontrib SWA.bn_update(trn_loader, model) after swap_swa_sgd (src/main.py:669-672): reset every
+    BatchNorm's running statistics and recompute them as a cumulative average (momentum b / (n + b)) over
+    one pass of the augmented train loader in train mode. Only the SincNet stream holds BatchNorm, and
+    nothing else it computes is kept, so only that stream runs (the WavLM stream's forward does not
+    touch any BatchNorm statistic)."""
+    bns = [m for m in model.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
+    if not bns:
+        return 0
+    was_training = model.training
+    momenta = {}
+    for m in bns:
+        m.running_mean.zero_()      # in place: captured HIP graphs keep pointing at the same buffers
+        m.running_var.fill_(1.0)
+        momenta[m] = m.momentum
+    model.train()
+    for m in bns:
+        m.train()
+    n = 0
+    for keys in feeder.epoch():
+        flat, offs, lens, _ = feeder.load(keys, device)
+        x = augmenter.run(flat, offs, lens, augmenter.draw(lens))
+        b = x.shape[0]
+        for m in bns:
+            m.momentum = b / float(n + b)
+        model.sinc_stream(x, freq_aug=False)
+        n += b
+    for m in bns:
+        m.momentum = momenta[m]
+    model.train(was_training)
+    return n
+
 
 class _PinnedRing:
     """Small ring of pinned host slots for H2D copies of per-replay inputs (non_blocking, stream-ordered;
     a slot is reused only after the copy that read it has executed)."""
 
     def __init__(self, nbytes, slots=4):
-        self.bufs = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(slots)]
+        self.gpu = torch.cuda.is_available()
+        self.bufs = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=self.gpu) for _ in range(slots)]
         self.events = [None] * slots
         self.i = 0
 
@@ -481,10 +570,11 @@ class _PinnedRing:
             views.append((buf[off:off + nb].view(dst.dtype).view(dst.shape), dst))
             off += nb
         for src, dst in views:
-            dst.copy_(src, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.events[k] = ev
+            dst.copy_(src, non_blocking=dst.is_cuda)
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[k] = ev
 
 
 def check_graph_memset_replay(device):

@@ -22,6 +22,14 @@ from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay
 from .wavlm import compute_time_mask
 
 
+def window_eligible(trainer):
+    """True when batching the window's clean passes is exact: no BatchNorm computes batch statistics
+    (freeze_bn, or a model without BatchNorm)."""
+    if trainer.freeze_bn:
+        return True
+    return not any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in trainer.model.modules())
+
+
 class WindowStep:
     def __init__(self, trainer, batch, K=None, graphs=True, max_len=MAX_LEN):
         tr = trainer
@@ -30,6 +38,9 @@ class WindowStep:
         self.tr, self.B, self.K = tr, int(batch), int(K or tr.accum)
         if self.K < 1:
             raise ValueError("window needs K >= 1")
+        if not window_eligible(tr):
+            raise ValueError("the accumulation window batches K micro-batches into one pass, which is the same "
+                             "math only when every BatchNorm is frozen (freeze_bn) or absent")
         N = self.K * self.B
         self.N = N
         self.graphs_on = graphs
@@ -179,7 +190,10 @@ class WindowStep:
         self.core.encoder.keep_dev = None
 
     def _prefix_grad(self, k):
-        """feature_projection.grad += g_k (micro-batch k's clean gradient)."""
+        """feature_projection.grad += g_k (micro-batch k's clean gradient). Without FGM feature_projection
+        is frozen (no .grad) and the copies' gradients are never used."""
+        if not self.adv:
+            return
         torch._foreach_add_([p.grad for p in self.fp_real], list(self.fp_copies[k][i].grad for i in range(4)))
 
     def _adv_chain(self, run_adv):

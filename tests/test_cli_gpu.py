@@ -2,7 +2,8 @@
 training epoch through the HIP path (native decode -> GPU RawBoost/codec/pad/mixup -> graphed FGM
 micro-steps -> AdamW/EMA), the reference's output layout, then --eval with the saved weights and a
 2021-DF eval with the codec breakdown. Scores written by the CLI must equal a direct fp32 forward of
-the same weights on the reference's numpy `pad` of each file."""
+the same weights on the reference's numpy `pad` of each file. A run resumed from the full training
+state (--save_train_state / --resume) must end where the uninterrupted run ends."""
 import json
 import os
 import shutil
@@ -72,7 +73,7 @@ def _direct_scores(cfg, weights, paths):
     from radhip.build import apply_lora_to_wavlm, get_model, load_weights
     from radhip.data import pad
     m = apply_lora_to_wavlm(get_model(cfg["model_config"], "cuda"), cfg["training_config"])
-    load_weights(m, weights, "cuda", strict=False)
+    load_weights(m, weights, "cuda", strict=True)
     m.eval()
     x = np.stack([pad(audio.read(p)[0]) for p in paths]).astype(np.float32)
     with torch.no_grad():
@@ -135,4 +136,35 @@ def test_cli_train_eval_and_2021(tmp_path, golden):
     np.testing.assert_allclose([float(ln.split()[1]) for ln in lines], ref[:6], rtol=1e-4, atol=1e-5)
     rep = (t21 / "t-DCF_EER_2021DF.txt").read_text()
     assert "EER" in rep and "low_mp3" in rep
+    os.environ.pop("WORLD_SIZE", None)
+
+
+def test_cli_full_resume_equals_continuous(tmp_path, golden):
+    """Two epochs in one run vs one epoch, then --resume from train_state_epoch_000.pt in a new run: the
+    second epoch's weights, EMA/SWA files and dev scores agree (up to the GPU's atomic-accumulation
+    order, far below any training step's effect)."""
+    import main as cli
+    db = tmp_path / "LA"
+    _database(db, golden)
+    conf, cfg = _config(tmp_path, golden, db)
+    cfg["num_epochs"] = 2
+    conf.write_text(json.dumps(cfg, indent=2))
+    out = tmp_path / "exp"
+    cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--save_train_state",
+                             "--comment", "cont"]))
+    cont = out / "LA_Tiny_ep2_bs2_cont"
+    state0 = cont / "weights" / "train_state_epoch_000.pt"
+    assert state0.exists() and (cont / "weights" / "train_state_epoch_001.pt").exists()
+    cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--resume", str(state0),
+                             "--comment", "res"]))
+    res = out / "LA_Tiny_ep2_bs2_res"
+    for f in ("checkpoint_epoch_001.pth", "swa.pth", "best.pth"):
+        a = torch.load(cont / "weights" / f, weights_only=True)
+        b = torch.load(res / "weights" / f, weights_only=True)
+        assert a.keys() == b.keys()
+        for k in a:
+            torch.testing.assert_close(b[k].float(), a[k].float(), rtol=1e-4, atol=2e-6, msg=f"{f}:{k}")
+    sa = [float(ln.split()[3]) for ln in (cont / "metrics" / "dev_score.txt").read_text().splitlines()]
+    sb = [float(ln.split()[3]) for ln in (res / "metrics" / "dev_score.txt").read_text().splitlines()]
+    np.testing.assert_allclose(sb, sa, rtol=1e-3, atol=1e-4)
     os.environ.pop("WORLD_SIZE", None)

@@ -183,3 +183,24 @@ def test_swa_running_mean():
     assert torch.allclose(p.data, torch.full((3,), 3.0))
     s.swap()
     assert torch.allclose(p.data, torch.full((3,), 6.0))
+
+
+@pytest.mark.parametrize("n,B,world", [(20, 4, 1), (22, 4, 1), (37, 3, 2)])
+def test_train_feeder_order_equals_reference_dataloader(n, B, world):
+    """TrainFeeder's per-epoch order == the reference's DataLoader(shuffle=True, drop_last=True,
+    generator=Generator().manual_seed(seed)) (src/main.py:909-920) over several epochs; with world > 1
+    each rank takes its B-row share of every global batch of world * B."""
+    import torch
+    from torch.utils.data import DataLoader
+    from radhip.data import TrainFeeder
+    keys = [f"LA_T_{i:07d}" for i in range(n)]
+    g = torch.Generator()
+    g.manual_seed(1234)
+    dl = DataLoader(keys, batch_size=B * world, shuffle=True, drop_last=True, generator=g)
+    feeders = [TrainFeeder(keys, {k: 0 for k in keys}, "/nonexistent", B, None, 1234, rank=r, world=world)
+               for r in range(world)]
+    for _ in range(3):
+        ref = [list(b) for b in dl]
+        got = [list(f.epoch()) for f in feeders]
+        for r in range(world):
+            assert got[r] == [b[r * B:(r + 1) * B] for b in ref]

@@ -91,12 +91,15 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
 
 
-@pytest.mark.parametrize("p,B", [(0.0, 2), (0.1, 2), (0.1, 21)])
-def test_fused_layers_match_fp32_restatement(p, B):
+@pytest.mark.parametrize("p,B,inter", [(0.0, 2, 512), (0.1, 2, 512), (0.1, 21, 512), (0.1, 8, 4096),
+                                       (0.1, 32, 4096)])
+def test_fused_layers_match_fp32_restatement(p, B, inter):
     """B = 21 (M = 4221 rows) takes the LoRA weight-grad kernel's multi-chunk path (2 chunks of 32
-    rows per block, ragged last block); B = 2 the single-chunk path with a ragged last chunk."""
+    rows per block, ragged last block); B = 2 the single-chunk path with a ragged last chunk.
+    inter = 4096 is WavLM-Large's FFN width: B = 8 is the adversarial pass and B = 32 the batched
+    clean pass the bench times."""
     from radhip import wavlm_fused
-    enc = _encoder(p=p).train()
+    enc = _encoder(p=p, inter=inter).train()
     T, E = 201, 1024
     torch.manual_seed(1)
     h0 = (0.5 * torch.randn(B, T, E, device=DEV)).requires_grad_(True)
@@ -127,11 +130,13 @@ def test_fused_layers_match_fp32_restatement(p, B):
         assert _rel(gp, prm.grad) < 5e-2, prm.shape
 
 
-def test_fused_encoder_matches_module_path_without_dropout(monkeypatch):
-    """Encoder.forward with the fused layers (bf16) vs the module path in fp32 (dropouts off)."""
-    enc = _encoder(n_layers=3, p=0.0).train()
+@pytest.mark.parametrize("B,inter", [(2, 512), (8, 4096)])
+def test_fused_encoder_matches_module_path_without_dropout(monkeypatch, B, inter):
+    """Encoder.forward with the fused layers (bf16) vs the module path in fp32 (dropouts off); the
+    module path is the one pinned to HF WavLM by the model golden. inter 4096 = WavLM-Large width."""
+    enc = _encoder(n_layers=3, p=0.0, inter=inter).train()
     torch.manual_seed(2)
-    x = (0.5 * torch.randn(2, 201, 1024, device=DEV))
+    x = (0.5 * torch.randn(B, 201, 1024, device=DEV))
     outs, grads = [], []
     for fused in (True, False):
         monkeypatch.setenv("RADHIP_FUSED_WAVLM", "1" if fused else "0")

@@ -1,6 +1,6 @@
 """Micro-benchmark of the fused gated-bias attention (rdx_attn_fwd / rdx_attn_bwd) at the Phase-6 shape
 (B = 8 (env B), T = 201, H = 16, 64-dim heads, dropout 0.1); also the program the PMC passes of
-tools/gpu_prof_r01.sh profile.
+tools/gpu_prof.sh profile.
   B=32 python tools/bench_attn.py
 """
 import json

@@ -1,7 +1,7 @@
 """Micro-benchmark of the hand-written kernels that dominate the bench step, at the window's batch shapes
 (env B: 8 = an adversarial pass, 32 = the batched clean pass): the gated attention (forward, backward),
 the WavLM positional conv (forward, backward) and the SincNet block-0 backward. It is also the program the
-rocprofv3 PMC passes of tools/gpu_prof_r01.sh profile (one counter group per run).
+rocprofv3 PMC passes of tools/gpu_prof.sh profile (one counter group per run).
 
   B=32 python tools/bench_kernels.py
 """

@@ -1,5 +1,5 @@
 """HBM bytes per launch of the hand-written kernels from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
-tools/gpu_prof_r01.sh, written to profiles/pmc_traffic.json (bench.py reads `hbm_bytes_per_launch` of the
+tools/gpu_prof.sh, written to profiles/pmc_traffic.json (bench.py reads `hbm_bytes_per_launch` of the
 dominant kernel into roofline.traffic).
 
 Counter conventions (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): both counters are in KiB;
