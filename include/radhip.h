@@ -237,23 +237,39 @@ int rdx_posconv_bwd(const void* dy, const void* u, const void* wkt, void* dh, in
 /* ---- WavLM self-attention with the gated relative-position bias (HF WavLMAttention as used by
  * WavLMFrontend, src/models/DualStreamSEMamba.py:292-439), MFMA bf16, 64-dim heads -------------------
  * q, k, v: bf16 [B, T, H*64] row views (row strides ldq/ldk/ldv, 16-byte aligned); gate [B, T, H] fp32;
- * pos_bias [H, T, ldpb] fp32 (frozen; ldpb >= 32*ceil(T/32), a multiple of 4, 16-byte aligned).
- * S = q k^T * scale + gate[b,i,h] * pos_bias[h,i,j]; P = softmax(S);
+ * rel_bias [H, 2T-1] fp32 (frozen): WavLM's position bias of (query i, key j) depends on j - i only
+ * (bucketed relative position, compute_bias), so it is passed as rel_bias[h][j - i + T - 1].
+ * S = q k^T * scale + gate[b,i,h] * rel_bias[h, j-i+T-1]; P = softmax(S);
  * O = dropout_p(P) v -> o [B, T, H*64] bf16 (row stride ldo); lse [B, H, T] fp32 (saved for bwd).
- * Dropout keeps (b,h,i,j) iff hash(seed, ((b*H+h)*T+i)*T+j) >= p*2^32, seed = f(seed_dev[0], salt)
- * read on the device (HIP-graph replayable); rdx_attn_dropout_mask materialises that mask (tests).
+ * Dropout: one hash per key pair (2m, 2m+1) of score row (b*H+h)*T+i, pair id row*ceil(T/2)+m, seed =
+ * f(seed_dev[0], salt) read on the device (HIP-graph replayable); key 2m keeps iff the hash's low 16 bits
+ * >= round(p*2^16), key 2m+1 iff its high 16 bits are. rdx_attn_dropout_mask materialises that mask over
+ * n = rows*T elements (tests). keep_mask (nullable; rdx_attn_keep_mask_words(B, T, H) uint32 words) receives
+ * the forward's keep bits for rdx_attn_bwd_fused.
  * rdx_attn_bwd: D [B, H, T] fp32 workspace; dq, dk, dv bf16 [B, T, H*64] (row stride ldg), dgate
- * [B, T, H] fp32 (all overwritten). */
+ * [B, T, H] fp32 (all overwritten); recomputes the dropout hash. */
 int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                 const float* gate, const float* pos_bias, int64_t ldpb, const int64_t* seed_dev, int salt,
-                 float p_drop, float scale, void* o, int64_t ldo, float* lse, int B, int T, int H, int head_dim, void* stream);
+                 const float* gate, const float* rel_bias, const int64_t* seed_dev, int salt, float p_drop,
+                 float scale, void* o, int64_t ldo, float* lse, uint32_t* keep_mask, int B, int T, int H, int head_dim,
+                 void* stream);
+int64_t rdx_attn_keep_mask_words(int B, int T, int H);
 int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                 const float* gate, const float* pos_bias, int64_t ldpb, const int64_t* seed_dev, int salt,
-                 float p_drop, float scale, const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo,
-                 float* D, void* dq, void* dk, void* dv, int64_t ldg, float* dgate, int B, int T, int H,
-                 int head_dim, void* stream);
-int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n,
+                 const float* gate, const float* rel_bias, const int64_t* seed_dev, int salt, float p_drop, float scale,
+                 const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo, float* D, void* dq,
+                 void* dk, void* dv, int64_t ldg, float* dgate, int B, int T, int H, int head_dim, void* stream);
+/* rdx_attn_bwd_fused: the same gradients as rdx_attn_bwd from ONE launch of one workgroup per (b, h)
+ * (S and dP computed once per tile pair; dS kept in LDS for dQ). T <= 224 (RDX_EUNSUPPORTED above);
+ * keep_mask is the forward's (required when p_drop > 0). */
+int rdx_attn_bwd_fused(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                       const float* gate, const float* rel_bias, const uint32_t* keep_mask, float p_drop, float scale,
+                       const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo, float* D,
+                       void* dq, void* dk, void* dv, int64_t ldg, float* dgate, int B, int T, int H, int head_dim,
+                       void* stream);
+int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n, int T,
                           void* stream);
+/* the element-wise dropout of the fused WavLM layer kernels below (element t kept iff
+ * hash(seed, t) >= p*2^32): its keep mask over n elements (tests) */
+int rdx_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n, void* stream);
 
 /* ---- Fused WavLM encoder layer pieces (HF WavLMEncoderLayerStableLayerNorm + peft LoRA q/v as
  * run by WavLMFrontend, src/models/DualStreamSEMamba.py:292-439 and src/main.py:103-158). Row-major

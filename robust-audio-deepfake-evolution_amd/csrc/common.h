@@ -74,6 +74,31 @@ __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t 
                      ((uint32_t)(seed >> 32) * 0x85ebca6bu);
   return fmix32(x) >= thr;
 }
+// The same decision for an index below 2^32 (then idx >> 32 contributes 0), with the seed words mixed once:
+// drop_keep32(drop_key32(seed), idx, thr) == drop_keep(seed, idx, thr) for every idx < 2^32.
+struct DropKey32 {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ DropKey32 drop_key32(uint64_t seed) {
+  return DropKey32{(uint32_t)seed, (uint32_t)(seed >> 32) * 0x85ebca6bu};
+}
+__device__ __forceinline__ bool drop_keep32(DropKey32 k, uint32_t idx, uint32_t thr) {
+  return fmix32(((idx ^ k.lo) * 0x9E3779B1u) ^ k.hi) >= thr;
+}
+// Attention dropout (csrc/attention.hip): one hash per PAIR of keys (2j, 2j + 1) of a score row; key 2j
+// is kept iff the low 16 bits of the hash are >= thr16 = p * 2^16, key 2j + 1 iff the high 16 bits are.
+// Pair id = row * ceil(T / 2) + key / 2 with row = (b * H + h) * T + q. pair_hash32 == pair_hash for
+// pair ids below 2^32.
+__device__ __forceinline__ uint32_t pair_hash(uint64_t seed, uint64_t pid) {
+  return fmix32((((uint32_t)pid ^ (uint32_t)seed) * 0x9E3779B1u) ^ (uint32_t)(pid >> 32) ^
+                ((uint32_t)(seed >> 32) * 0x85ebca6bu));
+}
+__device__ __forceinline__ uint32_t pair_hash32(DropKey32 k, uint32_t pid) {
+  return fmix32(((pid ^ k.lo) * 0x9E3779B1u) ^ k.hi);
+}
+__device__ __forceinline__ bool half_keep(uint32_t h, bool odd, uint32_t thr16) {
+  return (odd ? (h >> 16) : (h & 0xffffu)) >= thr16;
+}
 __device__ __forceinline__ uint64_t attn_seed(const int64_t* seed_dev, int salt) {
   return (uint64_t)seed_dev[0] * 0x9E3779B97F4A7C15ull + (uint64_t)(uint32_t)salt * 0xD1B54A32D192ED03ull;
 }

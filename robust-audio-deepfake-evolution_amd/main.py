@@ -299,13 +299,13 @@ class Runner:
         trainer.load_state_dict(st["trainer"])
         swa.load_state_dict(st["swa"])
         best.update(st["best"])
-        feeder.gen.set_state(st["loader_gen"])
         r = st["rng"]
         random.setstate((r["python"][0], tuple(r["python"][1]), r["python"][2]))
         npk = r["numpy"]
-        np.random.set_state((npk[0], npk[1].numpy().astype(np.uint32), npk[2], npk[3], npk[4]))
-        torch.set_rng_state(r["torch"])
-        torch.cuda.set_rng_state(r["cuda"], self.device)
+        np.random.set_state((npk[0], npk[1].cpu().numpy().astype(np.uint32), npk[2], npk[3], npk[4]))
+        torch.set_rng_state(r["torch"].cpu())          # (map_location put every tensor on the device)
+        torch.cuda.set_rng_state(r["cuda"].cpu(), self.device)
+        feeder.gen.set_state(st["loader_gen"].cpu())
         return int(st["epoch"]) + 1
 
     def run(self):

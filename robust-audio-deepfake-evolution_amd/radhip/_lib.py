@@ -90,12 +90,16 @@ SIGNATURES = {
     "rdx_sincnet_b0_bwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),
     "rdx_posconv_fwd": (c_int, [c_vp] * 5 + [c_int, c_int, c_vp]),
     "rdx_posconv_bwd": (c_int, [c_vp] * 4 + [c_int, c_int, c_vp]),
-    "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_f32, c_vp,
-                             c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp]),
-    "rdx_attn_bwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_int, c_f32, c_f32, c_vp,
-                             c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int,
-                             c_int, c_vp]),
-    "rdx_attn_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_vp]),
+    "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp, c_i64,
+                             c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_attn_keep_mask_words": (c_i64, [c_int, c_int, c_int]),
+    "rdx_attn_bwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp, c_i64,
+                             c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_attn_bwd_fused": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_i64,
+                                   c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
+                                   c_vp]),
+    "rdx_attn_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_int, c_vp]),
+    "rdx_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_vp]),
     "rdx_wl_ln1_fwd": (c_int, [c_vp] * 3 + [c_f32] + [c_vp] * 5 + [c_int, c_vp,
                        c_int, c_int, c_f32, c_vp, c_i64] + [c_vp] * 3
                        + [c_i64, c_int, c_vp]),

@@ -4,6 +4,7 @@ Every op here runs the hand-written HIP kernel on the tensor's current HIP strea
 path. Tensors must live on a ROCm device.
 """
 import ctypes
+import os
 
 import torch
 
@@ -582,16 +583,55 @@ def _ld(t):
     return t.stride(1)
 
 
-def pad_position_bias(pb):
-    """[H, T, T] -> [H, T, 32*ceil(T/32)] fp32, zero-padded rows (the attention kernels read each key
-    tile's position bias with aligned float4 loads)."""
+def rel_bias_table(pb, check=True):
+    """[H, T, T] position bias -> its relative-position table [H, 2T - 1] fp32, table[h, j - i + T - 1] =
+    pb[h, i, j]. WavLM's bias (compute_bias: bucketed key - query offsets) depends on j - i only; `check`
+    verifies that before the kernels rely on it. A [H, 2T - 1] input is taken as the table."""
+    if pb.dim() == 2:
+        return pb.detach().float().contiguous()
     H, T, T2 = pb.shape
-    ld = -(-T2 // 32) * 32
-    if T2 == ld and pb.is_contiguous():
-        return pb
-    out = torch.zeros(H, T, ld, device=pb.device, dtype=torch.float32)
-    out[:, :, :T2] = pb
-    return out
+    if T != T2:
+        raise ValueError("radhip attention: square [H, T, T] position bias expected")
+    pb = pb.detach().float()
+    tab = torch.cat([pb[:, 1:, 0].flip(1), pb[:, 0, :]], dim=1).contiguous()            # d = -(T-1) .. T-1
+    if check:
+        i = torch.arange(T, device=pb.device)
+        idx = (i[None, :] - i[:, None] + T - 1)                                          # [i, j] -> j - i + T - 1
+        if not torch.equal(tab[:, idx], pb):
+            raise ValueError("radhip attention: the position bias must depend on key - query only (Toeplitz)")
+    return tab
+
+
+FUSED_BWD_MAX_T = 224
+
+
+def fused_bwd_enabled(T):
+    return T <= FUSED_BWD_MAX_T and os.environ.get("RADHIP_ATTN_BWD", "fused") != "split"
+
+
+def attn_keep_mask(B, T, H, p_drop, device):
+    """uint32 buffer for the forward's dropout keep bits, read by the fused backward (None without
+    dropout or when the fused backward does not apply)."""
+    if p_drop <= 0 or not fused_bwd_enabled(T):
+        return None
+    return torch.empty(lib().rdx_attn_keep_mask_words(B, T, H), device=device, dtype=torch.int32)
+
+
+def attn_bwd_launch(q, ldq, k, ldk, v, ldv, gate, rel, mask, seed, salt, p_drop, o, ldo, lse, do, lddo, D, dq, dk, dv,
+                    ldg, dgate, B, T, H, stream):
+    """One gated-attention backward: the fused one-workgroup-per-(b, h) kernel when T <= 224 (dropout from
+    the forward's keep mask), else the query-stationary dQ + key-stationary dK/dV kernel pair (dropout
+    re-hashed from the seed). rel: the [H, 2T - 1] relative-position bias table."""
+    if fused_bwd_enabled(T):
+        if p_drop > 0 and mask is None:
+            raise RuntimeError("fused attention backward with dropout needs the forward's keep mask")
+        return check(lib().rdx_attn_bwd_fused(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
+                                              _p(mask) if mask is not None else None, p_drop, 0.125, o, ldo, _p(lse),
+                                              do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate), B, T, H, 64, stream),
+                     "attn_bwd_fused")
+    return check(lib().rdx_attn_bwd(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel), seed, salt, p_drop, 0.125, o, ldo,
+                                    _p(lse), do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate), B, T, H, 64, stream),
+                 "attn_bwd")
 
 
 class GatedAttention(torch.autograd.Function):
@@ -609,21 +649,23 @@ class GatedAttention(torch.autograd.Function):
         if pos_bias.requires_grad:
             raise ValueError("radhip attention: the position bias must be frozen")
         gate = gate.contiguous().float()
-        pb = pad_position_bias(pos_bias.detach().float())
+        rel = rel_bias_table(pos_bias)
         o = torch.empty(B, T, E, device=q.device, dtype=q.dtype)
         lse = torch.empty(B, H, T, device=q.device, dtype=torch.float32)
         sd = seed if seed is not None else torch.zeros(1, dtype=torch.int64, device=q.device)
+        mask = attn_keep_mask(B, T, H, float(p_drop), q.device)
         with _timed("attn_fwd", q, 2.0 * 2 * B * H * T * T * 64):
-            check(lib().rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), pb.shape[2],
-                                     _p(sd), int(salt),
-                                     float(p_drop), 0.125, _p(o), E, _p(lse), B, T, H, 64, _stream(q)), "attn_fwd")
-        ctx.save_for_backward(q, k, v, gate, pb, sd, o, lse)
+            check(lib().rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(rel),
+                                     _p(sd), int(salt), float(p_drop), 0.125, _p(o), E, _p(lse),
+                                     _p(mask) if mask is not None else None, B, T, H, 64, _stream(q)), "attn_fwd")
+        ctx.mask = mask
+        ctx.save_for_backward(q, k, v, gate, rel, sd, o, lse)
         ctx.p, ctx.salt = float(p_drop), int(salt)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, gate, pb, sd, o, lse = ctx.saved_tensors
+        q, k, v, gate, rel, sd, o, lse = ctx.saved_tensors
         B, T, E = q.shape
         H = gate.shape[2]
         do = do.to(q.dtype).contiguous()
@@ -632,10 +674,8 @@ class GatedAttention(torch.autograd.Function):
         dk, dv = torch.empty_like(dq), torch.empty_like(dq)
         dgate = torch.empty(B, T, H, device=q.device, dtype=torch.float32)
         with _timed("attn_bwd", q, 2.0 * 5 * B * H * T * T * 64):
-            check(lib().rdx_attn_bwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(pb), pb.shape[2],
-                                     _p(sd), ctx.salt,
-                                     ctx.p, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D), _p(dq), _p(dk), _p(dv), E,
-                                     _p(dgate), B, T, H, 64, _stream(q)), "attn_bwd")
+            attn_bwd_launch(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), gate, rel, ctx.mask, _p(sd), ctx.salt,
+                            ctx.p, _p(o), E, lse, _p(do), E, D, _p(dq), _p(dk), _p(dv), E, dgate, B, T, H, _stream(q))
         return dq, dk, dv, dgate, None, None, None, None
 
 
@@ -645,5 +685,17 @@ def attention_dropout_mask(seed, salt, p_drop, shape):
     for s in shape:
         n *= s
     keep = torch.empty(n, dtype=torch.uint8, device=seed.device)
-    check(lib().rdx_attn_dropout_mask(_p(seed), int(salt), float(p_drop), _p(keep), n, _stream(seed)), "attn_mask")
+    check(lib().rdx_attn_dropout_mask(_p(seed), int(salt), float(p_drop), _p(keep), n, int(shape[-1]), _stream(seed)),
+          "attn_mask")
+    return keep.view(*shape)
+
+
+def dropout_mask(seed, salt, p_drop, shape):
+    """The keep mask (uint8) of the element-wise counter-hash dropout of csrc/wavlm_layer.hip (hidden and
+    LoRA dropouts of the fused WavLM layer) over elements [*shape] in row-major order (tests)."""
+    n = 1
+    for s in shape:
+        n *= s
+    keep = torch.empty(n, dtype=torch.uint8, device=seed.device)
+    check(lib().rdx_dropout_mask(_p(seed), int(salt), float(p_drop), _p(keep), n, _stream(seed)), "dropout_mask")
     return keep.view(*shape)

@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from ._lib import check, lib
-from .ops import _p, _stream, _timed, pad_position_bias
+from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, rel_bias_table
 
 E_FUSED = 1024
 
@@ -124,7 +124,7 @@ class WavLMLayerFn(torch.autograd.Function):
     (lora_A q, lora_B q, lora_A v, lora_B v, fp32 leaves, or None)."""
 
     @staticmethod
-    def forward(ctx, h, aq, bq, av, bv, layer, cache, pb, seed, index, p_hidden, p_attn, p_lora, scale):
+    def forward(ctx, h, aq, bq, av, bv, layer, cache, rel, seed, index, p_hidden, p_attn, p_lora, scale):
         B, T, E = h.shape
         H = E // 64
         M = B * T
@@ -150,10 +150,11 @@ class WavLMLayerFn(torch.autograd.Function):
         o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(B, H, T, device=dev, dtype=torch.float32)
         zseed = sd if sd is not None else torch.zeros(1, dtype=torch.int64, device=dev)
+        mask = attn_keep_mask(B, T, H, float(p_attn), dev)
         with _timed("attn_fwd", hf, 2.0 * 2 * B * H * T * T * 64):
-            check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(pb),
-                                     pb.shape[2], _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse), B, T, H, 64, st),
-                  "attn_fwd")
+            check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(rel),
+                                     _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse),
+                                     _p(mask) if mask is not None else None, B, T, H, 64, st), "attn_fwd")
         aout = F.linear(o, cache.wo, cache.bo)
         h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
         x2 = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
@@ -168,8 +169,8 @@ class WavLMLayerFn(torch.autograd.Function):
         fo = F.linear(v, cache.w2, cache.b2)
         out = torch.empty(M, E, device=dev, dtype=torch.float32)
         check(lib().rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st), "wl_residual")
-        ctx.save_for_backward(hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, pb, aq, av)
-        ctx.layer, ctx.cache = layer, cache
+        ctx.save_for_backward(hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, rel, aq, av)
+        ctx.layer, ctx.cache, ctx.mask = layer, cache, mask
         ctx.lora_b = (bq, bv)
         ctx.meta = (B, T, E, H, index, float(p_hidden), float(p_attn), float(p_lora), float(scale), lora,
                     sd is not None)
@@ -177,7 +178,7 @@ class WavLMLayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, pb, aq, av = ctx.saved_tensors
+        hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, rel, aq, av = ctx.saved_tensors
         B, T, E, H, index, p_hidden, p_attn, p_lora, scale, lora, has_seed = ctx.meta
         layer, cache = ctx.layer, ctx.cache
         M = B * T
@@ -203,10 +204,9 @@ class WavLMLayerFn(torch.autograd.Function):
         dqkv = torch.empty(M, 3 * E, device=dev, dtype=torch.bfloat16)
         dgate = torch.empty(M, H, device=dev, dtype=torch.float32)
         with _timed("attn_bwd", hf, 2.0 * 5 * B * H * T * T * 64):
-            check(lib().rdx_attn_bwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(pb),
-                                     pb.shape[2], _p(zseed), int(index), p_attn, 0.125, _p(o), E, _p(lse), _p(do), E, _p(D),
-                                     _p(dqkv), _off(dqkv, E), _off(dqkv, 2 * E), 3 * E, _p(dgate), B, T, H, 64, st),
-                  "attn_bwd")
+            attn_bwd_launch(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, gate, rel, ctx.mask,
+                            _p(zseed), int(index), p_attn, _p(o), E, lse, _p(do), E, D, _p(dqkv), _off(dqkv, E),
+                            _off(dqkv, 2 * E), 3 * E, dgate, B, T, H, st)
         dx1 = torch.mm(dqkv, cache.wext)                                     # [M, E + 2r]
         dh = torch.empty(M, E, device=dev, dtype=torch.float32)
         check(lib().rdx_wl_ln1_bwd(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
@@ -242,7 +242,7 @@ class FusedEncoderRunner:
         key = (T, emb.data_ptr(), emb._version)
         if key != self.pb_key:
             with torch.no_grad():
-                self.pb = pad_position_bias(self.encoder.layers[0].attention.compute_bias(T, device).float())
+                self.pb = rel_bias_table(self.encoder.layers[0].attention.compute_bias(T, device).float())
             self.pb_key = key
         return self.pb
 

@@ -316,14 +316,27 @@ def test_fused_residual_block_matches_torch(dtype, first):
             assert e_f <= 1.5 * e_t + 1e-2, (n, e_f, e_t)
 
 
-@pytest.mark.parametrize("p_drop", [0.0, 0.1])
-def test_gated_attention_matches_torch(p_drop):
+def _toeplitz_bias(H, T, seed=0):
+    """A random relative-position bias: bias[h, i, j] = table[h, j - i + T - 1] (WavLM's bias depends on the
+    key - query offset only, and the kernels take it in that form)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    tab = torch.randn(H, 2 * T - 1, generator=g).to(DEV)
+    i = torch.arange(T, device=DEV)
+    return tab[:, i[None, :] - i[:, None] + T - 1]
+
+
+@pytest.mark.parametrize("bwd", ["fused", "split"])
+@pytest.mark.parametrize("p_drop,H", [(0.0, 4), (0.1, 4), (0.1, 16)])
+def test_gated_attention_matches_torch(p_drop, H, bwd, monkeypatch):
     """Fused MFMA WavLM attention (gated rel-pos bias formed in registers, hashed dropout) vs an fp32
     torch reference fed the same bf16 inputs and the kernel's own dropout mask; forward and the q/k/v/
-    gate gradients. k is a strided column view of a fused q|k|v tensor (as in the model)."""
+    gate gradients, through both backward paths (the one-launch fused kernel and the dQ + dK/dV pair).
+    k is a strided column view of a fused q|k|v tensor (as in the model). H = 16 takes the fused
+    kernel's head-per-XCD block mapping."""
     from radhip.ops import GatedAttention, attention_dropout_mask
+    monkeypatch.setenv("RADHIP_ATTN_BWD", bwd)
     torch.manual_seed(0)
-    B, T, H, D = 2, 201, 4, 64
+    B, T, D = 2, 201, 64
     E = H * D
     qkv = (0.5 * torch.randn(B, T, 3 * E, device=DEV)).to(torch.bfloat16)
     q = qkv[..., :E].contiguous().requires_grad_()
@@ -331,7 +344,7 @@ def test_gated_attention_matches_torch(p_drop):
     k = k_full[..., E:2 * E]
     v = qkv[..., 2 * E:].contiguous().requires_grad_()
     gate = torch.rand(B, T, H, device=DEV).mul(2).requires_grad_()
-    pb = torch.randn(H, T, T, device=DEV)
+    pb = _toeplitz_bias(H, T)
     seed = torch.tensor([1234567], dtype=torch.int64, device=DEV)
     o = GatedAttention.apply(q, k, v, gate, pb, seed, p_drop, 3)
     go = torch.randn(B, T, E, device=DEV).to(torch.bfloat16)
@@ -364,16 +377,17 @@ def test_gated_attention_matches_torch(p_drop):
         assert not torch.equal(o3, o)
 
 
-@pytest.mark.parametrize("B,T,H", [(1, 33, 2), (3, 64, 1), (1, 256, 2)])
+@pytest.mark.parametrize("B,T,H", [(1, 33, 2), (3, 64, 1), (2, 224, 8), (1, 225, 2), (1, 256, 2), (3, 2, 16)])
 def test_gated_attention_ragged_lengths(B, T, H):
-    """Sequence lengths with a one-row last tile, an exact tile multiple and the 256-row maximum: forward and
-    gradients against the fp32 torch reference (no dropout)."""
+    """Sequence lengths with a one-row last tile, an exact tile multiple, the fused backward's 224-row
+    maximum, the first length past it (dQ + dK/dV pair), the 256-row maximum and two frames: forward
+    and gradients against the fp32 torch reference (no dropout)."""
     from radhip.ops import GatedAttention
     torch.manual_seed(T)
     E = H * 64
     q, k, v = ((0.5 * torch.randn(B, T, E, device=DEV)).to(torch.bfloat16).requires_grad_() for _ in range(3))
     gate = (torch.rand(B, T, H, device=DEV) * 2).requires_grad_()
-    pb = torch.randn(H, T, T, device=DEV)
+    pb = _toeplitz_bias(H, T, seed=T)
     o = GatedAttention.apply(q, k, v, gate, pb, None, 0.0, 0)
     go = torch.randn(B, T, E, device=DEV).to(torch.bfloat16)
     o.backward(go)
@@ -437,3 +451,14 @@ def test_sincnet_block0_backward_kernel(N, H, W):
     torch.autograd.backward([cr, ir], [gc.float(), gi.float()])
     for got, ref in ((x.grad, xr.grad), (w1.grad, w1r.grad), (wd.grad, wdr.grad)):
         assert ((got.float() - ref).norm() / ref.norm()).item() < 1e-3
+
+
+def test_attention_rejects_non_toeplitz_bias():
+    """The kernels take the bias as a relative-position table; a bias that is not a function of key - query
+    is refused loudly rather than silently mis-read."""
+    from radhip.ops import GatedAttention
+    T, H = 40, 2
+    q = torch.randn(1, T, H * 64, device=DEV).to(torch.bfloat16)
+    gate = torch.rand(1, T, H, device=DEV)
+    with pytest.raises(ValueError, match="Toeplitz"):
+        GatedAttention.apply(q, q, q, gate, torch.randn(H, T, T, device=DEV), None, 0.0, 0)

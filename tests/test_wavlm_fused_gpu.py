@@ -41,10 +41,13 @@ def _encoder(n_layers=2, inter=512, p=0.1, seed=0):
 
 
 def _mask(seed, salt, p, shape):
-    from radhip.ops import attention_dropout_mask
+    """Scaled keep mask: attention scores [B, H, T, T] use the attention kernels' paired hash, the
+    layer's [M, E] hidden / LoRA dropouts the element-wise hash."""
+    from radhip.ops import attention_dropout_mask, dropout_mask
     if p == 0:
         return torch.ones(shape, device=DEV)
-    return attention_dropout_mask(seed, salt, p, shape).float() / (1 - p)
+    fn = attention_dropout_mask if len(shape) == 4 else dropout_mask
+    return fn(seed, salt, p, shape).float() / (1 - p)
 
 
 def _ref_layer(layer, i, h, pb, seed, p):
@@ -121,8 +124,10 @@ def test_fused_layers_match_fp32_restatement(p, B, inter):
         prm.grad = None
     # fp32 restatement with the same masks
     hr = h0
+    ii = torch.arange(T, device=DEV)
+    pb_full = pb[:, ii[None, :] - ii[:, None] + T - 1]          # relative-position table -> [H, T, T]
     for i, layer in enumerate(enc.layers):
-        hr = _ref_layer(layer, i, hr, pb[:, :, :T], seed, p)
+        hr = _ref_layer(layer, i, hr, pb_full, seed, p)
     (hr * gout).sum().backward()
     assert _rel(got_h, hr.detach()) < 3e-2
     assert _rel(got_g, h0.grad) < 3e-2

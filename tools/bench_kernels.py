@@ -39,7 +39,8 @@ def main():
     qkv = torch.randn(B, T, 3 * E, device=dev, dtype=torch.bfloat16)
     q, k, v = (t.detach().requires_grad_(True) for t in (qkv[..., :E], qkv[..., E:2 * E], qkv[..., 2 * E:]))
     gate = torch.rand(B, T, H, device=dev) + 1.0
-    pb = torch.randn(H, T, T, device=dev)
+    ii = torch.arange(T, device=dev)
+    pb = torch.randn(H, 2 * T - 1, device=dev)[:, ii[None, :] - ii[:, None] + T - 1]   # relative-position bias
     seed = torch.tensor([7], dtype=torch.int64, device=dev)
     do = torch.randn(B, T, E, device=dev, dtype=torch.bfloat16)
     out["attn_fwd_us"] = timed(lambda: GatedAttention.apply(q, k, v, gate, pb, seed, 0.1, 0), 20)
