@@ -316,6 +316,24 @@ int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx,
 int rdx_wl_lora_pack(int nl, const float* const* bq, const float* const* bv, void* const* wext, int64_t ldw,
                      int r, float scale, int E, void* stream);
 
+/* ---- bf16 MFMA GEMM with fused epilogues: the WavLM layer's projections (q|k|v + LoRA columns,
+ * out_proj, FFN1, FFN2 of HF WavLMEncoderLayerStableLayerNorm, src/models/DualStreamSEMamba.py:292-439)
+ * and their input gradients (the transposed frozen weight as B) --------------------------------------
+ * C[M, N] = A[M, K] . B[N, K]^T, bf16 rows (lda, ldb multiples of 8, 16-byte aligned), fp32 accumulate.
+ * epilogue RDX_EPI_BIAS: C bf16 = acc + bias (bias bf16 [N] or NULL);
+ *          RDX_EPI_BIAS_GELU: C = u = bf16(acc + bias), aux_out bf16 [M, ldao] = gelu(u) (erf form);
+ *          RDX_EPI_GELU_BWD: C bf16 = bf16(acc) * gelu'(aux), aux = u bf16 [M, ldaux];
+ *          RDX_EPI_RESID_DROP: C fp32 = aux fp32 [M, ldaux] + bf16(acc + bias) * dropout_p, the
+ *            element-wise hash of element m * N + n with seed f(seed_dev[0], salt) (rdx_dropout_mask).
+ * Requires K % 8 == 0, N % 4 == 0. */
+#define RDX_EPI_BIAS 0
+#define RDX_EPI_BIAS_GELU 1
+#define RDX_EPI_GELU_BWD 2
+#define RDX_EPI_RESID_DROP 3
+int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                  const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao,
+                  const int64_t* seed_dev, int salt, float p_drop, void* stream);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

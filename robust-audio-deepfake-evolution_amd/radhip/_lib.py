@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("RADHIP_LIB", os.path.join(_HERE, "libradhip.so"))
 
 RDX_F32 = 0
 RDX_BF16 = 1
+EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_RESID_DROP = 0, 1, 2, 3
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -90,6 +91,8 @@ SIGNATURES = {
     "rdx_sincnet_b0_bwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),
     "rdx_posconv_fwd": (c_int, [c_vp] * 5 + [c_int, c_int, c_vp]),
     "rdx_posconv_bwd": (c_int, [c_vp] * 4 + [c_int, c_int, c_vp]),
+    "rdx_gemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
+                              c_vp, c_i64, c_vp, c_int, c_f32, c_vp]),
     "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp, c_i64,
                              c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_attn_keep_mask_words": (c_i64, [c_int, c_int, c_int]),

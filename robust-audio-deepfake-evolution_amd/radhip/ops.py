@@ -699,3 +699,35 @@ def dropout_mask(seed, salt, p_drop, shape):
     keep = torch.empty(n, dtype=torch.uint8, device=seed.device)
     check(lib().rdx_dropout_mask(_p(seed), int(salt), float(p_drop), _p(keep), n, _stream(seed)), "dropout_mask")
     return keep.view(*shape)
+
+
+# --------------------------------------------------------------------------- bf16 GEMM --------
+def gemm_flops(M, N, K):
+    return 2.0 * M * N * K
+
+
+def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, seed=None, salt=0, p_drop=0.0,
+         name="gemm"):
+    """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on the hand-written MFMA kernel (csrc/gemm.hip):
+    bf16 row views a, b (unit inner stride); returns C (bf16, or fp32 for EPI_RESID_DROP)."""
+    _require_gpu(a, b)
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip gemm: bf16 operands with unit inner stride required")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"radhip gemm: K mismatch {K} vs {K2}")
+    if out is None:
+        dt = torch.float32 if epilogue == _lib.EPI_RESID_DROP else torch.bfloat16
+        out = torch.empty(M, N, device=a.device, dtype=dt)
+    if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
+        aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    with _timed(name, a, gemm_flops(M, N, K)):
+        check(lib().rdx_gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+                                  _p(bias) if bias is not None else None, int(epilogue),
+                                  _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                                  _p(aux_out) if aux_out is not None else None,
+                                  aux_out.stride(0) if aux_out is not None else 0,
+                                  _p(seed) if seed is not None else None, int(salt), float(p_drop), _stream(a)),
+              "gemm_bf16")
+    return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out

@@ -158,12 +158,17 @@ def test_cli_full_resume_equals_continuous(tmp_path, golden):
     cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--resume", str(state0),
                              "--comment", "res"]))
     res = out / "LA_Tiny_ep2_bs2_res"
+    # Tensor-wise relative L2 distance: the runs are not bitwise reproducible (fp32 atomics in the LoRA and
+    # scan gradient kernels), and AdamW's first steps move a weight by ~lr * sign(g), so an element whose
+    # gradient is ~0 can move either way; a lost optimizer / scheduler / RNG state moves whole tensors.
     for f in ("checkpoint_epoch_001.pth", "swa.pth", "best.pth"):
         a = torch.load(cont / "weights" / f, weights_only=True)
         b = torch.load(res / "weights" / f, weights_only=True)
         assert a.keys() == b.keys()
         for k in a:
-            torch.testing.assert_close(b[k].float(), a[k].float(), rtol=1e-4, atol=2e-6, msg=f"{f}:{k}")
+            x, y = a[k].double(), b[k].double()
+            rel = float((x - y).norm() / x.norm().clamp_min(1e-12))
+            assert rel < 1e-3, (f, k, rel)
     sa = [float(ln.split()[3]) for ln in (cont / "metrics" / "dev_score.txt").read_text().splitlines()]
     sb = [float(ln.split()[3]) for ln in (res / "metrics" / "dev_score.txt").read_text().splitlines()]
     np.testing.assert_allclose(sb, sa, rtol=1e-3, atol=1e-4)

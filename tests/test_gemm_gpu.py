@@ -1,0 +1,90 @@
+"""The hand-written bf16 MFMA GEMM (csrc/gemm.hip) with its fused epilogues against torch fp32 references
+of the same unfused math, at the WavLM layer's shapes (M = 8 x 201 and 32 x 201 tokens; the q|k|v +
+LoRA, out_proj, FFN1 and FFN2 projections and their input gradients) and ragged edges.
+Tolerances: bf16 operands with fp32 accumulation vs an fp32 GEMM of the same bf16 operands, 1e-2
+relative (max-norm) before the final bf16 rounding; the dropout mask of the residual epilogue is the
+element-wise hash (rdx_dropout_mask) and must match exactly."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12))
+
+
+def _ops(M, N, K, seed=0, lda=None):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lda = lda or K
+    a_full = torch.randn(M, lda, generator=g).to(DEV).to(torch.bfloat16)
+    a = a_full[:, :K]
+    b = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(N, generator=g)).to(DEV).to(torch.bfloat16)
+    return a, b, bias
+
+
+@pytest.mark.parametrize("M,N,K", [(1608, 3072, 1040), (1608, 1024, 1024), (6432, 4096, 1024), (1608, 1024, 4096),
+                                   (1608, 1040, 3072), (1, 4, 8), (130, 132, 72), (257, 260, 136)])
+def test_gemm_bias_matches_fp32(M, N, K):
+    from radhip.ops import gemm
+    a, b, bias = _ops(M, N, K)
+    got = gemm(a, b, bias)
+    ref = a.float() @ b.float().t() + bias.float()
+    assert got.dtype == torch.bfloat16 and got.shape == (M, N)
+    assert _rel(got, ref) < 1e-2
+    got0 = gemm(a, b)                                   # no bias
+    assert _rel(got0, a.float() @ b.float().t()) < 1e-2
+
+
+def test_gemm_strided_operand_view():
+    """A as a column slice of a wider buffer (lda > K), as the LoRA-extended x1 is used."""
+    from radhip.ops import gemm
+    a, b, bias = _ops(333, 256, 1040, lda=1088)
+    assert a.stride(0) == 1088
+    assert _rel(gemm(a, b, bias), a.float() @ b.float().t() + bias.float()) < 1e-2
+
+
+def test_gemm_bias_gelu_epilogue():
+    from radhip import _lib
+    from radhip.ops import gemm
+    a, b, bias = _ops(1608, 4096, 1024, seed=1)
+    u, v = gemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU)
+    ref_u = (a.float() @ b.float().t() + bias.float())
+    assert _rel(u, ref_u) < 1e-2
+    # v is gelu of the stored (bf16) u, exactly as the unfused GELU kernel computes it
+    ref_v = torch.nn.functional.gelu(u.float())
+    assert _rel(v, ref_v) < 1e-2
+    assert float((v.float() - ref_v.to(torch.bfloat16).float()).abs().max()) <= 2 ** -7 * float(ref_v.abs().max())
+
+
+def test_gemm_gelu_backward_epilogue():
+    from radhip import _lib
+    from radhip.ops import gemm
+    a, b, _ = _ops(1608, 4096, 1024, seed=2)
+    u = torch.randn(1608, 4096, device=DEV).to(torch.bfloat16)
+    du = gemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=u)
+    dv = (a.float() @ b.float().t()).to(torch.bfloat16).float()
+    x = u.float()
+    grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    assert _rel(du, dv * grad) < 2e-2
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_residual_dropout_epilogue(p):
+    from radhip import _lib
+    from radhip.ops import dropout_mask, gemm
+    M, N, K = 1608, 1024, 4096
+    a, b, bias = _ops(M, N, K, seed=3)
+    h = torch.randn(M, N, device=DEV)
+    seed = torch.tensor([4242], dtype=torch.int64, device=DEV)
+    out = gemm(a, b, bias, epilogue=_lib.EPI_RESID_DROP, aux=h, seed=seed, salt=7, p_drop=p)
+    assert out.dtype == torch.float32
+    fo = (a.float() @ b.float().t() + bias.float()).to(torch.bfloat16).float()
+    mk = dropout_mask(seed, 7, p, (M, N)).float() / (1 - p) if p > 0 else torch.ones_like(h)
+    ref = h + fo * mk
+    assert _rel(out - h, ref - h) < 2e-2
+    if p > 0:   # the mask itself is exact: dropped elements carry h unchanged
+        dropped = mk == 0
+        assert torch.equal(out[dropped], h[dropped])
