@@ -55,6 +55,11 @@ int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch, int64_t l
                                         const float* filters, int channels, int ksize,
                                         const int32_t* mask_dev, int mask_stride, float* out,
                                         void* stream);
+/* RawNet2 front end (legacy plugin, models/RawNet2Spoof.py:77-103 SincConv.forward and :244-245
+ * `F.max_pool1d(torch.abs(x), 3)`): the same fused sinc conv + |.|, pooled over time only.
+ *   out [batch, channels, (len-ksize+1)/3] fp32 = max over 3 consecutive conv times of |conv| */
+int rdx_sincconv_abspool1d_fwd(const float* x, int64_t batch, int64_t len, const float* filters,
+                               int channels, int ksize, int mask_lo, int mask_hi, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Bidirectional Mamba (replaces mamba_ssm Mamba.forward -> mamba_inner_fn, called twice per

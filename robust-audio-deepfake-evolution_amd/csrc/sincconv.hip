@@ -16,6 +16,11 @@ namespace rdx {
 
 constexpr int SINC_T3 = 256;  // pooled outputs per block (= threads)
 
+// kPoolC = true : MaxPool2d((3, 3)) over (channel, time) of |conv|  -> out [B, C/3, T/3]   (AASIST / SincNet)
+// kPoolC = false: MaxPool1d(3) over time of |conv|, per channel      -> out [B, C, T/3]     (RawNet2)
+// Either way a lane sweeps channel triples with 3 channels x 3 conv times of accumulators; in the
+// per-channel form a trailing partial triple clamps its filter rows and skips their stores.
+template <bool kPoolC>
 __global__ __launch_bounds__(SINC_T3) void sincconv_absmaxpool_kernel(
     const float* __restrict__ x, int64_t len, const float* __restrict__ filters, int channels, int K,
     int mask_lo, int mask_hi, const int32_t* __restrict__ mask_dev, int mask_stride, float* __restrict__ out,
@@ -38,12 +43,12 @@ __global__ __launch_bounds__(SINC_T3) void sincconv_absmaxpool_kernel(
   const int64_t t3 = t3_0 + threadIdx.x;
   const bool valid = t3 < T3;
   const float* sx = s_x + 3 * threadIdx.x;
-  float* ob = out + (int64_t)b * C3 * T3;
+  float* ob = out + (int64_t)b * (kPoolC ? C3 : channels) * T3;
   for (int c3 = 0; c3 < C3; ++c3) {
     const int c0 = 3 * c3;
     const float* w0 = filters + (int64_t)c0 * K;
-    const float* w1 = w0 + K;
-    const float* w2 = w1 + K;
+    const float* w1 = filters + (int64_t)min(c0 + 1, channels - 1) * K;
+    const float* w2 = filters + (int64_t)min(c0 + 2, channels - 1) * K;
     const bool m0 = (c0 >= mask_lo && c0 < mask_hi);
     const bool m1 = (c0 + 1 >= mask_lo && c0 + 1 < mask_hi);
     const bool m2 = (c0 + 2 >= mask_lo && c0 + 2 < mask_hi);
@@ -63,7 +68,14 @@ __global__ __launch_bounds__(SINC_T3) void sincconv_absmaxpool_kernel(
     float r0 = m0 ? 0.f : fmaxf(fabsf(a00), fmaxf(fabsf(a01), fabsf(a02)));
     float r1 = m1 ? 0.f : fmaxf(fabsf(a10), fmaxf(fabsf(a11), fabsf(a12)));
     float r2 = m2 ? 0.f : fmaxf(fabsf(a20), fmaxf(fabsf(a21), fabsf(a22)));
-    if (valid) ob[(int64_t)c3 * T3 + t3] = fmaxf(r0, fmaxf(r1, r2));
+    if (!valid) continue;
+    if (kPoolC) {
+      ob[(int64_t)c3 * T3 + t3] = fmaxf(r0, fmaxf(r1, r2));
+    } else {
+      ob[(int64_t)c0 * T3 + t3] = r0;
+      if (c0 + 1 < channels) ob[(int64_t)(c0 + 1) * T3 + t3] = r1;
+      if (c0 + 2 < channels) ob[(int64_t)(c0 + 2) * T3 + t3] = r2;
+    }
   }
 }
 
@@ -83,7 +95,7 @@ extern "C" int rdx_sincconv_absmaxpool_fwd(const float* x, int64_t batch, int64_
   if (ksize > 4096) return RDX_EUNSUPPORTED;
   dim3 grid((unsigned)((T3 + SINC_T3 - 1) / SINC_T3), (unsigned)batch);
   size_t smem = sizeof(float) * (3 * SINC_T3 + ksize - 1 + 2);
-  hipLaunchKernelGGL(sincconv_absmaxpool_kernel, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
+  hipLaunchKernelGGL(sincconv_absmaxpool_kernel<true>, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
                      filters, channels, ksize, mask_lo, mask_hi, (const int32_t*)nullptr, 0, out, T3, C3);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
@@ -102,8 +114,28 @@ extern "C" int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch
   if (ksize > 4096) return RDX_EUNSUPPORTED;
   dim3 grid((unsigned)((T3 + SINC_T3 - 1) / SINC_T3), (unsigned)batch);
   size_t smem = sizeof(float) * (3 * SINC_T3 + ksize - 1 + 2);
-  hipLaunchKernelGGL(sincconv_absmaxpool_kernel, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
+  hipLaunchKernelGGL(sincconv_absmaxpool_kernel<true>, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
                      filters, channels, ksize, 0, 0, mask_dev, mask_stride, out, T3, C3);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+// RawNet2 front end: |SincConv| then MaxPool1d(3) over time, channel by channel (no channel pooling).
+//   reference models/RawNet2Spoof.py:95-103 (F.conv1d with the sinc bank) and :244-245
+//   (F.max_pool1d(torch.abs(x), 3)).  x [B, len] -> out [B, channels, (len-ksize+1)/3].
+extern "C" int rdx_sincconv_abspool1d_fwd(const float* x, int64_t batch, int64_t len, const float* filters,
+                                          int channels, int ksize, int mask_lo, int mask_hi, float* out,
+                                          void* stream) {
+  RDX_REQUIRE(x && filters && out && batch > 0 && channels >= 1 && ksize > 0 && len >= ksize);
+  RDX_REQUIRE(batch <= 65535);
+  const int64_t T3 = (len - ksize + 1) / 3;
+  const int C3 = (channels + 2) / 3;
+  if (T3 <= 0) return RDX_EINVAL;
+  if (ksize > 4096) return RDX_EUNSUPPORTED;
+  dim3 grid((unsigned)((T3 + SINC_T3 - 1) / SINC_T3), (unsigned)batch);
+  size_t smem = sizeof(float) * (3 * SINC_T3 + ksize - 1 + 2);
+  hipLaunchKernelGGL(sincconv_absmaxpool_kernel<false>, grid, dim3(SINC_T3), smem, as_stream(stream), x, len,
+                     filters, channels, ksize, mask_lo, mask_hi, (const int32_t*)nullptr, 0, out, T3, C3);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

@@ -240,8 +240,8 @@ class Runner:
     def make_stepper(self, trainer, B):
         """How micro-batches execute: the accumulation window (HIP graphs, radhip/window.py), the
         per-micro-batch graphs (GraphedMicroStep), or eager launches."""
-        if self.args.eager:
-            return "eager", None
+        if self.args.eager or not hasattr(trainer.model, "wavlm_stream"):
+            return "eager", None        # the captured steps drive the dual-stream model's device-side draws
         if not self.args.no_window and window_eligible(trainer):
             w = WindowStep(trainer, B)
             for k in range(w.K):            # capture needs one staged window of draws

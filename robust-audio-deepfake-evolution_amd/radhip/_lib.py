@@ -59,6 +59,7 @@ SIGNATURES = {
     "rdx_version": (ctypes.c_char_p, []),
     "rdx_strerror": (ctypes.c_char_p, [c_int]),
     "rdx_sincconv_absmaxpool_fwd": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "rdx_sincconv_abspool1d_fwd": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "rdx_sincconv_absmaxpool_fwd_devmask": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_vp, c_int, c_vp,
                                                     c_vp]),
     "rdx_dwconv_bidir_fwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),

@@ -1,0 +1,116 @@
+"""Per-utterance augmentation API of the reference, on the same HIP kernels as the batched train path.
+
+  RawBoost(algo_id, fs).process(x)         src/rawboost.py:9-33  (algorithms :36-95)
+  apply_codec_aug(waveform, sample_rate)   src/data_utils.py:31-59
+
+Same names, arguments and host RNG consumption as the reference: every random parameter is drawn from
+numpy's global RNG (RawBoost) or python's `random` (codec gates) in the reference's order, so a caller
+interleaving these calls with its own draws sees the same stream. The signal work runs on the GPU
+(csrc/augment.hip: fp64 IIR for the LnL filters, batched polyphase resampling), one utterance per launch.
+
+Deviations, both shared with the batched path (radhip.train.Augmenter) and documented in DESIGN.md:
+  * ISD / SSI per-sample noise comes from a device Philox stream keyed by one 62-bit seed drawn from the
+    numpy RNG, instead of len(x) numpy normals (statistically equivalent, not sample-identical);
+  * signals are processed as fp32 (the model consumes fp32); `process` returns float64 like the
+    reference, `apply_codec_aug` float32 like the reference's torch round trip.
+Errors are raised, not swallowed: the reference's try/except fallbacks (rawboost in __getitem__,
+codec :55-57) would hide a missing HIP library.
+"""
+import random
+
+import numpy as np
+import torch
+
+from . import _lib
+from .ops import rawboost_batch, resample_batch, resample_kernel
+
+CODEC_RATES = (8000, 6000, 4000)
+
+
+def draw_rawboost(n, algo):
+    """Host draws of one RawBoost call for an utterance of n samples, after the algorithm choice, in
+    the order of rawboost.py:36-95 (LnL: n_a, the unused `a`, 5 numerator and n_a denominator taps, f;
+    ISD: beta; SSI: SNR), plus the Philox seed of the ISD / SSI noise."""
+    r = _lib.RawboostUtt()
+    r.len = n
+    r.algo = algo
+    if algo in (1, 4):
+        n_a = [1, 2, 3, 4, 5][np.random.randint(0, 5)]
+        np.random.randint(0, 90)                          # the unused `a` draw (rawboost.py:40)
+        b = np.array([1.0])
+        for _ in range(5):
+            b = np.convolve(b, [1.0, np.random.uniform(-1, 1)])
+        a = np.array([1.0])
+        for _ in range(n_a):
+            a = np.convolve(a, [1.0, np.random.uniform(-0.1, 0.1)])
+        r.n_a = n_a
+        r.b[:] = list(b)
+        aa = np.zeros(6)
+        aa[:len(a)] = a
+        r.a[:] = list(aa)
+        r.f = float(np.random.randn())
+    if algo in (2, 4):
+        r.beta = float(list(range(5, 10))[np.random.randint(0, 5)])
+    if algo == 3:
+        r.snr_db = float(np.random.uniform(10, 40))
+    if algo in (2, 3, 4):
+        r.seed = int(np.random.randint(0, 2 ** 62, dtype=np.int64))
+    return r
+
+
+def _device(device):
+    return torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+class RawBoost:
+    """Drop-in of src/rawboost.py::RawBoost: process(x) picks one of algo_id per call (np.random.randint,
+    :18) — 0 = none, 1 LnL convolutive, 2 ISD impulsive, 3 SSI stationary, 4 LnL then ISD."""
+
+    def __init__(self, algo_id=(0, 1, 2, 3, 4), fs=16000, device=None):
+        self.algo_id = list(algo_id)
+        self.fs = fs
+        self.device = device
+
+    def process(self, x):
+        algo = self.algo_id[np.random.randint(0, len(self.algo_id))]
+        if algo not in (1, 2, 3, 4):
+            return x
+        x = np.asarray(x).reshape(-1)
+        rec = draw_rawboost(len(x), algo)
+        rec.offset = 0
+        dev = _device(self.device)
+        out = rawboost_batch(torch.from_numpy(x.astype(np.float32)).to(dev), [rec])
+        return out.cpu().numpy().astype(np.float64)
+
+
+_KERNELS = {}
+
+
+def _resample_kernel_dev(a, b, dev):
+    key = (a, b, str(dev))
+    if key not in _KERNELS:
+        k, w, og, ng = resample_kernel(a, b)
+        _KERNELS[key] = (k.reshape(-1).to(dev), w, og, ng)
+    return _KERNELS[key]
+
+
+def apply_codec_aug(waveform_np, sample_rate=16000, device=None):
+    """Band-limiting "codec" augmentation (data_utils.py:31-59): with probability 0.5, resample to
+    8/6/4 kHz (random.choice) and back with torchaudio's default sinc-Hann kernel (width 6, rolloff 0.99),
+    on the GPU. Returns the input object unchanged when the gate is not taken."""
+    if random.random() < 0.5:
+        target_sr = random.choice(list(CODEC_RATES))
+        dev = _device(device)
+        x = waveform_np.reshape(-1) if isinstance(waveform_np, torch.Tensor) else np.asarray(waveform_np).reshape(-1)
+        x = torch.as_tensor(x, dtype=torch.float32).to(dev)
+        kd, wd, ogd, ngd = _resample_kernel_dev(sample_rate, target_sr, dev)
+        ku, wu, ogu, ngu = _resample_kernel_dev(target_sr, sample_rate, dev)
+        n = x.numel()
+        nd = -(-ngd * n // ogd)
+        nu = -(-ngu * nd // ogu)
+        mid = torch.empty(nd, device=dev)
+        out = torch.empty(nu, device=dev)
+        resample_batch(x, mid, kd, [_lib.ResampleJob(0, n, 0, nd, ogd, ngd, wd, 0)])
+        resample_batch(mid, out, ku, [_lib.ResampleJob(0, nd, 0, nu, ogu, ngu, wu, 0)])
+        return out.cpu().numpy()
+    return waveform_np

@@ -4,6 +4,7 @@ get_model (reference src/main.py:799-812): `models.<architecture>.Model(Args(mod
 apply_lora_to_wavlm (reference src/main.py:103-158): freeze the WavLM base, inject LoRA (r, alpha,
 dropout, q_proj/v_proj) with peft's state-dict layout, no silent fallback.
 """
+import inspect
 import json
 import os
 from importlib import import_module
@@ -28,12 +29,24 @@ def load_config(path):
         return json.load(f)
 
 
+def legacy_plugin(cls):
+    """True for the AASIST-era plugin signature Model(d_args) (models/AASIST.py:470,
+    models/RawNet2Spoof.py:170): one positional argument, the model_config dict itself."""
+    params = [p for p in inspect.signature(cls.__init__).parameters.values()
+              if p.name != "self" and p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)]
+    return len(params) == 1
+
+
 def get_model(model_config, device, extra=None):
+    """models.<architecture>.Model: the Phase-5/6 plugins take (Args(model_config), device) (src/main.py:799-812);
+    the legacy AASIST / RawNet2 plugins take the model_config dict alone (their reference signature, which
+    the reference's own get_model cannot call)."""
     module = import_module("models.{}".format(model_config["architecture"]))
     d = dict(model_config)
     if extra:
         d.update(extra)
-    model = getattr(module, "Model")(Args(d), device)
+    cls = getattr(module, "Model")
+    model = cls(d) if legacy_plugin(cls) else cls(Args(d), device)
     return model.to(device)
 
 

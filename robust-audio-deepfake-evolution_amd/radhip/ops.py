@@ -172,6 +172,23 @@ def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
     return out
 
 
+def sincconv_abspool1d(x, filters, mask_lo=0, mask_hi=0):
+    """|conv1d(x, filters)| max-pooled over 3 conv times per channel: [B, L] -> [B, C, (L-K+1)//3].
+
+    Replaces RawNet2's SincConv.forward + F.max_pool1d(torch.abs(.), 3)
+    (reference models/RawNet2Spoof.py:77-103, :244-245)."""
+    _require_gpu(x, filters)
+    x = x.contiguous().float()
+    filters = filters.contiguous().float()
+    B, L = x.shape
+    C, K = filters.shape
+    out = torch.empty(B, C, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
+    with _timed("sincconv_abspool1d", x, 2.0 * K * B * C * 3 * ((L - K + 1) // 3)):
+        check(lib().rdx_sincconv_abspool1d_fwd(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi),
+                                               _p(out), _stream(x)), "sincconv_abspool1d_fwd")
+    return out
+
+
 # ------------------------------------------------------------------------------ Bi-Mamba -------
 def _rowview_ld(x):
     """x: [B, L, D] view with unit inner stride and rows of stride ld; returns ld."""

@@ -21,11 +21,11 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .augment import CODEC_RATES, draw_rawboost
 from .ops import fgm_attack, pad_mixup, rawboost_batch, resample_batch, resample_kernel
 from .wavlm import compute_time_mask
 
 MAX_LEN = 64600
-CODEC_RATES = (8000, 6000, 4000)
 
 
 # ------------------------------------------------------------------------------- losses ------
@@ -245,32 +245,7 @@ class Augmenter:
 
     # --- host draws (mirror rawboost.py / data_utils.py draw order; per-sample noise -> Philox seed)
     def _draw_rawboost(self, n):
-        r = _lib.RawboostUtt()
-        r.len = n
-        algo = self.algo_ids[np.random.randint(0, len(self.algo_ids))]
-        r.algo = algo
-        if algo in (1, 4):
-            n_a = [1, 2, 3, 4, 5][np.random.randint(0, 5)]
-            np.random.randint(0, 90)                          # the unused `a` draw (rawboost.py:40)
-            b = np.array([1.0])
-            for _ in range(5):
-                b = np.convolve(b, [1.0, np.random.uniform(-1, 1)])
-            a = np.array([1.0])
-            for _ in range(n_a):
-                a = np.convolve(a, [1.0, np.random.uniform(-0.1, 0.1)])
-            r.n_a = n_a
-            r.b[:] = list(b)
-            aa = np.zeros(6)
-            aa[:len(a)] = a
-            r.a[:] = list(aa)
-            r.f = float(np.random.randn())
-        if algo in (2, 4):
-            r.beta = float(list(range(5, 10))[np.random.randint(0, 5)])
-        if algo == 3:
-            r.snr_db = float(np.random.uniform(10, 40))
-        if algo in (2, 3, 4):
-            r.seed = int(np.random.randint(0, 2 ** 62, dtype=np.int64))
-        return r
+        return draw_rawboost(n, self.algo_ids[np.random.randint(0, len(self.algo_ids))])
 
     def codec_len(self, n, sr):
         _, _, ogd, ngd = self.kinfo[(16000, sr)]
@@ -397,7 +372,9 @@ class Trainer:
             self.fgm = FGM(model, emb, tc.get("fgm_epsilon", 1.0), grad_hook=fgm_global_grads)
         warm = int(tc.get("warmup_steps", max(1, int(total_steps * float(tc.get("warmup_ratio", 0.05))))))
         warm = min(max(1, warm), max(1, total_steps - 1))
-        eta_min = oc.get("scheduler_config", {}).get("eta_min", 1e-6)
+        # the reference reads optim_config["scheduler_config"]["eta_min"] (src/main.py:477) and KeyErrors on the
+        # legacy AASIST / RawNet2 confs, which carry no scheduler_config: they fall back to their lr_min
+        eta_min = oc.get("scheduler_config", {}).get("eta_min", oc.get("lr_min", 1e-6))
         w_sched = torch.optim.lr_scheduler.LinearLR(self.opt, start_factor=float(tc.get("warmup_init_factor", 0.1)),
                                                     end_factor=1.0, total_iters=warm)
         c_sched = torch.optim.lr_scheduler.CosineAnnealingLR(self.opt, T_max=max(1, total_steps - warm),
@@ -513,9 +490,9 @@ class Trainer:
 def swa_bn_update(model, feeder, augmenter, device):
     """torchcontrib SWA.bn_update(trn_loader, model) after swap_swa_sgd (src/main.py:669-672): reset every
     BatchNorm's running statistics and recompute them as a cumulative average (momentum b / (n + b)) over
-    one pass of the augmented train loader in train mode. Only the SincNet stream holds BatchNorm, and
-    nothing else it computes is kept, so only that stream runs (the WavLM stream's forward does not
-    touch any BatchNorm statistic)."""
+    one pass of the augmented train loader in train mode. In the dual-stream model only the SincNet stream
+    holds BatchNorm, and nothing else it computes is kept, so only that stream runs (the WavLM stream's
+    forward does not touch any BatchNorm statistic); the legacy plugins run whole."""
     bns = [m for m in model.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
     if not bns:
         return 0
@@ -535,7 +512,10 @@ def swa_bn_update(model, feeder, augmenter, device):
         b = x.shape[0]
         for m in bns:
             m.momentum = b / float(n + b)
-        model.sinc_stream(x, freq_aug=False)
+        if hasattr(model, "sinc_stream"):
+            model.sinc_stream(x, freq_aug=False)
+        else:                       # legacy plugins: BatchNorm all through the network
+            model(x)
         n += b
     for m in bns:
         m.momentum = momenta[m]

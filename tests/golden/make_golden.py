@@ -443,6 +443,128 @@ def gen_train(main):
     npz(os.path.join(HERE, "train_toy.npz"), **arrays)
 
 
+def gen_legacy(ref_root):
+    """Legacy plugins (BASELINE configs 1-2): the reference's models/AASIST.py and models/RawNet2Spoof.py,
+    built from their own confs (src/config/AASIST.conf, RawNet2_baseline.conf) with seeded weights, at the
+    full 64 600-sample input. Two modes per model: eval (BatchNorm running statistics) and train with every
+    Dropout at p = 0 (BatchNorm batch statistics + running-stat update, deterministic). Stores the outputs,
+    every parameter gradient of sum(hidden * r_h) + sum(out * r_o), the updated running stats, and the
+    state_dict key / shape list. The input is seeded_array(f"{arch}.x", (2, 64600), scale=0.1), recomputed
+    by the tests rather than stored."""
+    import copy
+    import importlib.util
+    for arch, conf in (("AASIST", "AASIST.conf"), ("RawNet2Spoof", "RawNet2_baseline.conf")):
+        spec = importlib.util.spec_from_file_location(f"ref_{arch}", os.path.join(ref_root, "models", arch + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        with open(os.path.join(ref_root, "src", "config", conf)) as f:
+            mc = json.load(f)["model_config"]
+        arrays = {}
+        x = seeded_array(f"{arch}.x", (2, 64600), scale=0.1).astype(np.float32)
+        for mode in ("eval", "train"):
+            torch.manual_seed(0)
+            m = mod.Model(copy.deepcopy(mc))
+            seeded_fill_(m, seed=41)
+            # float64 throughout: the block-0 weight gradients reduce over B x 24 x 21490 terms, where an
+            # fp32 CPU oracle is itself ~0.5 % off; the fixture holds the exact values
+            m = m.double()
+            for c in ("conv_time", "Sinc_conv"):
+                if hasattr(m, c):
+                    getattr(m, c).band_pass = getattr(m, c).band_pass.double()
+            if mode == "train":
+                for d in m.modules():
+                    if isinstance(d, torch.nn.Dropout):
+                        d.p = 0.0
+                m.train()
+            else:
+                m.eval()
+            hid, out = m(torch.from_numpy(x).double(), Freq_aug=False)
+            rh = seeded_array(f"{arch}.rh", tuple(hid.shape)).astype(np.float32)
+            ro = seeded_array(f"{arch}.ro", tuple(out.shape)).astype(np.float32)
+            rh64, ro64 = torch.from_numpy(rh).double(), torch.from_numpy(ro).double()
+            ((hid * rh64).sum() + (out * ro64).sum()).backward()
+            arrays[f"{mode}:hidden"] = hid.detach().numpy().astype(np.float32)
+            arrays[f"{mode}:out"] = out.detach().numpy().astype(np.float32)
+            arrays[f"{mode}:rh"] = rh
+            arrays[f"{mode}:ro"] = ro
+            for k, v in grads_of(m).items():
+                arrays[f"{mode}:{k}"] = v
+            if mode == "train":
+                for k, v in m.state_dict().items():
+                    if k.endswith("running_mean") or k.endswith("running_var"):
+                        arrays[f"stat:{k}"] = v.numpy().astype(np.float32)
+            else:
+                sd = m.state_dict()
+                arrays["keys"] = np.array(list(sd.keys()))
+                arrays["shapes"] = np.array([json.dumps(list(v.shape)) for v in sd.values()])
+                arrays["n_params"] = np.array(sum(p.numel() for p in m.parameters()))
+        npz(os.path.join(HERE, f"legacy_{arch}.npz"), **arrays)
+
+
+def gen_getitem(ref_src):
+    """Gate order of Dataset_ASVspoof2019_train.__getitem__ (data_utils.py:163-184), run by the reference
+    itself: RawBoost gate (python random) -> RawBoost draws (numpy) -> codec gate (python random) with
+    apply_codec_aug's inner 0.5 gate and random.choice of the rate -> pad_random's crop start (numpy, on the
+    post-codec length). soundfile and torchaudio are absent: sf.read is stubbed to return a ramp of a
+    per-key length, and T.Resample by a stub that logs (orig, new) and returns torchaudio's output length
+    ceil(new' * n / orig') (gcd-reduced rates, torchaudio's _apply_sinc_resample_kernel). RawBoost is the
+    reference's own, with algo 1 (LnL), whose numpy draw sequence the product reproduces exactly (the ISD /
+    SSI per-sample noise is a documented Philox deviation, so those algorithms would desynchronise the
+    streams). Records per call: rawboost applied, codec rate (0 = none), crop start (-1 = tiled)."""
+    import math
+    import data_utils as DU
+    lens = {f"LA_T_{i:07d}": n for i, n in enumerate([70000, 64601, 30000, 90000, 64000, 100000, 66000, 80000] * 8)}
+    DU.sf.read = lambda path: (np.arange(lens[os.path.basename(str(path))[:-5]], dtype=np.float64) * 1e-5, 16000)
+    log = []
+
+    class Resample:
+        def __init__(self, orig, new):
+            g = math.gcd(int(orig), int(new))
+            self.o, self.n = int(orig) // g, int(new) // g
+            log.append(("resample", int(orig), int(new)))
+
+        def __call__(self, sig):
+            return torch.zeros(sig.shape[0], math.ceil(self.n * sig.shape[-1] / self.o))
+    DU.T.Resample = Resample
+    real_pad_random = DU.pad_random
+
+    def pad_random(x, max_len=64600):
+        st = np.random.get_state()
+        out = real_pad_random(x, max_len)
+        if x.shape[0] >= max_len:
+            rs = np.random.RandomState()
+            rs.set_state(st)
+            log.append(("start", int(rs.randint(x.shape[0] - max_len)), int(x.shape[0])))
+        else:
+            log.append(("start", -1, int(x.shape[0])))
+        return out
+    DU.pad_random = pad_random
+    keys = list(lens)
+    ds = DU.Dataset_ASVspoof2019_train(keys, {k: 0 for k in keys}, __import__("pathlib").Path("/nonexistent"), algo=1, use_codec=True,
+                                       codec_p=0.6, rawboost_p=0.8)
+    real_process = ds.rawboost.process
+
+    def process(x):
+        log.append(("rawboost",))
+        return real_process(x)
+    ds.rawboost.process = process
+    random.seed(2024)
+    np.random.seed(2024)
+    recs = []
+    for k in keys:
+        del log[:]
+        ds[keys.index(k)]
+        rb = int(any(e[0] == "rawboost" for e in log))
+        rates = [e[2] for e in log if e[0] == "resample" and e[1] == 16000]
+        st = [e for e in log if e[0] == "start"][0]
+        recs.append([lens[k], rb, rates[0] if rates else 0, st[1], st[2]])
+    DU.pad_random = real_pad_random
+    with open(os.path.join(HERE, "getitem_order.json"), "w") as f:
+        json.dump({"seed": 2024, "algo": 1, "rawboost_p": 0.8, "use_codec": True, "codec_p": 0.6,
+                   "fields": ["len", "rawboost", "codec_rate", "start", "len_after_codec"], "records": recs}, f)
+    print("wrote getitem_order.json")
+
+
 def main_():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -483,6 +605,10 @@ def main_():
             gen_scorefile(main)
     if want("model"):
         gen_model(DS)
+    if want("legacy"):
+        gen_legacy(args.ref)
+    if want("getitem"):
+        gen_getitem(ref_src)
 
 
 if __name__ == "__main__":

@@ -158,17 +158,20 @@ def test_cli_full_resume_equals_continuous(tmp_path, golden):
     cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--resume", str(state0),
                              "--comment", "res"]))
     res = out / "LA_Tiny_ep2_bs2_res"
-    # Tensor-wise relative L2 distance: the runs are not bitwise reproducible (fp32 atomics in the LoRA and
-    # scan gradient kernels), and AdamW's first steps move a weight by ~lr * sign(g), so an element whose
-    # gradient is ~0 can move either way; a lost optimizer / scheduler / RNG state moves whole tensors.
+    # Tensor-wise L2 distance, judged against how far the second epoch moved each tensor: the runs are not
+    # bitwise reproducible (fp32 atomics in the LoRA and scan gradient kernels; AdamW's first steps move a
+    # weight by ~lr * sign(g), so an element whose gradient is ~0 can move either way), while a lost
+    # optimizer / scheduler / RNG state would put the resumed epoch's update elsewhere entirely.
+    w0 = torch.load(state0, weights_only=True, map_location="cpu")["model"]
     for f in ("checkpoint_epoch_001.pth", "swa.pth", "best.pth"):
-        a = torch.load(cont / "weights" / f, weights_only=True)
-        b = torch.load(res / "weights" / f, weights_only=True)
+        a = torch.load(cont / "weights" / f, weights_only=True, map_location="cpu")
+        b = torch.load(res / "weights" / f, weights_only=True, map_location="cpu")
         assert a.keys() == b.keys()
         for k in a:
             x, y = a[k].double(), b[k].double()
-            rel = float((x - y).norm() / x.norm().clamp_min(1e-12))
-            assert rel < 1e-3, (f, k, rel)
+            moved = float((x - w0[k].double()).norm()) if k in w0 else float(x.norm())
+            d = float((x - y).norm())
+            assert d <= 0.05 * moved + 1e-4 * float(x.norm()) + 1e-12, (f, k, d, moved)
     sa = [float(ln.split()[3]) for ln in (cont / "metrics" / "dev_score.txt").read_text().splitlines()]
     sb = [float(ln.split()[3]) for ln in (res / "metrics" / "dev_score.txt").read_text().splitlines()]
     np.testing.assert_allclose(sb, sa, rtol=1e-3, atol=1e-4)

@@ -204,3 +204,23 @@ def test_train_feeder_order_equals_reference_dataloader(n, B, world):
         got = [list(f.epoch()) for f in feeders]
         for r in range(world):
             assert got[r] == [b[r * B:(r + 1) * B] for b in ref]
+
+
+def test_getitem_gate_order_matches_reference(golden):
+    """Dataset_ASVspoof2019_train.__getitem__ (data_utils.py:163-184) draw order, pinned by
+    getitem_order.json (make_golden.gen_getitem runs the reference's own dataset, RawBoost algo 1):
+    RawBoost gate and draws, codec gates and rate, then pad_random's crop start on the post-codec
+    length — replayed call by call through Augmenter.draw on the same python / numpy seeds."""
+    import random
+    from radhip.train import Augmenter
+    g = golden("getitem_order.json")
+    aug = Augmenter("cpu", algo=g["algo"], rawboost_p=g["rawboost_p"], use_codec=g["use_codec"], codec_p=g["codec_p"])
+    random.seed(g["seed"])
+    np.random.seed(g["seed"])
+    got = []
+    for n, *_ in g["records"]:
+        (rec, sr, start), = aug.draw([n])
+        m = aug.codec_len(n, sr) if sr is not None else n
+        got.append([n, int(rec is not None), sr or 0, start if m > aug.max_len else -1, m])
+    assert got == g["records"]
+    assert 0 < sum(r[1] for r in got) < len(got) and 0 < sum(1 for r in got if r[2]) < len(got)
