@@ -565,6 +565,82 @@ def gen_getitem(ref_src):
     print("wrote getitem_order.json")
 
 
+DIRTY_LENS = [30000, 70000, 64000, 100000, 30000, 50000, 66000, 20000, 30000, 90000, 64601, 45000] * 3
+
+
+def dirty_audio(i):
+    """Utterance i of the dirty-filter fixture as int16 samples (FLAC-encodable, and what sf.read returns
+    divided by 32768). Utterances 0, 4 and 8 (+12k) are identical and shorter than 64 600 samples, so their
+    losses tie exactly and pin the stable order of the sort."""
+    n = DIRTY_LENS[i]
+    tie = i % 12 in (0, 4, 8)
+    rng = np.random.default_rng(0 if tie else 100 + i)
+    off = 0 if tie else 400 * (i % 5 - 2)
+    return np.clip(np.round(3000 * rng.standard_normal(n) + off), -32768, 32767).astype(np.int16)
+
+
+def gen_dirty(ref_src):
+    """src/filter_dirty_data.py run by the reference itself on a toy scorer: models.ToyScore (registered in
+    sys.modules; logits [0, 40 * mean(x) + b]) loaded from a torch.save'd state dict, a 36-utterance train
+    protocol, sf.read stubbed to the int16 / 32768 samples of dirty_audio(i), np.random seeded 77 before
+    main() (the reference does not seed; pad_random crops long utterances with it). Stores the protocol,
+    the per-utterance CE losses in protocol order, and the two output files' bytes."""
+    import importlib
+    import data_utils as DU
+    FD = importlib.import_module("filter_dirty_data")
+
+    class ToyScore(torch.nn.Module):
+        def __init__(self, args, device):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.tensor([40.0, 0.05]))
+
+        def forward(self, x, Freq_aug=False):
+            z = self.w[0] * x.mean(dim=1) + self.w[1]
+            return x[:, :4], torch.stack([torch.zeros_like(z), z], dim=1)
+    mod = types.ModuleType("models.ToyScore")
+    mod.Model = ToyScore
+    sys.modules["models.ToyScore"] = mod
+    keys = [f"LA_T_{9000000 + i:07d}" for i in range(len(DIRTY_LENS))]
+    audio = {k: dirty_audio(i) for i, k in enumerate(keys)}
+    DU.sf.read = lambda path: (audio[os.path.basename(str(path))[:-5]].astype(np.float64) / 32768.0, 16000)
+    FD.tqdm = lambda it: it
+    rows = [f"LA_{i % 7:04d} {k} - {'-' if i % 3 == 0 else 'A0%d' % (1 + i % 6)} {'bonafide' if i % 3 == 0 else 'spoof'}"
+            for i, k in enumerate(keys)]
+    losses = []
+    real_ce = torch.nn.CrossEntropyLoss
+
+    class CE(real_ce):
+        def forward(self, a, b):
+            out = super().forward(a, b)
+            losses.extend(out.detach().float().tolist())
+            return out
+    FD.nn = types.SimpleNamespace(CrossEntropyLoss=CE)
+    with tempfile.TemporaryDirectory() as td:
+        db = os.path.join(td, "LA")
+        os.makedirs(os.path.join(db, "ASVspoof2019_LA_cm_protocols"))
+        with open(os.path.join(db, "ASVspoof2019_LA_cm_protocols", "ASVspoof2019.LA.cm.train.trn.txt"), "w") as f:
+            f.write("\n".join(rows) + "\n")
+        conf = os.path.join(td, "toy.conf")
+        with open(conf, "w") as f:
+            json.dump({"database_path": db, "track": "LA", "model_config": {"architecture": "ToyScore"}}, f)
+        mp = os.path.join(td, "toy.pth")
+        torch.save({"module.w": torch.tensor([40.0, 0.05])}, mp)
+        out = os.path.join(td, "dirty_samples.txt")
+        np.random.seed(77)
+        import contextlib
+        with contextlib.redirect_stdout(io.StringIO()):
+            FD.main(argparse.Namespace(config=conf, model_path=mp, output_path=out, batch_size=5, filter_ratio=0.25,
+                                       device="cpu", allow_cpu=True, amp=False))
+        dirty = open(out).read()
+        clean = open(out.replace(".txt", "_cleaned_protocol.txt")).read()
+    del sys.modules["models.ToyScore"]
+    with open(os.path.join(HERE, "dirty_filter.json"), "w") as f:
+        json.dump({"keys": keys, "protocol": rows, "np_seed": 77, "batch_size": 5, "filter_ratio": 0.25,
+                   "weights": [40.0, 0.05], "losses": losses, "dirty_txt": dirty, "cleaned_protocol_txt": clean}, f,
+                  indent=0)
+    print("wrote dirty_filter.json")
+
+
 def main_():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -609,6 +685,8 @@ def main_():
         gen_legacy(args.ref)
     if want("getitem"):
         gen_getitem(ref_src)
+    if want("dirty"):
+        gen_dirty(ref_src)
 
 
 if __name__ == "__main__":
