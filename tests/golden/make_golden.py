@@ -23,7 +23,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from seeded import seeded_array, seeded_fill_  # noqa: E402
+from seeded import dirty_audio, seeded_array, seeded_fill_  # noqa: E402
 
 
 def install_stubs(ref_src):
@@ -565,20 +565,6 @@ def gen_getitem(ref_src):
     print("wrote getitem_order.json")
 
 
-DIRTY_LENS = [30000, 70000, 64000, 100000, 30000, 50000, 66000, 20000, 30000, 90000, 64601, 45000] * 3
-
-
-def dirty_audio(i):
-    """Utterance i of the dirty-filter fixture as int16 samples (FLAC-encodable, and what sf.read returns
-    divided by 32768). Utterances 0, 4 and 8 (+12k) are identical and shorter than 64 600 samples, so their
-    losses tie exactly and pin the stable order of the sort."""
-    n = DIRTY_LENS[i]
-    tie = i % 12 in (0, 4, 8)
-    rng = np.random.default_rng(0 if tie else 100 + i)
-    off = 0 if tie else 400 * (i % 5 - 2)
-    return np.clip(np.round(3000 * rng.standard_normal(n) + off), -32768, 32767).astype(np.int16)
-
-
 def gen_dirty(ref_src):
     """src/filter_dirty_data.py run by the reference itself on a toy scorer: models.ToyScore (registered in
     sys.modules; logits [0, 40 * mean(x) + b]) loaded from a torch.save'd state dict, a 36-utterance train
@@ -600,7 +586,7 @@ def gen_dirty(ref_src):
     mod = types.ModuleType("models.ToyScore")
     mod.Model = ToyScore
     sys.modules["models.ToyScore"] = mod
-    keys = [f"LA_T_{9000000 + i:07d}" for i in range(len(DIRTY_LENS))]
+    keys = [f"LA_T_{9000000 + i:07d}" for i in range(36)]
     audio = {k: dirty_audio(i) for i, k in enumerate(keys)}
     DU.sf.read = lambda path: (audio[os.path.basename(str(path))[:-5]].astype(np.float64) / 32768.0, 16000)
     FD.tqdm = lambda it: it

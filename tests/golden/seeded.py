@@ -50,3 +50,17 @@ def seeded_fill_(module, seed=1234, skip=()):
 def seeded_array(tag, shape, seed=1234, scale=1.0):
     rng = np.random.default_rng([seed, zlib.crc32(tag.encode())])
     return rng.standard_normal(shape) * scale
+
+
+DIRTY_LENS = [30000, 70000, 64000, 100000, 30000, 50000, 66000, 20000, 30000, 90000, 64601, 45000] * 3
+
+
+def dirty_audio(i):
+    """Utterance i of the dirty-filter fixture as int16 samples (FLAC-encodable, and what sf.read returns
+    divided by 32768). Utterances 0, 4 and 8 (+12k) are identical and shorter than 64 600 samples, so their
+    losses tie exactly and pin the stable order of the sort."""
+    n = DIRTY_LENS[i]
+    tie = i % 12 in (0, 4, 8)
+    rng = np.random.default_rng(0 if tie else 100 + i)
+    off = 0 if tie else 400 * (i % 5 - 2)
+    return np.clip(np.round(3000 * rng.standard_normal(n) + off), -32768, 32767).astype(np.int16)

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from flac_writer import encode
-from make_golden import dirty_audio
+from seeded import dirty_audio
 
 pytestmark = pytest.mark.gpu
 
