@@ -346,6 +346,29 @@ int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
 int rdx_timestamp_acc(int64_t* acc, int sign, void* stream);
 int rdx_wallclock_khz(int device);
 
+/* ------------------------------------------------------------------------------------------
+ * Batched / implicit-GEMM form of rdx_gemm_bf16 (bias epilogue): for z < batch,
+ *   C[z*crow + m, n] = bf16(sum_k A[z*sA + m*lda + k] * B[n*ldb + k] + bias[n])
+ * lda may be smaller than K (overlapping rows): a stride-s convolution over token-major [T, C]
+ * activations is then a GEMM over its input in place (lda = s*C, K = ksize*C), no im2col copy.
+ * ------------------------------------------------------------------------------------------ */
+int rdx_gemm_bf16_strided(const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, void* C, int64_t ldc,
+                          int64_t crow, int batch, int M, int N, int K, const void* bias, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * WavLM frozen CNN feature encoder (HF WavLMFeatureEncoder, feat_extract_norm "layer", conv_dim 512),
+ * replacing the MIOpen conv + transpose + LayerNorm + GELU chain of WavLMFrontend's frozen CNN
+ * (src/models/DualStreamSEMamba.py:392-439). Activations token-major [B, T_l, 512].
+ *   rdx_fe_conv0: layer 0 (C_in 1, ksize 10): out bf16 [B, (len-ksize)/stride+1, 512] =
+ *     gelu(LayerNorm(conv(bf16(x)) + bias)); w [512][ksize] and bias [512] fp32 holding bf16 values.
+ *   rdx_fe_ln_gelu: LayerNorm(512) + GELU of rows [rows, 512] bf16, in place, or into out32 (fp32).
+ * Layers 1-6 are rdx_gemm_bf16_strided over the previous layer's output (lda = stride*512).
+ * ------------------------------------------------------------------------------------------ */
+int rdx_fe_conv0(const float* x, int64_t batch, int64_t len, const float* w, const float* bias, const float* gamma,
+                 const float* beta, float eps, int ksize, int stride, void* out, void* stream);
+int rdx_fe_ln_gelu(void* io, int64_t rows, const float* gamma, const float* beta, float eps, float* out32,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

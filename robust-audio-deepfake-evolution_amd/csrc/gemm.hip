@@ -65,6 +65,8 @@ struct GemmArgs {
   float inv_keep;
   int tiles_n;
   int xcd_panels;              // 1: deal column panels to XCDs
+  int64_t sA;                  // batched (grid.y = batch index z): A advances z * sA elements and the
+  int64_t crow;                //   output (and aux) row index by z * crow rows
 };
 
 template <int EPI>
@@ -84,6 +86,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
     }
   }
   const int m0 = mt * GM, n0 = ntile * GN;
+  const __hip_bfloat16* __restrict__ Ab = g.A + (int64_t)blockIdx.y * g.sA;
+  const int64_t mrow0 = (int64_t)blockIdx.y * g.crow;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
   const int M = g.M, N = g.N, K = g.K;
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
       gbf16x8 z;
 #pragma unroll
       for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
-      ra[j] = (am < M && k < K) ? *reinterpret_cast<const gbf16x8*>(g.A + (int64_t)am * g.lda + k) : z;
+      ra[j] = (am < M && k < K) ? *reinterpret_cast<const gbf16x8*>(Ab + (int64_t)am * g.lda + k) : z;
       rb[j] = (bn < N && k < K) ? *reinterpret_cast<const gbf16x8*>(g.B + (int64_t)bn * g.ldb + k) : z;
     }
   };
@@ -151,6 +155,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
   for (int mi = 0; mi < 2; ++mi) {
     const int m = m0 + wm * 64 + mi * 32 + r;
     if (m >= M) continue;
+    const int64_t mg = mrow0 + m;
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
 #pragma unroll
@@ -168,29 +173,29 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
           v[3] += __uint_as_float(bb.y & 0xffff0000u);
         }
         if (EPI == RDX_EPI_BIAS) {
-          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + (int64_t)m * g.ldc + n) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + mg * g.ldc + n) =
               make_uint2(g_pack2(v[0], v[1]), g_pack2(v[2], v[3]));
         } else if (EPI == RDX_EPI_BIAS_GELU) {
           float u[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) u[e] = g_bf16_round(v[e]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + (int64_t)m * g.ldc + n) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + mg * g.ldc + n) =
               make_uint2(g_pack2(u[0], u[1]), g_pack2(u[2], u[3]));
-          *reinterpret_cast<uint2*>(g.aux_out + (int64_t)m * g.ldao + n) =
+          *reinterpret_cast<uint2*>(g.aux_out + mg * g.ldao + n) =
               make_uint2(g_pack2(g_gelu(u[0]), g_gelu(u[1])), g_pack2(g_gelu(u[2]), g_gelu(u[3])));
         } else if (EPI == RDX_EPI_GELU_BWD) {
           const uint2 uu = *reinterpret_cast<const uint2*>(reinterpret_cast<const __hip_bfloat16*>(g.aux) +
-                                                           (int64_t)m * g.ldaux + n);
+                                                           mg * g.ldaux + n);
           const float u[4] = {__uint_as_float(uu.x << 16), __uint_as_float(uu.x & 0xffff0000u),
                               __uint_as_float(uu.y << 16), __uint_as_float(uu.y & 0xffff0000u)};
           float d[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) d[e] = g_bf16_round(v[e]) * g_gelu_grad(u[e]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + (int64_t)m * g.ldc + n) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + mg * g.ldc + n) =
               make_uint2(g_pack2(d[0], d[1]), g_pack2(d[2], d[3]));
         } else {  // RDX_EPI_RESID_DROP
           const float4 hv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(g.aux) +
-                                                             (int64_t)m * g.ldaux + n);
+                                                             mg * g.ldaux + n);
           const float hx[4] = {hv.x, hv.y, hv.z, hv.w};
           float o[4];
 #pragma unroll
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
             const float ms = g.thr ? (drop_keep(seed, (uint64_t)m * N + n + e, g.thr) ? g.inv_keep : 0.f) : 1.f;
             o[e] = hx[e] + fo * ms;
           }
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + (int64_t)m * g.ldc + n) =
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + mg * g.ldc + n) =
               make_float4(o[0], o[1], o[2], o[3]);
         }
       }
@@ -208,9 +213,10 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
 }
 
 template <int EPI>
-static int gemm_launch(const GemmArgs& g, hipStream_t st) {
+static int gemm_launch(const GemmArgs& g, hipStream_t st, int batch = 1) {
   const int tm = (g.M + GM - 1) / GM;
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI>), dim3((unsigned)(tm * g.tiles_n)), dim3(G_THREADS), 4 * G_TILE, st, g);
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI>), dim3((unsigned)(tm * g.tiles_n), (unsigned)batch), dim3(G_THREADS),
+                     4 * G_TILE, st, g);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -256,6 +262,8 @@ extern "C" int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t 
   g.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   g.tiles_n = (N + GN - 1) / GN;
   g.xcd_panels = (g.tiles_n % 8 == 0) ? 1 : 0;
+  g.sA = 0;
+  g.crow = 0;
   const int64_t tiles = (int64_t)((M + GM - 1) / GM) * g.tiles_n;
   RDX_REQUIRE(tiles <= 0x7fffffff);
   hipStream_t st = as_stream(stream);
@@ -265,4 +273,43 @@ extern "C" int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t 
     case RDX_EPI_GELU_BWD: return gemm_launch<RDX_EPI_GELU_BWD>(g, st);
     default: return gemm_launch<RDX_EPI_RESID_DROP>(g, st);
   }
+}
+
+// Batched / implicit-GEMM form, bias epilogue only: for z < batch, C[z*crow + m, :] = bf16(A_z[m, :] . B^T + bias)
+// with A_z = A + z*sA, row m at A_z + m*lda. lda may be SMALLER than K: rows then overlap, which is how a
+// strided convolution over token-major activations reads its im2col matrix in place (featconv.hip).
+extern "C" int rdx_gemm_bf16_strided(const void* A, int64_t lda, int64_t sA, const void* B, int64_t ldb, void* C,
+                                     int64_t ldc, int64_t crow, int batch, int M, int N, int K, const void* bias,
+                                     void* stream) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  RDX_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && batch <= 65535 && al(A) && al(B) && al(C));
+  RDX_REQUIRE(lda > 0 && lda % 8 == 0 && sA >= 0 && sA % 8 == 0 && ldb % 8 == 0 && ldb >= K && K % 8 == 0);
+  RDX_REQUIRE(N % 4 == 0 && ldc >= N && ldc % 4 == 0 && crow >= 0 && (batch == 1 || crow >= M));
+  RDX_REQUIRE(!bias || ((uintptr_t)bias & 7) == 0);
+  GemmArgs g;
+  g.A = (const __hip_bfloat16*)A;
+  g.lda = lda;
+  g.B = (const __hip_bfloat16*)B;
+  g.ldb = ldb;
+  g.C = C;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.bias = (const __hip_bfloat16*)bias;
+  g.aux = nullptr;
+  g.ldaux = 0;
+  g.aux_out = nullptr;
+  g.ldao = 0;
+  g.seed_dev = nullptr;
+  g.salt = 0;
+  g.thr = 0;
+  g.inv_keep = 1.f;
+  g.tiles_n = (N + GN - 1) / GN;
+  g.xcd_panels = (g.tiles_n % 8 == 0) ? 1 : 0;
+  g.sA = sA;
+  g.crow = crow;
+  const int64_t tiles = (int64_t)((M + GM - 1) / GM) * g.tiles_n;
+  RDX_REQUIRE(tiles <= 0x7fffffff);
+  return gemm_launch<RDX_EPI_BIAS>(g, as_stream(stream), batch);
 }

@@ -748,3 +748,56 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
                                   _p(seed) if seed is not None else None, int(salt), float(p_drop), _stream(a)),
               "gemm_bf16")
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
+
+
+# ------------------------------------------------------------------- WavLM CNN feature encoder ----
+def fe_conv_weights(layers):
+    """Per-layer device operands of the fused frozen CNN (csrc/featconv.hip) from the ConvLayer modules:
+    layer 0 (w fp32 [512, 10] and bias fp32, both bf16-rounded as autocast feeds them), layers >= 1 the
+    weight permuted to [C_out][k][C_in] = [512, K*512] bf16 and the bf16 bias; LayerNorm gamma/beta fp32."""
+    out = []
+    with torch.no_grad():
+        for i, ly in enumerate(layers):
+            c = ly.conv
+            w = c.weight.detach()
+            b = c.bias.detach().to(torch.bfloat16) if c.bias is not None else None   # wavlm-large: conv_bias False
+            if i == 0:
+                wk = w.reshape(w.shape[0], -1).to(torch.bfloat16).float().contiguous()
+                bk = b.float().contiguous() if b is not None else torch.zeros(w.shape[0], device=w.device)
+            else:
+                wk = w.permute(0, 2, 1).reshape(w.shape[0], -1).to(torch.bfloat16).contiguous()
+                bk = b.contiguous() if b is not None else None
+            out.append((wk, bk, ly.layer_norm.weight.detach().float().contiguous(),
+                        ly.layer_norm.bias.detach().float().contiguous(), float(ly.layer_norm.eps),
+                        c.kernel_size[0], c.stride[0]))
+    return out
+
+
+def feature_encoder_fused(x, ops_):
+    """Frozen WavLM CNN, x [B, L] fp32 -> [B, T, 512] fp32 token-major (HF WavLMFeatureEncoder, "layer" norm):
+    conv0+LN+GELU in one kernel, then per layer the implicit GEMM (rdx_gemm_bf16_strided, rows of the
+    token-major input overlapping at stride*512) and the LN+GELU pass; the last LN+GELU writes fp32."""
+    _require_gpu(x)
+    if len(ops_) < 2:
+        raise ValueError("fused feature encoder: needs at least two conv layers")
+    x = x.contiguous().float()
+    B, L = x.shape
+    w0, b0, g0, be0, eps0, k0, s0 = ops_[0]
+    T = (L - k0) // s0 + 1
+    h = torch.empty(B, T, 512, device=x.device, dtype=torch.bfloat16)
+    with _timed("fe_conv0", x, 2.0 * B * T * 512 * k0):
+        check(lib().rdx_fe_conv0(_p(x), B, L, _p(w0), _p(b0), _p(g0), _p(be0), eps0, k0, s0, _p(h), _stream(x)),
+              "fe_conv0")
+    for i, (w, b, g, be, eps, k, s) in enumerate(ops_[1:], start=1):
+        To = (T - k) // s + 1
+        y = torch.empty(B, To, 512, device=x.device, dtype=torch.bfloat16)
+        with _timed("fe_conv_gemm", x, gemm_flops(B * To, 512, k * 512)):
+            check(lib().rdx_gemm_bf16_strided(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To, B, To, 512,
+                                              k * 512, _p(b) if b is not None else None, _stream(x)), "gemm_bf16_strided")
+        last = i == len(ops_) - 1
+        out32 = torch.empty(B, To, 512, device=x.device, dtype=torch.float32) if last else None
+        with _timed("fe_ln_gelu", x, 0.0):
+            check(lib().rdx_fe_ln_gelu(_p(y), B * To, _p(g), _p(be), eps, _p(out32) if last else None, _stream(x)),
+                  "fe_ln_gelu")
+        h, T = (out32 if last else y), To
+    return h

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import wavlm_fused
-from .ops import GatedAttention, PosConv, posconv_weights
+from .ops import GatedAttention, PosConv, fe_conv_weights, feature_encoder_fused, posconv_weights
 
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
 # restated, not verifiable offline: parity unpinned for those regularisers)
@@ -172,8 +172,28 @@ class FeatureEncoder(nn.Module):
     def __init__(self, cfg):
         super().__init__()
         self.conv_layers = nn.ModuleList([ConvLayer(cfg, i) for i in range(len(cfg.conv_dim))])
+        self.cfg = cfg
+
+    def _fused_ok(self, x):
+        """bf16 CUDA pass with the WavLM-Large CNN geometry and frozen weights -> csrc/featconv.hip (token-major
+        conv0+LN+GELU kernel, implicit-GEMM convs, LN+GELU passes) instead of MIOpen convs plus transposes,
+        casts and separate LayerNorm/GELU launches."""
+        c = self.cfg
+        return (x.is_cuda and x.dim() == 2 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and len(c.conv_dim) >= 2
+                and all(d == 512 for d in c.conv_dim) and c.conv_kernel[0] == 10
+                and c.feat_extract_norm == "layer" and c.feat_extract_activation == "gelu"
+                and all(k * 512 % 8 == 0 for k in c.conv_kernel)
+                and os.environ.get("RADHIP_FUSED_FE", "1") != "0"
+                and not any(p.requires_grad for p in self.parameters()))
 
     def forward(self, x):
+        if self._fused_ok(x):
+            key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+            if getattr(self, "_fe_key", None) != key:
+                self._fe_ops = fe_conv_weights(self.conv_layers)
+                self._fe_key = key
+            return feature_encoder_fused(x, self._fe_ops).transpose(1, 2)     # [B, 512, T] view, as the modules
         x = x[:, None]
         for layer in self.conv_layers:
             x = layer(x)
