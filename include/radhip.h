@@ -369,6 +369,25 @@ int rdx_fe_conv0(const float* x, int64_t batch, int64_t len, const float* w, con
 int rdx_fe_ln_gelu(void* io, int64_t rows, const float* gamma, const float* beta, float eps, float* out32,
                    void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * SincNet residual-stack convolutions (Residual_block conv1 2x3 pad (1,1), conv2 2x3 pad (0,1),
+ * conv_downsample 1x3 pad (0,1); src/models/DualStreamSEMamba.py:144-200), NHWC bf16, C_in, C_out in
+ * {32, 64}, kh in {1, 2}, stride 1, column padding 1, row padding ph; replaces MIOpen's solvers.
+ *   rdx_sconv_fwd:   y [N, H+2ph-kh+1, W, co] = conv(x [N, H, W, ci], w), w tap-major [kh*3][co][ci] bf16.
+ *                    With y2 and bn = [conv bias | running mean | invstd*gamma | beta] (4 x co fp32) also
+ *                    y2 = bf16(selu(((bf16(y) + cb) - mean) * invstd*gamma + beta)).
+ *                    The input gradient is this call on dY with the flipped kernel [kh*3][ci][co] and
+ *                    row padding kh-1-ph.
+ *   rdx_sconv_wgrad: dw [kh*3][co][ci] fp32 from x and dy; part: rdx_sconv_wgrad_nblk(N, Ho, W) rows of
+ *                    kh*3*co*ci fp32 scratch (per-workgroup partials and the two-stage reduction's
+ *                    slices, summed in a fixed order: deterministic).
+ * ------------------------------------------------------------------------------------------ */
+int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, const float* bn, int N, int H, int W, int ci,
+                  int co, int kh, int ph, void* stream);
+int rdx_sconv_wgrad_nblk(int N, int Ho, int W);
+int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* part, int N, int H, int W, int ci, int co,
+                    int kh, int ph, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,434 @@
+// SincNet residual-stack convolutions on gfx950 MFMA: NHWC bf16, kernel (KH x 3) with KH in {1, 2}, stride 1,
+// padding (ph, 1), C_in and C_out in {32, 64} — conv1 (2x3, pad (1,1)), conv2 (2x3, pad (0,1)) and
+// conv_downsample (1x3, pad (0,1)) of Residual_block (src/models/DualStreamSEMamba.py:144-200) in blocks 1-5 and
+// conv2 of block 0, forward, input gradient and weight gradient. They replace MIOpen's implicit-GEMM solvers
+// and the layout transposes / zero-fills around them.
+//
+// Forward (also the input gradient: dX is the same convolution of dY with the kernel flipped in both axes,
+// C_in/C_out exchanged and the row padding KH-1-ph):
+//   Y[n, ho, w, co] = sum_{kh, kw, ci} X[n, ho + kh - ph, w + kw - 1, ci] * Wt[co, ci, kh, kw]
+// A 256-thread workgroup owns a strip of 128 positions of one utterance and walks its output rows top-down:
+// the weights [tap][co][ci] are staged in LDS once, each input row (130 positions with the two halo columns,
+// zero outside the image) is read from HBM once into a ring of KH + 1 LDS row slots (16-byte chunks
+// XOR-swizzled by position / output channel), prefetched a row ahead; each wave owns 32 positions and runs
+// KH*3*C_in/16 mfma_f32_32x32x16_bf16 steps per 32 output channels, computing Y^T (weights as the row
+// operand), so a lane holds one position and groups of 4 consecutive channels: 8-byte stores.
+// Epilogue options: bf16 output (no bias: the conv biases are folded into the next fused pass, as
+// radhip.ops.BnSelu / ResTail expect), or additionally the frozen-BN + SELU activation of that output (the
+// conv1 -> bn2 -> selu chain), so conv2's input is produced without another pass over HBM.
+//
+// Weight gradient: dW[co, ci, kh, kw] = sum_{n, ho, w} dY[n, ho, w, co] * X[n, ho + kh - ph, w + kw - 1, ci].
+// A workgroup walks units of (output row, 128-position strip) in a grid-stride loop, stages the dY strip and
+// the KH input rows (130 positions) row-major in LDS, and accumulates (tap, co-tile, ci-tile) 32x32 MFMA tiles
+// with K = positions in registers (4 waves split the tiles); both operands are read down their columns with
+// ds_read_b64_tr_b16 (the tap's column shift is a row offset into the input image). One fp32 partial per
+// workgroup, summed by a second kernel in a fixed order (deterministic, no atomics).
+#include "common.h"
+
+namespace rdx {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 sbf16x8;
+typedef __attribute__((ext_vector_type(16))) float sf32x16;
+
+constexpr int SC_T = 256;        // threads
+constexpr int SC_P = 128;        // output positions per strip
+constexpr int SC_PW = SC_P + 2;  // staged input positions (halo 1 each side)
+
+__device__ __forceinline__ sf32x16 sc_mfma(sbf16x8 a, sbf16x8 b, sf32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ uint32_t sc_pack2(float a, float b) {
+  __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
+}
+__device__ __forceinline__ float sc_bf16(float x) { return __bfloat162float(__float2bfloat16(x)); }
+__device__ __forceinline__ float sc_selu(float u) {  // as sincnet.hip selu_f
+  return 1.0507009873554805f * (u > 0.f ? u : 1.6732632423543772f * expm1f(u));
+}
+
+// LDS byte offset of the 16-byte chunk `ch` (8 channels) of row `row` in a [rows][C] bf16 image; chunks are
+// XOR-swizzled by the row so 32 lanes reading the same chunk of 32 consecutive rows spread over the banks.
+template <int C>
+__device__ __forceinline__ int sc_off(int row, int ch) {
+  constexpr int NCH = C / 8;
+  return row * (C * 2) + 16 * (ch ^ (row & (NCH - 1)));
+}
+
+struct SConvArgs {
+  const __hip_bfloat16* x;  // [N, H, W, CI]
+  const __hip_bfloat16* w;  // [KH*3][CO][CI] (tap-major, prepared on the host)
+  __hip_bfloat16* y;        // [N, Ho, W, CO]
+  __hip_bfloat16* y2;       // optional: selu(bn(y + cb)) [N, Ho, W, CO]
+  const float* bn;          // [4][CO]: conv bias cb, running mean, invstd * gamma, beta (frozen BN)
+  int N, H, W, Ho, ph;
+  int rows_per;             // output rows per workgroup (grid.z chunks of the Ho rows)
+};
+
+// Input rows cycle through KH + 1 LDS slots: input row (ho - ph + kh) of output row ho lives in slot
+// (ho + kh) % (KH + 1), and the row the next output row adds is loaded into registers while the current
+// row's MFMAs run, then written to the slot the current row no longer needs (one barrier per row).
+template <int CI>
+__device__ __forceinline__ void sc_load_row(uint4* regs, const __hip_bfloat16* x, int n, int hi, int H, int W, int p0) {
+  constexpr int XCH = CI / 8, NV = (SC_PW * XCH + SC_T - 1) / SC_T;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i = threadIdx.x + SC_T * j;
+    const int ch = i % XCH, pp = i / XCH, wi = p0 - 1 + pp;
+    regs[j] = make_uint4(0, 0, 0, 0);
+    if (pp < SC_PW && hi >= 0 && hi < H && wi >= 0 && wi < W)
+      regs[j] = *reinterpret_cast<const uint4*>(x + (((int64_t)n * H + hi) * W + wi) * CI + ch * 8);
+  }
+}
+template <int CI>
+__device__ __forceinline__ void sc_store_row(char* slot, const uint4* regs) {
+  constexpr int XCH = CI / 8, NV = (SC_PW * XCH + SC_T - 1) / SC_T;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i = threadIdx.x + SC_T * j;
+    if (i < SC_PW * XCH) *reinterpret_cast<uint4*>(slot + sc_off<CI>(i / XCH, i % XCH)) = regs[j];
+  }
+}
+
+template <int CI, int CO, int KH>
+__global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char sc_lds[];
+  constexpr int NSLOT = KH + 1, SLOT = SC_PW * CI * 2, XCH = CI / 8;
+  constexpr int NV = (SC_PW * XCH + SC_T - 1) / SC_T;
+  char* ws = sc_lds;                          // [KH*3*CO][CI]
+  char* xs = sc_lds + KH * 3 * CO * CI * 2;   // NSLOT x [SC_PW][CI]
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int n = blockIdx.y, p0 = blockIdx.x * SC_P;
+  const int ho0 = blockIdx.z * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
+  for (int i = tid; i < KH * 3 * CO * XCH; i += SC_T) {
+    const int ch = i % XCH, rowc = i / XCH;  // rowc = tap * CO + co
+    *reinterpret_cast<uint4*>(ws + sc_off<CI>(rowc, ch)) = *reinterpret_cast<const uint4*>(a.w + (int64_t)rowc * CI + ch * 8);
+  }
+  uint4 pre[NV];
+#pragma unroll
+  for (int kh = 0; kh < KH; ++kh) {
+    sc_load_row<CI>(pre, a.x, n, ho0 + kh - a.ph, a.H, a.W, p0);
+    sc_store_row<CI>(xs + ((ho0 + kh) % NSLOT) * SLOT, pre);
+  }
+  __syncthreads();
+  constexpr int NT = CO / 32;
+  const int pw = wv * 32 + r;  // this lane's position within the strip (B operand row)
+  const int p = p0 + pw;
+  for (int ho = ho0; ho < ho1; ++ho) {
+    const bool more = ho + 1 < ho1;
+    if (more) sc_load_row<CI>(pre, a.x, n, ho - a.ph + KH, a.H, a.W, p0);
+    sf32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      const char* xk = xs + ((ho + kh) % NSLOT) * SLOT;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int s = 0; s < CI / 16; ++s) {
+          const sbf16x8 xf = *reinterpret_cast<const sbf16x8*>(xk + sc_off<CI>(pw + kw, 2 * s + h));
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int rowc = (kh * 3 + kw) * CO + t * 32 + r;
+            const sbf16x8 wf = *reinterpret_cast<const sbf16x8*>(ws + sc_off<CI>(rowc, 2 * s + h));
+            acc[t] = sc_mfma(wf, xf, acc[t]);  // Y^T tile: rows co, columns positions
+          }
+        }
+    }
+    // epilogue: lane owns position p, channels co = t*32 + 8g + 4h + e
+    if (p < a.W) {
+      const int64_t obase = (((int64_t)n * a.Ho + ho) * a.W + p) * CO;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = t * 32 + 8 * g + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
+          *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]));
+          if (a.y2) {
+            float u[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // the arithmetic of bnselu_fwd_kernel on the bf16 conv output
+              const int c = co + e;
+              u[e] = sc_selu(fmaf((sc_bf16(v[e]) + a.bn[c]) - a.bn[CO + c], a.bn[2 * CO + c], a.bn[3 * CO + c]));
+            }
+            *reinterpret_cast<uint2*>(a.y2 + obase + co) = make_uint2(sc_pack2(u[0], u[1]), sc_pack2(u[2], u[3]));
+          }
+        }
+    }
+    if (more) sc_store_row<CI>(xs + ((ho + KH) % NSLOT) * SLOT, pre);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------- weight gradient ------
+struct SWgradArgs {
+  const __hip_bfloat16* x;   // [N, H, W, CI]
+  const __hip_bfloat16* dy;  // [N, Ho, W, CO]
+  float* part;               // [gridDim.x][KH*3][CO][CI]
+  int N, H, W, Ho, ph;
+  int64_t units;             // N * strips * nz
+  int strips, nz, rows_per;  // 128-position strips, row chunks, rows per chunk
+};
+
+typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 sbf16x4v;
+typedef __attribute__((address_space(3))) sbf16x4v lds_sbf16x4v;
+
+// Row-major [pos][C] image in LDS as 8-row x 32-channel subtiles of 512 B, the 16-byte chunk XOR-swizzled by
+// (row >> 2) & 3: conflict-free for the hardware-transposed ds_read_b64_tr_b16 reads below.
+template <int C>
+__device__ __forceinline__ int sc_img(int row, int ch) {
+  return (C * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+// MFMA operand running down a column (K = positions): element j = IMG[r0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)]
+// [c0 + (lane & 31)], two ds_read_b64_tr_b16. Both operands of the weight-gradient MFMA use this same
+// permuted position order, so the reduction over positions is unaffected.
+template <int C>
+__device__ __forceinline__ sbf16x8 sc_read_tr(const char* img, int r0, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = r0 + 16 * s + 4 * (g >> 1) + (i >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const int sub = 2 * (col & 7);
+  const sbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_sbf16x4v*)(img + sc_img<C>(row, col >> 3) + sub));
+  const sbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_sbf16x4v*)(img + sc_img<C>(row + 8, col >> 3) + sub));
+  sbf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = lo[j];
+    r[4 + j] = hi[j];
+  }
+  return r;
+}
+
+constexpr int SC_XR = 136;  // staged input rows per kernel row: 130 used, padded to whole 8-row subtiles
+
+// A unit is (utterance, strip, chunk of output rows); the unit walks its rows top-down. Input rows cycle
+// through KH + 1 image slots (row (ho - ph + kh) in slot (ho + kh) % (KH + 1)) and dY rows through two, so
+// each input row is read from HBM once per unit and one barrier per row separates the writes of row ho from
+// the MFMA reads of row ho - 1 (they never touch the same slot).
+template <int CI, int CO, int KH>
+__global__ __launch_bounds__(SC_T) void sconv_wgrad_kernel(SWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char sc_lds[];
+  constexpr int NSLOT = KH + 1, XSLOT = SC_XR * CI * 2, DSLOT = SC_P * CO * 2;
+  char* dyi = sc_lds;                       // 2 x [SC_P][CO]
+  char* xi = sc_lds + 2 * DSLOT;            // NSLOT x [SC_XR][CI]
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  constexpr int NTAP = KH * 3, TCO = CO / 32, TCI = CI / 32;
+  constexpr int NTILE = NTAP * TCO * TCI;
+  constexpr int PER = (NTILE + 3) / 4;  // tiles per wave
+  sf32x16 acc[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+  auto stage_x = [&](int n, int hi, int p0, char* slot) {
+    for (int i = tid; i < SC_XR * (CI / 8); i += SC_T) {
+      const int ch = i % (CI / 8), pp = i / (CI / 8), wi = p0 - 1 + pp;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (pp < SC_PW && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
+        v = *reinterpret_cast<const uint4*>(a.x + (((int64_t)n * a.H + hi) * a.W + wi) * CI + ch * 8);
+      *reinterpret_cast<uint4*>(slot + sc_img<CI>(pp, ch)) = v;
+    }
+  };
+  for (int64_t u = blockIdx.x; u < a.units; u += gridDim.x) {
+    const int zc = (int)(u % a.nz);
+    const int64_t us = u / a.nz;
+    const int strip = (int)(us % a.strips), n = (int)(us / a.strips);
+    const int p0 = strip * SC_P;
+    const int ho0 = zc * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
+    __syncthreads();  // the previous unit's reads are done
+    for (int kh = 0; kh + 1 < KH; ++kh) stage_x(n, ho0 + kh - a.ph, p0, xi + ((ho0 + kh) % NSLOT) * XSLOT);
+    for (int ho = ho0; ho < ho1; ++ho) {
+      stage_x(n, ho - a.ph + KH - 1, p0, xi + ((ho + KH - 1) % NSLOT) * XSLOT);
+      char* dys = dyi + (ho & 1) * DSLOT;
+      for (int i = tid; i < SC_P * (CO / 8); i += SC_T) {
+        const int ch = i % (CO / 8), pp = i / (CO / 8), wi = p0 + pp;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (wi < a.W) v = *reinterpret_cast<const uint4*>(a.dy + (((int64_t)n * a.Ho + ho) * a.W + wi) * CO + ch * 8);
+        *reinterpret_cast<uint4*>(dys + sc_img<CO>(pp, ch)) = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int tile = wv + 4 * j;
+        if (tile >= NTILE) break;
+        const int tap = tile / (TCO * TCI), tco = (tile / TCI) % TCO, tci = tile % TCI;
+        const int kh = tap / 3, kw = tap % 3;
+        const char* xk = xi + ((ho + kh) % NSLOT) * XSLOT;
+#pragma unroll
+        for (int s = 0; s < SC_P / 16; ++s) {
+          // output position pl pairs with staged input row pl + kw (input column p0 + pl + kw - 1)
+          acc[j] = sc_mfma(sc_read_tr<CO>(dys, 0, tco * 32, s, lane), sc_read_tr<CI>(xk, kw, tci * 32, s, lane),
+                           acc[j]);
+        }
+      }
+    }
+  }
+  // partial: lane owns ci column (lane & 31) of its tile, co rows (i & 3) + 8 (i >> 2) + 4 h
+  const int r = lane & 31, h = lane >> 5;
+  float* out = a.part + (int64_t)blockIdx.x * NTAP * CO * CI;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int tile = wv + 4 * j;
+    if (tile >= NTILE) break;
+    const int tap = tile / (TCO * TCI), tco = (tile / TCI) % TCO, tci = tile % TCI;
+    const int ci = tci * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int co = tco * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      out[((int64_t)tap * CO + co) * CI + ci] = acc[j][i];
+    }
+  }
+}
+
+// Fixed-order reduction of the per-workgroup partials [nblk][n]: stage 1 sums slice z of SC_RS slices of the
+// partial rows (8 independent loads in flight per thread) into part2 [SC_RS][n]; stage 2 sums the slices.
+constexpr int SC_RS = 16;
+__global__ void sconv_wgrad_reduce1_kernel(const float* __restrict__ part, int nblk, int64_t n, float* __restrict__ part2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int per = (nblk + SC_RS - 1) / SC_RS, b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int b = b0;
+  for (; b + 8 <= b1; b += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += part[(int64_t)(b + k) * n + i];
+  }
+  for (; b < b1; ++b) s[0] += part[(int64_t)b * n + i];
+  part2[(int64_t)blockIdx.y * n + i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+__global__ void sconv_wgrad_reduce2_kernel(const float* __restrict__ part2, int64_t n, float* __restrict__ dw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+#pragma unroll
+  for (int z = 0; z < SC_RS; ++z) s += part2[(int64_t)z * n + i];
+  dw[i] = s;
+}
+
+template <int CI, int CO, int KH>
+static int sconv_fwd_launch(const SConvArgs& a, hipStream_t st) {
+  const size_t smem = (size_t)(KH + 1) * SC_PW * CI * 2 + (size_t)KH * 3 * CO * CI * 2;
+  const int strips = (a.W + SC_P - 1) / SC_P;
+  // about 1024 workgroups for 256 CUs: split the rows when strips x N alone is small (each split restages
+  // the weights and KH - 1 halo rows)
+  const int want = (int)((1024 + (int64_t)strips * a.N - 1) / ((int64_t)strips * a.N));
+  const int nz = want < 1 ? 1 : (want > a.Ho ? a.Ho : want);
+  SConvArgs b = a;
+  b.rows_per = (a.Ho + nz - 1) / nz;
+  dim3 grid((unsigned)strips, (unsigned)a.N, (unsigned)((a.Ho + b.rows_per - 1) / b.rows_per));
+  hipLaunchKernelGGL((sconv_fwd_kernel<CI, CO, KH>), grid, dim3(SC_T), smem, st, b);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+template <int CI, int CO, int KH>
+static int sconv_wgrad_launch(const SWgradArgs& a, int nblk, hipStream_t st) {
+  const size_t smem = (2 * (size_t)SC_P * CO + (size_t)(KH + 1) * SC_XR * CI) * 2;
+  hipLaunchKernelGGL((sconv_wgrad_kernel<CI, CO, KH>), dim3((unsigned)nblk), dim3(SC_T), smem, st, a);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+}  // namespace rdx
+
+using namespace rdx;
+
+#define SC_DISPATCH(FN, ...)                                                                   \
+  if (ci == 32 && co == 32 && kh == 2) return FN<32, 32, 2>(__VA_ARGS__);                      \
+  if (ci == 32 && co == 64 && kh == 2) return FN<32, 64, 2>(__VA_ARGS__);                      \
+  if (ci == 64 && co == 32 && kh == 2) return FN<64, 32, 2>(__VA_ARGS__);                      \
+  if (ci == 64 && co == 64 && kh == 2) return FN<64, 64, 2>(__VA_ARGS__);                      \
+  if (ci == 32 && co == 64 && kh == 1) return FN<32, 64, 1>(__VA_ARGS__);                      \
+  if (ci == 64 && co == 32 && kh == 1) return FN<64, 32, 1>(__VA_ARGS__);                      \
+  if (ci == 32 && co == 32 && kh == 1) return FN<32, 32, 1>(__VA_ARGS__);                      \
+  if (ci == 64 && co == 64 && kh == 1) return FN<64, 64, 1>(__VA_ARGS__);                      \
+  return RDX_EUNSUPPORTED;
+
+// y[N, Ho, W, co] = conv(x[N, H, W, ci], w) with Ho = H + 2*ph - kh + 1; w is tap-major [kh*3][co][ci] bf16.
+// With y2 (and bn = [cb | mean | invstd*gamma | beta], 4 x co fp32) also
+//   y2 = bf16(selu(((bf16(y) + cb) - mean) * invstd*gamma + beta)), exactly radhip.ops.BnSelu's forward.
+extern "C" int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, const float* bn, int N, int H, int W,
+                             int ci, int co, int kh, int ph, void* stream) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  RDX_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && (kh == 1 || kh == 2) && ph >= 0 && ph <= kh);
+  RDX_REQUIRE(al(x) && al(w) && al(y) && (!y2 || (al(y2) && bn)));
+  SConvArgs a;
+  a.x = (const __hip_bfloat16*)x;
+  a.w = (const __hip_bfloat16*)w;
+  a.y = (__hip_bfloat16*)y;
+  a.y2 = (__hip_bfloat16*)y2;
+  a.bn = bn;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.ph = ph;
+  a.Ho = H + 2 * ph - kh + 1;
+  RDX_REQUIRE(a.Ho > 0 && N <= 65535);
+  hipStream_t st = as_stream(stream);
+  SC_DISPATCH(sconv_fwd_launch, a, st)
+}
+
+// row chunks of the weight-gradient units: about 4 rows each, at least 2048 units where the shape allows
+static int sc_wgrad_nz(int N, int Ho, int W) {
+  const int64_t su = (int64_t)N * ((W + SC_P - 1) / SC_P);
+  int nz = (int)((2048 + su - 1) / su);
+  if (nz < (Ho + 3) / 4) nz = (Ho + 3) / 4;
+  return nz > Ho ? Ho : nz;
+}
+
+static int sc_wgrad_blocks(int N, int Ho, int W) {
+  const int nz = sc_wgrad_nz(N, Ho, W);
+  const int64_t units = (int64_t)N * ((W + SC_P - 1) / SC_P) * nz;
+  return (int)(units < 1024 ? units : 1024);
+}
+
+// rows of kh*3*co*ci fp32 the weight-gradient scratch needs: one partial per workgroup + the reduction slices
+extern "C" int rdx_sconv_wgrad_nblk(int N, int Ho, int W) { return sc_wgrad_blocks(N, Ho, W) + SC_RS; }
+
+// dw [kh*3][co][ci] fp32 = sum over positions of dy (x) shifted x; part: [nblk][kh*3*co*ci] fp32 scratch,
+// nblk = rdx_sconv_wgrad_nblk(N, Ho, W).
+extern "C" int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* part, int N, int H, int W, int ci,
+                               int co, int kh, int ph, void* stream) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  RDX_REQUIRE(x && dy && dw && part && N > 0 && H > 0 && W > 0 && (kh == 1 || kh == 2) && ph >= 0 && ph <= kh);
+  RDX_REQUIRE(al(x) && al(dy));
+  SWgradArgs a;
+  a.x = (const __hip_bfloat16*)x;
+  a.dy = (const __hip_bfloat16*)dy;
+  a.part = part;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.ph = ph;
+  a.Ho = H + 2 * ph - kh + 1;
+  RDX_REQUIRE(a.Ho > 0);
+  a.strips = (W + SC_P - 1) / SC_P;
+  a.nz = sc_wgrad_nz(N, a.Ho, W);
+  a.rows_per = (a.Ho + a.nz - 1) / a.nz;
+  a.nz = (a.Ho + a.rows_per - 1) / a.rows_per;
+  a.units = (int64_t)N * a.strips * a.nz;
+  const int nblk = sc_wgrad_blocks(N, a.Ho, W);
+  hipStream_t st = as_stream(stream);
+  int rc = RDX_EUNSUPPORTED;
+  if (ci == 32 && co == 32 && kh == 2) rc = sconv_wgrad_launch<32, 32, 2>(a, nblk, st);
+  else if (ci == 32 && co == 64 && kh == 2) rc = sconv_wgrad_launch<32, 64, 2>(a, nblk, st);
+  else if (ci == 64 && co == 32 && kh == 2) rc = sconv_wgrad_launch<64, 32, 2>(a, nblk, st);
+  else if (ci == 64 && co == 64 && kh == 2) rc = sconv_wgrad_launch<64, 64, 2>(a, nblk, st);
+  else if (ci == 32 && co == 64 && kh == 1) rc = sconv_wgrad_launch<32, 64, 1>(a, nblk, st);
+  else if (ci == 64 && co == 32 && kh == 1) rc = sconv_wgrad_launch<64, 32, 1>(a, nblk, st);
+  else if (ci == 32 && co == 32 && kh == 1) rc = sconv_wgrad_launch<32, 32, 1>(a, nblk, st);
+  else if (ci == 64 && co == 64 && kh == 1) rc = sconv_wgrad_launch<64, 64, 1>(a, nblk, st);
+  if (rc != RDX_OK) return rc;
+  const int64_t n = (int64_t)kh * 3 * co * ci;
+  float* part2 = part + (int64_t)nblk * n;  // SC_RS more rows of the scratch
+  hipLaunchKernelGGL(sconv_wgrad_reduce1_kernel, dim3((unsigned)((n + 255) / 256), SC_RS), dim3(256), 0, st, part, nblk,
+                     n, part2);
+  hipLaunchKernelGGL(sconv_wgrad_reduce2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part2, n, dw);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}

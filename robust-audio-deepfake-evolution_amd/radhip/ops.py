@@ -550,6 +550,109 @@ class Block0Convs(torch.autograd.Function):
         return dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape)
 
 
+# ------------------------------------------------------------- SincNet residual convolutions ----
+SCONV_CH = (32, 64)
+
+
+def sconv_ok(x, weight):
+    """The shapes csrc/sconv.hip covers: bf16-autocast NHWC input, C_in and C_out in {32, 64}, kernel (1|2) x 3."""
+    co, ci, kh, kw = weight.shape
+    return (x.is_cuda and x.dim() == 4 and x.shape[1] == ci and ci in SCONV_CH and co in SCONV_CH and kh in (1, 2)
+            and kw == 3 and os.environ.get("RADHIP_SCONV", "1") != "0")
+
+
+def _sconv_w(weight):
+    """[C_out, C_in, KH, 3] -> tap-major [KH*3][C_out][C_in] bf16 (forward) and the flipped, transposed
+    [KH*3][C_in][C_out] bf16 (input gradient = the same convolution of dY)."""
+    co, ci, kh, kw = weight.shape
+    wb = weight.detach().to(torch.bfloat16)
+    wf = wb.permute(2, 3, 0, 1).reshape(kh * kw, co, ci).contiguous()
+    wd = wb.flip(2, 3).permute(2, 3, 1, 0).reshape(kh * kw, ci, co).contiguous()
+    return wf, wd
+
+
+def _sconv_run(x, w_tap, ci, co, kh, ph, y2=None, bn=None):
+    N, _, H, W = x.shape
+    Ho = H + 2 * ph - kh + 1
+    y = torch.empty(N, co, Ho, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+    with _timed("sconv_fwd", x, 2.0 * N * Ho * W * co * ci * kh * 3):
+        check(lib().rdx_sconv_fwd(_p(x), _p(w_tap), _p(y), _p(y2) if y2 is not None else None,
+                                  _p(bn) if bn is not None else None, N, H, W, ci, co, kh, ph, _stream(x)), "sconv_fwd")
+    return y
+
+
+def _sconv_backward(x, dy, wd, weight_shape, ph, need_dx):
+    co, ci, kh, kw = weight_shape
+    N, _, H, W = x.shape
+    Ho = dy.shape[2]
+    dx = _sconv_run(dy, wd, co, ci, kh, kh - 1 - ph) if need_dx else None
+    nblk = lib().rdx_sconv_wgrad_nblk(N, Ho, W)
+    part = torch.empty(nblk, kh * 3 * co * ci, device=x.device, dtype=torch.float32)
+    dw = torch.empty(kh * 3, co, ci, device=x.device, dtype=torch.float32)
+    with _timed("sconv_wgrad", x, 2.0 * N * Ho * W * co * ci * kh * 3):
+        check(lib().rdx_sconv_wgrad(_p(x), _p(dy), _p(dw), _p(part), N, H, W, ci, co, kh, ph, _stream(x)), "sconv_wgrad")
+    return dx, dw.view(kh, 3, co, ci).permute(2, 3, 0, 1)
+
+
+class SConv(torch.autograd.Function):
+    """conv2d(x, weight, padding=(ph, 1)) of the SincNet residual stack, NHWC bf16, no bias (csrc/sconv.hip):
+    the input gradient runs the same MFMA kernel on dY with the flipped kernel, the weight gradient the
+    transposed-operand kernel (per-workgroup partials, fixed-order reduction)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, ph):
+        _require_gpu(x)
+        x = _nhwc(x.to(torch.bfloat16))
+        co, ci, kh, _ = weight.shape
+        wf, wd = _sconv_w(weight)
+        ctx.save_for_backward(x, wd)
+        ctx.meta = (tuple(weight.shape), ph, weight.dtype)
+        return _sconv_run(x, wf, ci, co, kh, ph)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wd = ctx.saved_tensors
+        shape, ph, wdt = ctx.meta
+        dy = _nhwc(dy.to(torch.bfloat16))
+        dx, dw = _sconv_backward(x, dy, wd, shape, ph, ctx.needs_input_grad[0])
+        return dx, dw.to(wdt), None
+
+
+class SConvBnSelu(torch.autograd.Function):
+    """selu(frozen_bn(conv2d(x, weight, padding=(ph, 1)) + conv_bias)) in one forward launch (conv1 -> bn2 ->
+    selu of Residual_block; BnSelu's arithmetic in the conv epilogue). Backward: rdx_bnselu_bwd on the saved
+    conv output (d conv_bias, d gamma, d beta and dc), then the SConv gradients of dc."""
+
+    @staticmethod
+    def forward(ctx, x, weight, ph, conv_bias, mean, invstd, gamma, beta):
+        _require_gpu(x)
+        x = _nhwc(x.to(torch.bfloat16))
+        co, ci, kh, _ = weight.shape
+        wf, wd = _sconv_w(weight)
+        f32 = [t.detach().contiguous().float() for t in (conv_bias, mean, invstd, gamma, beta)]
+        bn = torch.stack([f32[0], f32[1], f32[2] * f32[3], f32[4]]).contiguous()
+        N, _, H, W = x.shape
+        y = torch.empty(N, co, H + 2 * ph - kh + 1, W, device=x.device, dtype=torch.bfloat16,
+                        memory_format=torch.channels_last)
+        c = _sconv_run(x, wf, ci, co, kh, ph, y2=y, bn=bn)
+        ctx.save_for_backward(x, wd, c, *f32)
+        ctx.meta = (tuple(weight.shape), ph, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wd, c, cb, mean, invstd, w, b = ctx.saved_tensors
+        shape, ph, wdt = ctx.meta
+        N, C, H, W = c.shape
+        dy = _nhwc(dy.to(torch.bfloat16))
+        dc = torch.empty_like(c)
+        sums = torch.zeros(3, C, device=c.device, dtype=torch.float32)
+        check(lib().rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(dy), _p(cb), _p(mean), _p(invstd), _p(w), _p(b), _p(dc),
+                                   _p(sums), N * H * W, C, _stream(c)), "bnselu_bwd")
+        dx, dw = _sconv_backward(x, dc, wd, shape, ph, ctx.needs_input_grad[0])
+        return dx, dw.to(wdt), None, sums[0], None, None, sums[1], sums[2]
+
+
 # ------------------------------------------------------------ WavLM positional convolution ----
 def posconv_weights(weight):
     """Conv weight [1024, 64, 128] (weight_norm applied) -> the two bf16 operand layouts of csrc/posconv.hip:

@@ -12,7 +12,7 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import Block0Convs, BnSelu, ResTail, sincconv_absmaxpool
+from .ops import Block0Convs, BnSelu, ResTail, SConv, SConvBnSelu, sconv_ok, sincconv_absmaxpool
 
 
 def _bf16_autocast(x):
@@ -118,20 +118,31 @@ class Residual_block(nn.Module):
                 self.bn1(x)
         if self._fused_ok(x):
             # NHWC fused epilogues (csrc/sincnet.hip): conv1's bias is folded into the frozen-BN+SELU pass,
-            # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass
+            # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass. Under bf16 autocast the
+            # 32/64-channel convolutions run on csrc/sconv.hip (conv1 with the BN+SELU in its epilogue).
             bn = self.bn2
+            bf = _bf16_autocast(x)
+            invstd = torch.rsqrt(bn.running_var + bn.eps)
             idn = None
-            if (self.first and self.downsample and x.shape[1] == 1 and _bf16_autocast(x)
+            if (self.first and self.downsample and x.shape[1] == 1 and bf
                     and os.environ.get("RADHIP_FUSED_B0", "1") != "0"):
                 # one input channel: both convs' backward in one HIP pass (radhip.ops.Block0Convs)
                 c, idn = Block0Convs.apply(x, self.conv1.weight, self.conv_downsample.weight)
+                out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
+            elif bf and sconv_ok(x, self.conv1.weight):
+                out = SConvBnSelu.apply(x, self.conv1.weight, 1, self.conv1.bias, bn.running_mean, invstd,
+                                        bn.weight, bn.bias)
             else:
                 c = F.conv2d(x, self.conv1.weight, None, self.conv1.stride, self.conv1.padding)
-            out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, torch.rsqrt(bn.running_var + bn.eps),
-                               bn.weight, bn.bias)
-            a = F.conv2d(out, self.conv2.weight, None, self.conv2.stride, self.conv2.padding)
+                out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
+            if bf and sconv_ok(out, self.conv2.weight):
+                a = SConv.apply(out, self.conv2.weight, 0)
+            else:
+                a = F.conv2d(out, self.conv2.weight, None, self.conv2.stride, self.conv2.padding)
             if self.downsample:
-                if idn is None:
+                if idn is None and bf and sconv_ok(x, self.conv_downsample.weight):
+                    idn = SConv.apply(x, self.conv_downsample.weight, 0)
+                elif idn is None:
                     idn = F.conv2d(x, self.conv_downsample.weight, None, self.conv_downsample.stride,
                                    self.conv_downsample.padding)
                 bias = self.conv2.bias + self.conv_downsample.bias

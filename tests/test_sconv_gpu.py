@@ -1,0 +1,77 @@
+"""SincNet residual-stack convolutions on the hand-written MFMA kernels (csrc/sconv.hip) against torch fp32.
+
+Every (C_in, C_out, kernel, padding) the Phase-6 SincNet stack uses (Residual_block, src/models/
+DualStreamSEMamba.py:144-200: conv1 2x3 pad (1,1), conv2 2x3 pad (0,1), conv_downsample 1x3 pad (0,1), 32 and
+64 channels), widths that are and are not multiples of the 128-position strip. The reference is conv2d in
+fp32 on the same bf16-rounded operands (what bf16 autocast feeds MIOpen), so the only differences are fp32
+summation order and the bf16 rounding of the outputs: forward and input gradient within bf16 output
+rounding (rtol 1e-2 of the tensor scale), weight gradient (fp32 output, reductions over N*H*W) to 2e-3."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from seeded import seeded_array
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CASES = [(32, 32, 2, 1, 23, 300), (32, 32, 2, 0, 24, 300), (32, 64, 2, 1, 23, 129), (64, 64, 2, 0, 24, 257),
+         (32, 64, 1, 0, 23, 200), (64, 64, 2, 1, 23, 88), (32, 32, 2, 0, 24, 7163)]
+
+
+def _t(tag, shape, scale):
+    return torch.from_numpy(seeded_array(tag, shape, scale=scale)).float().to(torch.bfloat16).float().to(DEV)
+
+
+def _close(got, ref, rtol, what):
+    scale = float(ref.abs().max())
+    np.testing.assert_allclose(got.detach().float().cpu().numpy(), ref.detach().float().cpu().numpy(), rtol=rtol,
+                               atol=rtol * scale,
+                               err_msg=what)
+
+
+@pytest.mark.parametrize("ci,co,kh,ph,H,W", CASES)
+def test_sconv_forward_and_gradients_match_torch(ci, co, kh, ph, H, W):
+    from radhip.ops import SConv
+    N = 2
+    x = _t(f"sc.x{ci}{W}", (N, ci, H, W), 1.0)
+    w = _t(f"sc.w{ci}{co}{kh}", (co, ci, kh, 3), 0.1)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, 1, (ph, 1))
+    dy = _t(f"sc.dy{co}{W}", tuple(ref.shape), 1.0)
+    (ref * dy).sum().backward()
+    xg = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wg = w.clone().requires_grad_(True)
+    y = SConv.apply(xg, wg, ph)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    _close(y, ref, 1e-2, "y")
+    (y.float() * dy).sum().backward()
+    _close(xg.grad, xr.grad, 1e-2, "dx")
+    _close(wg.grad, wr.grad, 2e-3, "dw")
+
+
+def test_sconv_bn_selu_matches_conv_then_bnselu():
+    from radhip.ops import BnSelu, SConvBnSelu
+    N, ci, co, H, W = 2, 32, 64, 23, 300
+    x = _t("scb.x", (N, ci, H, W), 1.0)
+    w = _t("scb.w", (co, ci, 2, 3), 0.1)
+    cb = _t("scb.cb", (co,), 0.1).requires_grad_(True)
+    mean = _t("scb.m", (co,), 0.1)
+    invstd = 1.0 / torch.sqrt(_t("scb.v", (co,), 0.1).abs() + 0.5)
+    gamma = (1 + _t("scb.g", (co,), 0.1)).requires_grad_(True)
+    beta = _t("scb.b", (co,), 0.1).requires_grad_(True)
+    xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    # reference: torch conv2d on the bf16 operands (bf16 output, as autocast), then the fused BnSelu kernel
+    c = F.conv2d(xb.float(), w, None, 1, (1, 1)).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = BnSelu.apply(c, cb, mean, invstd, gamma, beta)
+    dy = _t("scb.dy", tuple(ref.shape), 1.0)
+    (ref.float() * dy).sum().backward()
+    ref_grads = [t.grad.clone() for t in (cb, gamma, beta)]
+    for t in (cb, gamma, beta):
+        t.grad = None
+    got = SConvBnSelu.apply(xb, w, 1, cb, mean, invstd, gamma, beta)
+    _close(got, ref, 2e-2, "y")
+    (got.float() * dy).sum().backward()
+    for g, r, nm in zip((cb.grad, gamma.grad, beta.grad), ref_grads, ("dcb", "dgamma", "dbeta")):
+        _close(g, r, 2e-2, nm)
