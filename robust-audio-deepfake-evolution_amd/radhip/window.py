@@ -84,6 +84,7 @@ class WindowStep:
         self._flat_real = [p for _ in range(self.K) for p in self.fp_real]
         self.ring = _PinnedRing(8192 + 2 * N * 8 + N * (T + nl + 16) + self.K * (self.B * T + nl + 64))
         self.graphs = None
+        self.chain_captured = False
         self.feats = None
         self._host = None
         self.reset_host()
@@ -196,6 +197,18 @@ class WindowStep:
             return
         torch._foreach_add_([p.grad for p in self.fp_real], list(self.fp_copies[k][i].grad for i in range(4)))
 
+    def _adv_step(self, k):
+        """Micro-batch k's FGM chain link: its clean gradient into feature_projection.grad, the attack on the
+        accumulated gradient, the adversarial pass, the restore. All device work, so with one process it is
+        captured as ONE graph per k (no host round trip between the replays); with several ranks the attack's
+        all-reduce (fgm_global_grads) stays outside the graphs."""
+        tr = self.tr
+        self._prefix_grad(k)
+        if self.adv:
+            tr.fgm.attack()
+            self._adv_pass(k)
+            tr.fgm.restore()
+
     def _adv_chain(self, run_adv):
         tr = self.tr
         for k in range(self.K):
@@ -204,6 +217,10 @@ class WindowStep:
                 tr.fgm.attack()
                 run_adv(k)
                 tr.fgm.restore()
+
+    def _chain_in_graph(self):
+        import torch.distributed as dist
+        return self.adv and not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
     # ------------------------------------------------------------------ driver ----------------
     def capture(self, warmup=2):
@@ -214,12 +231,15 @@ class WindowStep:
         self._stage()
         side = torch.cuda.Stream(device=tr.device)
         side.wait_stream(torch.cuda.current_stream(tr.device))
+        chain = self._chain_in_graph()
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self._clean_pass()
                 self._adv_chain(self._adv_pass)
         torch.cuda.current_stream(tr.device).wait_stream(side)
         torch.cuda.synchronize(tr.device)
+        if chain:   # capture must not leave the warm-up's FGM state behind: feature_projection was restored
+            tr.fgm.backup = {}
 
         def new_graph():
             if ops.CAPTURE_TIMING is not None:   # bench.py: stamp the first launch sites of each graph
@@ -230,17 +250,27 @@ class WindowStep:
             self._clean_pass()
         gadv = []
         if self.adv:
+            # the captured attack perturbs feature_projection in place: keep the real values to put back
+            fp_saved = [p.detach().clone() for p in self.fp_real]
             for k in range(self.K):
                 g = new_graph()
                 with torch.cuda.graph(g):
-                    self._adv_pass(k)
+                    if chain:
+                        self._adv_step(k)
+                    else:
+                        self._adv_pass(k)
                 gadv.append(g)
+            with torch.no_grad():
+                for p, v in zip(self.fp_real, fp_saved):
+                    p.copy_(v)
+            tr.fgm.backup = {}
         torch.cuda.synchronize(tr.device)
         self._unbind()
         tr.grads.zero()
         self.fp_grad.zero_()
         tr.loss_sum.copy_(saved_loss)
         self.graphs = (g0, gadv)
+        self.chain_captured = chain
 
     def run(self, last_in_epoch=False):
         """Execute the window (every micro-batch added); ends with the optimizer step."""
@@ -254,7 +284,11 @@ class WindowStep:
                 self.capture()
             g0, gadv = self.graphs
             g0.replay()
-            self._adv_chain(lambda k: gadv[k].replay())
+            if self.chain_captured:
+                for g in gadv:
+                    g.replay()
+            else:
+                self._adv_chain(lambda k: gadv[k].replay())
         else:
             self._clean_pass()
             self._adv_chain(self._adv_pass)
