@@ -41,8 +41,10 @@ class GraphTimer:
         """Call before capturing each graph."""
         self._in_graph = {}
 
-    def slot(self, name, work):
-        grp = self._in_graph.setdefault(name, {"total": 0, "sampled": 0})
+    def slot(self, name, work, shape=None):
+        """shape: an extra key for kernels whose launch sites differ in size within one graph (the SincNet
+        blocks, the CNN layers): sites are grouped (sampled and scaled) per (name, shape), reported per name."""
+        grp = self._in_graph.setdefault((name, shape), {"total": 0, "sampled": 0})
         grp["total"] += 1
         if grp["sampled"] >= self.per_graph:
             return None
@@ -81,15 +83,15 @@ class GraphTimer:
 
 
 class _timed:
-    __slots__ = ("name", "t", "work", "ev", "reg", "site")
+    __slots__ = ("name", "t", "work", "ev", "reg", "site", "shape")
 
-    def __init__(self, name, t, work=0.0):
-        self.name, self.t, self.work = name, t, work
+    def __init__(self, name, t, work=0.0, shape=None):
+        self.name, self.t, self.work, self.shape = name, t, work, shape
         self.reg = self.site = None
 
     def __enter__(self):
         if CAPTURE_TIMING is not None and torch.cuda.is_current_stream_capturing():
-            self.site = CAPTURE_TIMING.slot(self.name, self.work)   # None: this site is not sampled
+            self.site = CAPTURE_TIMING.slot(self.name, self.work, self.shape)   # None: not a sampled site
             if self.site is not None:
                 check(lib().rdx_timestamp_acc(_p(self.site), -1, _stream(self.t)), "timestamp")
         elif TIMING is not None:
@@ -575,7 +577,9 @@ def _sconv_run(x, w_tap, ci, co, kh, ph, y2=None, bn=None):
     N, _, H, W = x.shape
     Ho = H + 2 * ph - kh + 1
     y = torch.empty(N, co, Ho, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
-    with _timed("sconv_fwd", x, 2.0 * N * Ho * W * co * ci * kh * 3):
+    # algorithmic HBM bytes (the convolution is HBM-bound: ~100 FLOP per byte at these channel counts)
+    nbytes = 2.0 * (N * H * W * ci + N * Ho * W * co * (2 if y2 is not None else 1))
+    with _timed("sconv_fwd", x, nbytes, shape=(N, H, W, ci, co, kh, ph)):
         check(lib().rdx_sconv_fwd(_p(x), _p(w_tap), _p(y), _p(y2) if y2 is not None else None,
                                   _p(bn) if bn is not None else None, N, H, W, ci, co, kh, ph, _stream(x)), "sconv_fwd")
     return y
@@ -589,7 +593,7 @@ def _sconv_backward(x, dy, wd, weight_shape, ph, need_dx):
     nblk = lib().rdx_sconv_wgrad_nblk(N, Ho, W)
     part = torch.empty(nblk, kh * 3 * co * ci, device=x.device, dtype=torch.float32)
     dw = torch.empty(kh * 3, co, ci, device=x.device, dtype=torch.float32)
-    with _timed("sconv_wgrad", x, 2.0 * N * Ho * W * co * ci * kh * 3):
+    with _timed("sconv_wgrad", x, 2.0 * (N * H * W * ci + N * Ho * W * co), shape=(N, H, W, ci, co, kh, ph)):
         check(lib().rdx_sconv_wgrad(_p(x), _p(dy), _p(dw), _p(part), N, H, W, ci, co, kh, ph, _stream(x)), "sconv_wgrad")
     return dx, dw.view(kh, 3, co, ci).permute(2, 3, 0, 1)
 
@@ -888,18 +892,18 @@ def feature_encoder_fused(x, ops_):
     w0, b0, g0, be0, eps0, k0, s0 = ops_[0]
     T = (L - k0) // s0 + 1
     h = torch.empty(B, T, 512, device=x.device, dtype=torch.bfloat16)
-    with _timed("fe_conv0", x, 2.0 * B * T * 512 * k0):
+    with _timed("fe_conv0", x, 4.0 * B * L + 2.0 * B * T * 512):            # bytes: waveform in, bf16 out
         check(lib().rdx_fe_conv0(_p(x), B, L, _p(w0), _p(b0), _p(g0), _p(be0), eps0, k0, s0, _p(h), _stream(x)),
               "fe_conv0")
     for i, (w, b, g, be, eps, k, s) in enumerate(ops_[1:], start=1):
         To = (T - k) // s + 1
         y = torch.empty(B, To, 512, device=x.device, dtype=torch.bfloat16)
-        with _timed("fe_conv_gemm", x, gemm_flops(B * To, 512, k * 512)):
+        with _timed("fe_conv_gemm", x, gemm_flops(B * To, 512, k * 512), shape=(B, T, k)):
             check(lib().rdx_gemm_bf16_strided(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To, B, To, 512,
                                               k * 512, _p(b) if b is not None else None, _stream(x)), "gemm_bf16_strided")
         last = i == len(ops_) - 1
         out32 = torch.empty(B, To, 512, device=x.device, dtype=torch.float32) if last else None
-        with _timed("fe_ln_gelu", x, 0.0):
+        with _timed("fe_ln_gelu", x, (2.0 + (4.0 if last else 2.0)) * B * To * 512, shape=(B, To)):
             check(lib().rdx_fe_ln_gelu(_p(y), B * To, _p(g), _p(be), eps, _p(out32) if last else None, _stream(x)),
                   "fe_ln_gelu")
         h, T = (out32 if last else y), To
