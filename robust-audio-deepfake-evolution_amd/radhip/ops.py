@@ -563,7 +563,25 @@ def sconv_ok(x, weight):
             and kw == 3 and os.environ.get("RADHIP_SCONV", "1") != "0")
 
 
+# Per-window cache of the SincNet convolution weight layouts (radhip/window.py sets it to a dict for the span
+# of one accumulation window, in which the parameters do not change): the clean pass prepares them, the
+# adversarial passes reuse them. Under HIP graphs the clean pass's graph rewrites the cached tensors on every
+# replay and the adversarial graphs read them.
+SCONV_WCACHE = None
+
+
 def _sconv_w(weight):
+    if SCONV_WCACHE is not None:
+        hit = SCONV_WCACHE.get(id(weight))
+        if hit is not None and hit[0] is weight:
+            return hit[1], hit[2]
+    wf, wd = _sconv_w_prep(weight)
+    if SCONV_WCACHE is not None:
+        SCONV_WCACHE[id(weight)] = (weight, wf, wd)
+    return wf, wd
+
+
+def _sconv_w_prep(weight):
     """[C_out, C_in, KH, 3] -> tap-major [KH*3][C_out][C_in] bf16 (forward) and the flipped, transposed
     [KH*3][C_in][C_out] bf16 (input gradient = the same convolution of dY)."""
     co, ci, kh, kw = weight.shape

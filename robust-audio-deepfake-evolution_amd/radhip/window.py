@@ -82,8 +82,14 @@ class WindowStep:
             self.fp_copies.append(tuple(group))
         self._flat_copies = [c for g in self.fp_copies for c in g]
         self._flat_real = [p for _ in range(self.K) for p in self.fp_real]
+        # parameters whose gradients autograd delivers (everything trainable but the LoRA weights, which
+        # the fused WavLM layer accumulates into .grad itself): during a pass their .grad is unset, so
+        # autograd hands each gradient over instead of launching one fp32 add per parameter into the flat
+        # buffer; one multi-tensor add per pass then accumulates them (_pass_grads)
+        self.handed = [p for n, p in m.named_parameters() if p.requires_grad and "lora_" not in n]
         self.ring = _PinnedRing(8192 + 2 * N * 8 + N * (T + nl + 16) + self.K * (self.B * T + nl + 64))
         self.graphs = None
+        self._wcache = {}
         self.chain_captured = False
         self.feats = None
         self._host = None
@@ -147,7 +153,27 @@ class WindowStep:
         ya, yb = self.ya[k * B:(k + 1) * B], self.yb[k * B:(k + 1) * B]
         return lam * tr.criterion(out, ya) + (1.0 - lam) * tr.criterion(out, yb)
 
+    def _pass_grads(self, fn):
+        """Run one forward/backward with the handed-over gradients unset, then add them into the flat
+        fp32 buffer in one multi-tensor launch and point .grad back at its views."""
+        views = [p.grad for p in self.handed]
+        for p in self.handed:
+            p.grad = None
+        try:
+            fn()
+        finally:
+            got = [(v, p.grad) for p, v in zip(self.handed, views) if p.grad is not None]
+            if got:
+                torch._foreach_add_([v for v, _ in got], [g for _, g in got])
+            for p, v in zip(self.handed, views):
+                p.grad = v
+
     def _clean_pass(self):
+        self._wcache = {}                  # weight layouts prepared by this pass, reused by the window's others
+        ops.SCONV_WCACHE = self._wcache
+        self._pass_grads(self._clean_pass_body)
+
+    def _clean_pass_body(self):
         tr, core, B = self.tr, self.core, self.B
         with torch.no_grad():
             torch._foreach_copy_(self._flat_copies, self._flat_real)
@@ -170,6 +196,13 @@ class WindowStep:
             core.cnn_reuse = None
 
     def _adv_pass(self, k):
+        ops.SCONV_WCACHE = self._wcache
+        try:
+            self._pass_grads(lambda: self._adv_pass_body(k))
+        finally:
+            ops.SCONV_WCACHE = None
+
+    def _adv_pass_body(self, k):
         tr, core, B = self.tr, self.core, self.B
         self.conv.mask_dev = self.a_mask[k]
         core.time_mask_dev = self.a_tmask[k]
@@ -186,6 +219,7 @@ class WindowStep:
             core.cnn_feats_given = None
 
     def _unbind(self):
+        ops.SCONV_WCACHE = None
         self.conv.mask_dev = None
         self.core.time_mask_dev = None
         self.core.encoder.keep_dev = None
@@ -282,6 +316,7 @@ class WindowStep:
         if self.graphs_on:
             if self.graphs is None:
                 self.capture()
+            ops.SCONV_WCACHE = None
             g0, gadv = self.graphs
             g0.replay()
             if self.chain_captured:
