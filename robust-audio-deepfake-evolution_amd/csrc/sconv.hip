@@ -225,15 +225,45 @@ __global__ __launch_bounds__(SC_T) void sconv_wgrad_kernel(SWgradArgs a) {
   for (int j = 0; j < PER; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-  auto stage_x = [&](int n, int hi, int p0, char* slot) {
-    for (int i = tid; i < SC_XR * (CI / 8); i += SC_T) {
+  // one staged row per thread-slice: X rows (SC_XR x CI) and dY rows (SC_P x CO) as 16-byte vectors, loaded
+  // into registers one row ahead and written to their LDS slot after the current row's MFMAs
+  constexpr int XV = SC_XR * (CI / 8), XN = (XV + SC_T - 1) / SC_T;
+  constexpr int DV = SC_P * (CO / 8), DN = (DV + SC_T - 1) / SC_T;
+  auto load_x = [&](uint4 (&r)[XN], int n, int hi, int p0) {
+#pragma unroll
+    for (int j = 0; j < XN; ++j) {
+      const int i = tid + SC_T * j;
       const int ch = i % (CI / 8), pp = i / (CI / 8), wi = p0 - 1 + pp;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (pp < SC_PW && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
-        v = *reinterpret_cast<const uint4*>(a.x + (((int64_t)n * a.H + hi) * a.W + wi) * CI + ch * 8);
-      *reinterpret_cast<uint4*>(slot + sc_img<CI>(pp, ch)) = v;
+      r[j] = make_uint4(0, 0, 0, 0);
+      if (i < XV && pp < SC_PW && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
+        r[j] = *reinterpret_cast<const uint4*>(a.x + (((int64_t)n * a.H + hi) * a.W + wi) * CI + ch * 8);
     }
   };
+  auto store_x = [&](char* slot, const uint4 (&r)[XN]) {
+#pragma unroll
+    for (int j = 0; j < XN; ++j) {
+      const int i = tid + SC_T * j;
+      if (i < XV) *reinterpret_cast<uint4*>(slot + sc_img<CI>(i / (CI / 8), i % (CI / 8))) = r[j];
+    }
+  };
+  auto load_dy = [&](uint4 (&r)[DN], int n, int ho, int p0) {
+#pragma unroll
+    for (int j = 0; j < DN; ++j) {
+      const int i = tid + SC_T * j;
+      const int ch = i % (CO / 8), pp = i / (CO / 8), wi = p0 + pp;
+      r[j] = make_uint4(0, 0, 0, 0);
+      if (i < DV && ho < a.Ho && wi < a.W)
+        r[j] = *reinterpret_cast<const uint4*>(a.dy + (((int64_t)n * a.Ho + ho) * a.W + wi) * CO + ch * 8);
+    }
+  };
+  auto store_dy = [&](char* slot, const uint4 (&r)[DN]) {
+#pragma unroll
+    for (int j = 0; j < DN; ++j) {
+      const int i = tid + SC_T * j;
+      if (i < DV) *reinterpret_cast<uint4*>(slot + sc_img<CO>(i / (CO / 8), i % (CO / 8))) = r[j];
+    }
+  };
+  uint4 rx[XN], rd[DN];
   for (int64_t u = blockIdx.x; u < a.units; u += gridDim.x) {
     const int zc = (int)(u % a.nz);
     const int64_t us = u / a.nz;
@@ -241,17 +271,19 @@ __global__ __launch_bounds__(SC_T) void sconv_wgrad_kernel(SWgradArgs a) {
     const int p0 = strip * SC_P;
     const int ho0 = zc * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
     __syncthreads();  // the previous unit's reads are done
-    for (int kh = 0; kh + 1 < KH; ++kh) stage_x(n, ho0 + kh - a.ph, p0, xi + ((ho0 + kh) % NSLOT) * XSLOT);
+    for (int kh = 0; kh < KH; ++kh) {  // input rows of output row ho0, and its dY row
+      load_x(rx, n, ho0 + kh - a.ph, p0);
+      store_x(xi + ((ho0 + kh) % NSLOT) * XSLOT, rx);
+    }
+    load_dy(rd, n, ho0, p0);
+    store_dy(dyi + (ho0 & 1) * DSLOT, rd);
+    if (ho0 + 1 < ho1) {  // prefetch the rows output row ho0 + 1 adds
+      load_x(rx, n, ho0 + 1 - a.ph + KH - 1, p0);
+      load_dy(rd, n, ho0 + 1, p0);
+    }
     for (int ho = ho0; ho < ho1; ++ho) {
-      stage_x(n, ho - a.ph + KH - 1, p0, xi + ((ho + KH - 1) % NSLOT) * XSLOT);
-      char* dys = dyi + (ho & 1) * DSLOT;
-      for (int i = tid; i < SC_P * (CO / 8); i += SC_T) {
-        const int ch = i % (CO / 8), pp = i / (CO / 8), wi = p0 + pp;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (wi < a.W) v = *reinterpret_cast<const uint4*>(a.dy + (((int64_t)n * a.Ho + ho) * a.W + wi) * CO + ch * 8);
-        *reinterpret_cast<uint4*>(dys + sc_img<CO>(pp, ch)) = v;
-      }
       __syncthreads();
+      const char* dys = dyi + (ho & 1) * DSLOT;
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         const int tile = wv + 4 * j;
@@ -264,6 +296,15 @@ __global__ __launch_bounds__(SC_T) void sconv_wgrad_kernel(SWgradArgs a) {
           // output position pl pairs with staged input row pl + kw (input column p0 + pl + kw - 1)
           acc[j] = sc_mfma(sc_read_tr<CO>(dys, 0, tco * 32, s, lane), sc_read_tr<CI>(xk, kw, tci * 32, s, lane),
                            acc[j]);
+        }
+      }
+      if (ho + 1 < ho1) {
+        // the slots of rows ho - 1 (X) and ho - 1 (dY) are free: every wave passed this row's barrier
+        store_x(xi + ((ho + KH) % NSLOT) * XSLOT, rx);
+        store_dy(dyi + ((ho + 1) & 1) * DSLOT, rd);
+        if (ho + 2 < ho1) {
+          load_x(rx, n, ho + 2 - a.ph + KH - 1, p0);
+          load_dy(rd, n, ho + 2, p0);
         }
       }
     }
