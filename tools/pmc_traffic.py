@@ -20,7 +20,8 @@ import sys
 
 # bench.py operation -> the kernels of one launch of it
 OPS = {"attn_fwd": ("attn_fwd",), "attn_bwd": ("attn_bwd",), "posconv_fwd": ("posconv_kernel<false>",),
-       "posconv_bwd": ("posconv_kernel<true>",), "sincnet_b0_bwd": ("b0_bwd_kernel",)}
+       "posconv_bwd": ("posconv_kernel<true>",), "sincnet_b0_bwd": ("b0_bwd_kernel",),
+       "sconv_fwd": ("sconv_fwd_kernel",), "sconv_wgrad": ("sconv_wgrad_kernel",)}
 
 
 def per_kernel(path, counter):
@@ -31,7 +32,7 @@ def per_kernel(path, counter):
                 continue
             name = r["Kernel_Name"].split("(")[0].replace("void ", "")
             vals[name].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+    return {k: (sum(v), len(v)) for k, v in vals.items()}
 
 
 def main(d):
@@ -39,17 +40,29 @@ def main(d):
     for B in (8, 32):
         f = per_kernel(os.path.join(d, f"attn_FETCH_SIZE_{B}.csv"), "FETCH_SIZE")
         w = per_kernel(os.path.join(d, f"attn_WRITE_SIZE_{B}.csv"), "WRITE_SIZE")
-        rows = {k: {"fetch_kib": f.get(k, 0.0), "write_kib": w.get(k, 0.0),
-                    "hbm_bytes": 2 * 1024 * f.get(k, 0.0) + 1024 * w.get(k, 0.0)}
-                for k in sorted(set(f) | set(w)) if "rdx::" in k}
+        rows = {}
+        for k in sorted(set(f) | set(w)):
+            if "rdx::" not in k:
+                continue
+            fs, fn = f.get(k, (0.0, 1))
+            ws, wn = w.get(k, (0.0, 1))
+            rows[k] = {"fetch_kib": fs / fn, "write_kib": ws / wn, "dispatches": max(fn, wn),
+                       "hbm_bytes": 2 * 1024 * fs / fn + 1024 * ws / wn}
         res[f"B{B}"] = {"kernels": rows}
         for op, keys in OPS.items():
-            res[f"B{B}"][op] = sum(v["hbm_bytes"] for k, v in rows.items() if any(x in k for x in keys))
+            sel = [v for k, v in rows.items() if any(x in k for x in keys)]
+            tot = sum(v["hbm_bytes"] * v["dispatches"] for v in sel)
+            cnt = sum(v["dispatches"] for v in sel)
+            # bytes per dispatch of this operation, over all its shapes / template variants
+            res[f"B{B}"][op] = (tot, cnt)
     out = {"note": ("HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x 2 gfx950 correction + WRITE_SIZE, "
                     "KiB -> bytes); per-launch value = (B32 + 4 B8) / 5, the bench's launch mix")}
     for k in OPS:
-        out[k] = {"hbm_bytes_per_launch": round((res["B32"][k] + 4 * res["B8"][k]) / 5),
-                  "B8": round(res["B8"][k]), "B32": round(res["B32"][k])}
+        (t32, c32), (t8, c8) = res["B32"][k], res["B8"][k]
+        if c32 + c8 == 0:
+            continue
+        out[k] = {"hbm_bytes_per_launch": round((t32 + 4 * t8) / max(c32 + 4 * c8, 1)),
+                  "B8": round(t8 / max(c8, 1)), "B32": round(t32 / max(c32, 1))}
     out["detail"] = res
     print(json.dumps(out, indent=1))
 
