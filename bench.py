@@ -266,11 +266,14 @@ def cpu_baseline(config, threads, protocol):
     plan = [(2, 3, 10), (8, 3, 10)] if protocol == "full" else [(2, 1, 2)]
     runs = []
     for B, warm, timed in plan:
-        for _ in range(warm):
+        for i in range(warm):
             step(B)
+            print(f"[cpu_baseline] B={B} warm-up step {i + 1}/{warm}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
-        for _ in range(timed):
+        for i in range(timed):
             step(B)
+            print(f"[cpu_baseline] B={B} timed step {i + 1}/{timed} {time.perf_counter() - t0:.1f} s",
+                  file=sys.stderr, flush=True)
         dt = time.perf_counter() - t0
         runs.append({"micro_batch": B, "warmup_steps": warm, "timed_steps": timed, "seconds": round(dt, 2),
                      "utt_s": round(B * timed / dt, 4)})
