@@ -381,8 +381,19 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    prof = None
+    if os.environ.get("RADHIP_TORCH_PROFILE"):     # tools: which framework ops launch the small kernels
+        from torch.profiler import ProfilerActivity, profile
+        prof = profile(activities=[ProfilerActivity.CPU], record_shapes=True)
+        prof.__enter__()
     for _ in range(args.steps):
         step()
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        with open(os.environ["RADHIP_TORCH_PROFILE"], "w") as f:
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="count", row_limit=250,
+                                                                         max_name_column_width=40,
+                                                                         max_shapes_column_width=120))
     ev1.record(stream)
     torch.cuda.synchronize()
     if ws > 1:

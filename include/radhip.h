@@ -199,6 +199,21 @@ int rdx_fgm_attack(int ntensors, float* const* params, const float* const* grads
                    float* const* backup, const int64_t* numels, float eps, double* workspace,
                    void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Mixup focal loss, replaces criterion(out, y_a) * lam + criterion(out, y_b) * (1 - lam), divided by the
+ * accumulation steps (src/main.py:297-305 kornia FocalLoss, :1040-1050 mixup + accumulation):
+ *   loss = scale * sum_b [ lam_b f(z_b, ya_b) + (1 - lam_b) f(z_b, yb_b) ],  lam_b = lam[b / rows_per_lam]
+ *   f(z, y) = -a_y (1 - p_y)^gamma log p_y,  p = softmax(z);  mode 0: a_y = y == 0 ? 1 - alpha : alpha
+ *   (kornia >= 0.7 'per_class'), mode 1: a_y = alpha; alpha < 0: a = 1.
+ * logits [B, C] (row stride ld, bf16 when logits_bf16 else fp32), C <= 16; yb NULL: no mixup (lam ignored
+ * for the weight of ya when lam is NULL, = 1). One workgroup writes loss (fp32 scalar) and dlogits (fp32
+ * [B, C], d loss / d logits). rdx_focal_mixup_bwd: out = grad[0] * dlogits in the logits' dtype (n = B*C).
+ * ------------------------------------------------------------------------------------------ */
+int rdx_focal_mixup_fwd(const void* logits, int logits_bf16, int ld, int B, int C, const int64_t* ya,
+                        const int64_t* yb, const float* lam, int rows_per_lam, float alpha, float gamma,
+                        int mode, float scale, float* loss, float* dlogits, void* stream);
+int rdx_focal_mixup_bwd(const float* grad, const float* dlogits, void* out, int out_bf16, int n, void* stream);
+
 /* ---- SincNet residual stack, NHWC fused epilogues (Residual_block.forward,
  * src/models/DualStreamSEMamba.py:182-200, with freeze_bn: src/main.py:44-51,1016-1018) -----------
  * Activations are [npix, C] row-major (channels_last), C % 8 == 0, C <= 512, 256 % (C/8) == 0.

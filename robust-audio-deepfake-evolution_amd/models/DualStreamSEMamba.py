@@ -7,7 +7,8 @@ strictly. forward(x[B, T], Freq_aug) -> (features[B, emb], logits[B, 2]).
 
 What runs where:
   WavLM stream   radhip.wavlm (fused frozen QKV GEMM, SDPA) + HIP layer-weighted sum
-  SincNet stream HIP fused SincConv+|.|+maxpool, then the residual Conv2d encoder (MIOpen)
+  SincNet stream HIP fused SincConv+|.|+maxpool, then the residual Conv2d encoder (csrc/sconv.hip), on a
+                 side stream so that it is a parallel branch of the captured graphs
   Bi-Mamba       radhip.mamba.Mamba.bidirectional: HIP conv / selective scan / gate, both
                  directions per launch, one shared out_proj
 """
@@ -50,6 +51,19 @@ def _load_hf_weights(model, path):
     if missing:
         raise RuntimeError(f"WavLM checkpoint at {path} lacks {len(missing)} tensors, e.g. {missing[:3]}")
     model.load_state_dict(ren, strict=True)
+
+
+_SIDE = {}
+
+
+def _side_stream(x):
+    """Per-device side stream for the SincNet branch (RADHIP_SINC_BRANCH=0 runs both streams in order)."""
+    if not x.is_cuda or os.environ.get("RADHIP_SINC_BRANCH", "1") == "0":
+        return None
+    d = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    if d not in _SIDE:
+        _SIDE[d] = torch.cuda.Stream(device=d)
+    return _SIDE[d]
 
 
 class WavLMFrontend(nn.Module):
@@ -183,11 +197,28 @@ class Model(nn.Module):
         self.dropout = nn.Dropout(0.1)
         self.classifier = nn.Linear(emb_size, 2)
 
+    def _streams(self, x, Freq_aug):
+        """The two streams are independent until the fusion. On the GPU the SincNet stream runs on a side
+        stream forked from the current one (reference order: WavLM, then SincNet, :728-750), so inside a
+        captured HIP graph it is a parallel branch: its kernels (and, because autograd runs each backward
+        op on its forward op's stream, its backward) fill the CUs the latency-bound WavLM kernels leave idle.
+        No RNG is drawn inside either stream (the band mask is drawn on the host), so the order is free."""
+        side = _side_stream(x)
+        if side is None:
+            return self.wavlm_stream(x), self.sinc_stream(x, freq_aug=Freq_aug)
+        cur = torch.cuda.current_stream(x.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            f_sinc = self.sinc_stream(x, freq_aug=Freq_aug)
+        f_wavlm = self.wavlm_stream(x)
+        cur.wait_stream(side)
+        f_sinc.record_stream(cur)
+        return f_wavlm, f_sinc
+
     def forward(self, x, Freq_aug=False):
         if x.ndim == 3:
             x = x.squeeze(-1)
-        f_wavlm = self.wavlm_stream(x)
-        f_sinc = self.sinc_stream(x, freq_aug=Freq_aug)
+        f_wavlm, f_sinc = self._streams(x, Freq_aug)
         f = self.fusion(f_wavlm, f_sinc)
         for layer in self.backbone_layers:
             f = layer(f)

@@ -132,6 +132,9 @@ SIGNATURES = {
                          c_f32, c_int, c_vp]),
     "rdx_timestamp_acc": (c_int, [c_vp, c_int, c_vp]),
     "rdx_wallclock_khz": (c_int, [c_int]),
+    "rdx_focal_mixup_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_int,
+                                    c_f32, c_vp, c_vp, c_vp]),
+    "rdx_focal_mixup_bwd": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "rdx_fgm_attack": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                ctypes.POINTER(c_i64), c_f32, c_vp, c_vp]),
 }

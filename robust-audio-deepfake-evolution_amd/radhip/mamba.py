@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ops import BiGate, DWConvBidir, SelectiveScan
+from .ops import BiGate, DWConvBidir, SelectiveScan, SplitLast
 
 
 class Mamba(nn.Module):
@@ -60,12 +60,13 @@ class Mamba(nn.Module):
     def _run(self, x, dirs):
         Di, R, N = self.d_inner, self.dt_rank, self.d_state
         xz = self.in_proj(x)                                    # [B, L, 2*Di]
-        u = DWConvBidir.apply(xz[..., :Di], self.conv1d.weight, self.conv1d.bias, dirs)  # [dirs, B, L, Di]
+        xi, z = SplitLast.apply(xz, Di, Di)                     # views; backward is one concatenation
+        u = DWConvBidir.apply(xi, self.conv1d.weight, self.conv1d.bias, dirs)  # [dirs, B, L, Di]
         x_dbl = F.linear(u, self.x_proj.weight)                 # [dirs, B, L, R + 2N]
-        delta = F.linear(x_dbl[..., :R], self.dt_proj.weight)   # bias + softplus are fused in the scan
-        y = SelectiveScan.apply(u, delta, self.A_log, x_dbl[..., R:R + N], x_dbl[..., R + N:], self.D,
-                                self.dt_proj.bias)              # [dirs, B, L, Di] fp32
-        g = BiGate.apply(y, xz[..., Di:])                       # (sum_dir y) * silu(z)
+        dt, Bm, Cm = SplitLast.apply(x_dbl, R, N, N)
+        delta = F.linear(dt, self.dt_proj.weight)               # bias + softplus are fused in the scan
+        y = SelectiveScan.apply(u, delta, self.A_log, Bm, Cm, self.D, self.dt_proj.bias)  # [dirs, B, L, Di] fp32
+        g = BiGate.apply(y, z)                                  # (sum_dir y) * silu(z)
         return self.out_proj(g)
 
     def forward(self, hidden_states, inference_params=None):

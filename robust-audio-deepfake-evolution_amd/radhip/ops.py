@@ -360,6 +360,75 @@ def layer_weighted_sum(hidden_states, layer_weights):
     return LayerWeightedSum.apply(layer_weights, *hidden_states)
 
 
+class SplitLast(torch.autograd.Function):
+    """x[..., a:b] views of consecutive last-dim ranges whose backward is ONE concatenation of the parts'
+    gradients, instead of one zero-fill + copy per slice and an add per extra slice (SliceBackward)."""
+
+    @staticmethod
+    def forward(ctx, x, *sizes):
+        ctx.sizes, ctx.dtype = sizes, x.dtype
+        outs, o = [], 0
+        for n in sizes:
+            outs.append(x.narrow(-1, o, n))
+            o += n
+        if o != x.shape[-1]:
+            raise ValueError("SplitLast: the sizes must cover the last dimension")
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        return (torch.cat([g.to(ctx.dtype) for g in grads], dim=-1),) + (None,) * len(ctx.sizes)
+
+
+# ----------------------------------------------------------------------------------- loss ----
+class MixupFocal(torch.autograd.Function):
+    """scale * sum_b [lam_b focal(z_b, ya_b) + (1 - lam_b) focal(z_b, yb_b)] on csrc/loss.hip: the value and
+    d/dlogits in one launch, the backward in one more (lam_b = lam[b // rows_per_lam], a device tensor)."""
+
+    @staticmethod
+    def forward(ctx, logits, ya, yb, lam, rows_per_lam, alpha, gamma, mode, scale):
+        _require_gpu(logits, ya)
+        if logits.dim() != 2 or logits.dtype not in (torch.bfloat16, torch.float32) or logits.stride(1) != 1:
+            raise ValueError("mixup focal: [B, C] bf16/fp32 logits with unit column stride required")
+        B, C = logits.shape
+        ya = ya.contiguous()
+        yb = yb.contiguous() if yb is not None else None
+        lam = lam.contiguous().float() if lam is not None else None
+        if ya.dtype != torch.int64 or ya.numel() != B or (yb is not None and (yb.dtype != torch.int64 or yb.numel() != B)):
+            raise ValueError("mixup focal: int64 labels of B entries required")
+        if lam is not None and lam.numel() * rows_per_lam < B:
+            raise ValueError("mixup focal: lam has too few entries for the rows")
+        loss = torch.empty((), device=logits.device, dtype=torch.float32)
+        d32 = torch.empty(B, C, device=logits.device, dtype=torch.float32)
+        check(lib().rdx_focal_mixup_fwd(_p(logits), int(logits.dtype == torch.bfloat16), logits.stride(0), B, C, _p(ya),
+                                        _p(yb) if yb is not None else None, _p(lam) if lam is not None else None,
+                                        int(rows_per_lam), float(alpha), float(gamma), int(mode), float(scale),
+                                        _p(loss), _p(d32), _stream(logits)), "focal_mixup_fwd")
+        ctx.save_for_backward(d32)
+        ctx.out_dtype = logits.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        d32, = ctx.saved_tensors
+        g = g.float().contiguous()
+        out = torch.empty(d32.shape, device=d32.device, dtype=ctx.out_dtype)
+        check(lib().rdx_focal_mixup_bwd(_p(g), _p(d32), _p(out), int(ctx.out_dtype == torch.bfloat16), d32.numel(),
+                                        _stream(d32)), "focal_mixup_bwd")
+        return out, None, None, None, None, None, None, None, None
+
+
+def mixup_focal(logits, ya, yb, lam, rows_per_lam, focal, divisor):
+    """The mixup focal criterion of a pass, divided by `divisor` (the accumulation steps), for a
+    radhip.train.FocalLoss `focal`: per_class mode averages each micro-batch of rows_per_lam rows over its
+    rows * C elements, scalar mode over its rows."""
+    C = logits.shape[1]
+    mode = 0 if focal.alpha_mode == "per_class" else 1
+    scale = 1.0 / (rows_per_lam * (C if mode == 0 else 1) * divisor)
+    alpha = -1.0 if focal.alpha is None else float(focal.alpha)
+    return MixupFocal.apply(logits, ya, yb, lam, rows_per_lam, alpha, float(focal.gamma), mode, scale)
+
+
 # ------------------------------------------------------------------------------------ FGM ----
 def fgm_attack(params, grads, backups, eps):
     """backup <- p; p += eps * g / ||g|| per tensor (skip when the norm is 0 or NaN). fp32 tensors."""

@@ -498,6 +498,7 @@ class WavLMEncoderModel(nn.Module):
         # micro-batch's own feature_projection gradient (the FGM attack needs the running sums)
         self.cnn_feats_given = None
         self.fp_groups = None
+        self.fp_nocache = True
 
     def _cnn_frozen(self):
         return not self.feature_extractor.training and not any(p.requires_grad for p in self.feature_extractor.parameters())
@@ -526,6 +527,10 @@ class WavLMEncoderModel(nn.Module):
             for xk, (lw, lb, pw, pb) in zip(feats.chunk(K, dim=0), self.fp_groups):
                 parts.append(F.linear(F.layer_norm(xk, xk.shape[-1:], lw, lb, fp.layer_norm.eps), pw, pb))
             h = fp.dropout(torch.cat(parts, dim=0))
+        elif self.fp_nocache and torch.is_autocast_enabled("cuda"):
+            # the FGM target changes between the passes of one autocast region: cast it afresh each time
+            with torch.autocast("cuda", dtype=torch.get_autocast_dtype("cuda"), cache_enabled=False):
+                h = self.feature_projection(feats)
         else:
             h = self.feature_projection(feats)
         c = self.config

@@ -147,11 +147,37 @@ class WindowStep:
                          (h["a_tmask"], self.a_tmask), (h["a_keep"], self.a_keep)])
 
     # ------------------------------------------------------------------ passes ----------------
+    def _amp(self):
+        """Autocast with its weight-cast cache on. Every pass of a window runs inside one outer context
+        (run / capture), so each trainable fp32 weight is cast to the compute dtype once per window, by the
+        clean pass (inside graph G0 when graphed), and the adversarial passes reuse that copy: the weights
+        do not change within a window. The one exception, the FGM target feature_projection, is perturbed
+        between passes and is cast without the cache (WavLMModel.forward, fp_nocache)."""
+        tr = self.tr
+        return torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32, cache_enabled=True)
+
     def _loss(self, out, k):
         tr, B = self.tr, self.B
         lam = self.lam[k]
         ya, yb = self.ya[k * B:(k + 1) * B], self.yb[k * B:(k + 1) * B]
         return lam * tr.criterion(out, ya) + (1.0 - lam) * tr.criterion(out, yb)
+
+    def _focal_fused(self, out):
+        from .train import FocalLoss
+        return isinstance(self.tr.criterion, FocalLoss) and out.is_cuda and out.shape[1] <= 16
+
+    def _pass_loss(self, out, k=None):
+        """The pass's loss / accum: micro-batch k's rows (adversarial pass) or all K (clean pass). The focal
+        criterion is one HIP launch per pass (ops.mixup_focal); any other criterion runs as modules."""
+        tr, B, K = self.tr, self.B, self.K
+        if self._focal_fused(out):
+            if k is None:
+                return ops.mixup_focal(out, self.ya, self.yb, self.lam, B, tr.criterion, tr.accum)
+            sl = slice(k * B, (k + 1) * B)
+            return ops.mixup_focal(out, self.ya[sl], self.yb[sl], self.lam[k:k + 1], B, tr.criterion, tr.accum)
+        if k is None:
+            return sum(self._loss(out[j * B:(j + 1) * B], j) for j in range(K)) / tr.accum
+        return self._loss(out, k) / tr.accum
 
     def _pass_grads(self, fn):
         """Run one forward/backward with the handed-over gradients unset, then add them into the flat
@@ -184,10 +210,9 @@ class WindowStep:
         core.time_mask_dev = self.c_tmask
         core.encoder.keep_dev = self.c_keep
         try:
-            with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32,
-                                cache_enabled=False):
+            with self._amp():
                 _, out = tr.model(self.x, Freq_aug=tr.freq_aug)
-                loss = sum(self._loss(out[k * B:(k + 1) * B], k) for k in range(self.K)) / tr.accum
+                loss = self._pass_loss(out)
             tr.scaler.scale(loss).backward()
             tr.loss_sum.add_(loss.detach().double() * (tr.accum * B))
         finally:
@@ -210,10 +235,9 @@ class WindowStep:
         if self.feats is not None:
             core.cnn_feats_given = self.feats[k * B:(k + 1) * B]
         try:
-            with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32,
-                                cache_enabled=False):
+            with self._amp():
                 _, out = tr.model(self.x[k * B:(k + 1) * B], Freq_aug=tr.freq_aug)
-                adv = self._loss(out, k) / tr.accum
+                adv = self._pass_loss(out, k)
             tr.scaler.scale(adv).backward()
         finally:
             core.cnn_feats_given = None
@@ -268,8 +292,9 @@ class WindowStep:
         chain = self._chain_in_graph()
         with torch.cuda.stream(side):
             for _ in range(warmup):
-                self._clean_pass()
-                self._adv_chain(self._adv_pass)
+                with self._amp():
+                    self._clean_pass()
+                    self._adv_chain(self._adv_pass)
         torch.cuda.current_stream(tr.device).wait_stream(side)
         torch.cuda.synchronize(tr.device)
         if chain:   # capture must not leave the warm-up's FGM state behind: feature_projection was restored
@@ -279,25 +304,26 @@ class WindowStep:
             if ops.CAPTURE_TIMING is not None:   # bench.py: stamp the first launch sites of each graph
                 ops.CAPTURE_TIMING.new_graph()
             return torch.cuda.CUDAGraph()
-        g0 = new_graph()
-        with torch.cuda.graph(g0):
-            self._clean_pass()
-        gadv = []
-        if self.adv:
-            # the captured attack perturbs feature_projection in place: keep the real values to put back
-            fp_saved = [p.detach().clone() for p in self.fp_real]
-            for k in range(self.K):
-                g = new_graph()
-                with torch.cuda.graph(g):
-                    if chain:
-                        self._adv_step(k)
-                    else:
-                        self._adv_pass(k)
-                gadv.append(g)
-            with torch.no_grad():
-                for p, v in zip(self.fp_real, fp_saved):
-                    p.copy_(v)
-            tr.fgm.backup = {}
+        with self._amp():        # one cast cache for G0 and the adversarial graphs (see _amp)
+            g0 = new_graph()
+            with torch.cuda.graph(g0):
+                self._clean_pass()
+            gadv = []
+            if self.adv:
+                # the captured attack perturbs feature_projection in place: keep the real values to put back
+                fp_saved = [p.detach().clone() for p in self.fp_real]
+                for k in range(self.K):
+                    g = new_graph()
+                    with torch.cuda.graph(g):
+                        if chain:
+                            self._adv_step(k)
+                        else:
+                            self._adv_pass(k)
+                    gadv.append(g)
+                with torch.no_grad():
+                    for p, v in zip(self.fp_real, fp_saved):
+                        p.copy_(v)
+                tr.fgm.backup = {}
         torch.cuda.synchronize(tr.device)
         self._unbind()
         tr.grads.zero()
@@ -325,8 +351,9 @@ class WindowStep:
             else:
                 self._adv_chain(lambda k: gadv[k].replay())
         else:
-            self._clean_pass()
-            self._adv_chain(self._adv_pass)
+            with self._amp():
+                self._clean_pass()
+                self._adv_chain(self._adv_pass)
             self._unbind()
         tr.micro += self.K
         tr.n_seen += self.N
