@@ -125,7 +125,7 @@ def build(config, device, layerdrop):
     return model
 
 
-def roofline_from_rows(rows, steps, graphed=False):
+def roofline_from_rows(rows, steps, graphed=False, split=False):
     """The dominant hand-written kernel = largest total time over the timed region (every launch site
     counted: GraphTimer scales its sampled sites), with its achieved rate over its average launch."""
     if not rows:
@@ -155,9 +155,13 @@ def roofline_from_rows(rows, steps, graphed=False):
             "work_unit": "FLOP" if bound == "mfma" else "bytes",
             "launches_per_step": r["launches_per_step"], "ms_per_step": round(r["ms_per_step"], 4),
             "timing": ("device wall-clock stamps (rdx_timestamp_acc) captured around the first 2 launch sites of each "
-                       "kernel in each replayed HIP graph (each standing for the graph's same-shape sites of that "
-                       "kernel), accumulated over every replay of the timed region; HIP events on the launch "
-                       "stream for eager launches") if graphed else
+                       "kernel and shape in each replayed HIP graph (each standing for the graph's same-shape sites "
+                       "of that kernel), accumulated over every replay"
+                       + (" of a kernel-timing region of the same steps right after the timed region, replaying a "
+                          "second capture of the window with these stamps and the SincNet branch serialized on the "
+                          "main stream (the timed region replays unstamped graphs with the branch concurrent)"
+                          if split else " of the timed region")
+                       + "; HIP events on the launch stream for eager launches") if graphed else
                       "HIP events on the launch stream around every launch of the timed region"}
     return roof, rows
 
@@ -325,7 +329,7 @@ def main():
     import random as pyrandom
     pyrandom.seed(1234 + rank)
     B = args.micro_batch
-    graph, graph_timer, window = None, None, None
+    graph, graph_timer, window, window_t = None, None, None, None
     if not args.no_window:
         from radhip.window import WindowStep
         window = WindowStep(trainer, B, graphs=not args.eager)
@@ -334,15 +338,35 @@ def main():
     if not args.eager:
         hb.set("capturing HIP graphs")
         graph_timer = ops.GraphTimer(dev)
-        ops.CAPTURE_TIMING = graph_timer    # captured clock stamps around every radhip launch in the graphs
         if window is not None:
-            for k in range(args.accum):     # capture needs one staged window of draws
-                window.add(k, np.zeros(B, dtype=np.int64))
-            window.capture()
-            window.reset_host()
+            # the timed region replays unstamped graphs (SincNet stream as a concurrent branch); the kernel
+            # timings come from a second capture of the same window with captured clock stamps around the
+            # radhip launches and the branch serialized (as rocprofv3's kernel trace runs it), replayed over
+            # a kernel-timing region of the same number of steps after the timed one
+            def capture(w):
+                for k in range(args.accum):     # capture needs one staged window of draws
+                    w.add(k, np.zeros(B, dtype=np.int64))
+                w.capture()
+                w.reset_host()
+            capture(window)
+            window_t = WindowStep(trainer, B, graphs=True)
+            prev = os.environ.get("RADHIP_SINC_BRANCH")
+            os.environ["RADHIP_SINC_BRANCH"] = "0"
+            ops.CAPTURE_TIMING = graph_timer
+            try:
+                capture(window_t)
+            finally:
+                ops.CAPTURE_TIMING = None
+                if prev is None:
+                    os.environ.pop("RADHIP_SINC_BRANCH")
+                else:
+                    os.environ["RADHIP_SINC_BRANCH"] = prev
         else:
+            ops.CAPTURE_TIMING = graph_timer    # captured clock stamps around every radhip launch in the graph
             graph.capture()
-        ops.CAPTURE_TIMING = None
+            ops.CAPTURE_TIMING = None
+
+    cur = {"window": window}
 
     def micro(i, last):
         idx = np.random.randint(0, args.pool, size=B)
@@ -350,11 +374,12 @@ def main():
         lens = [L_RAW] * B
         plan = aug.draw(lens)
         lam, perm = trainer.mixup_draw(B)
-        if window is not None:
-            aug.run(pool_x, offs, lens, plan, perm, lam, out=window.xslot(i))
-            window.add(i, pool_y[idx].numpy(), lam, perm)
+        w = cur["window"]
+        if w is not None:
+            aug.run(pool_x, offs, lens, plan, perm, lam, out=w.xslot(i))
+            w.add(i, pool_y[idx].numpy(), lam, perm)
             if last:
-                window.run()
+                w.run()
         elif graph is not None:
             aug.run(pool_x, offs, lens, plan, perm, lam, out=graph.x)
             graph.run(pool_y[idx].numpy(), lam, perm, last_in_epoch=last)
@@ -374,7 +399,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     hb.set("timed steps")
-    ops.TIMING = {}
+    split = window_t is not None            # kernel timings from their own region (see the capture above)
+    ops.TIMING = None if split else {}
     if graph_timer is not None:
         graph_timer.reset()
     stream = torch.cuda.current_stream(dev)
@@ -400,6 +426,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    if split:
+        hb.set("kernel-timing steps")
+        cur["window"] = window_t
+        ops.TIMING = {}
+        graph_timer.reset()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        cur["window"] = window
     timing, ops.TIMING = ops.TIMING, None
     rows = ops.event_rows(timing)            # eager launches (augmentation, FGM)
     if graph_timer is not None:              # launches inside the replayed graphs
@@ -417,7 +452,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
     loss = trainer.epoch_loss()
-    roof, rows = roofline_from_rows(rows, args.steps, graphed=not args.eager)
+    roof, rows = roofline_from_rows(rows, args.steps, graphed=not args.eager, split=split)
     utts = ws * args.steps * args.accum * B
     value = utts / wall_max
     if rank == 0:

@@ -75,8 +75,10 @@ int rdx_sincconv_abspool1d_fwd(const float* x, int64_t batch, int64_t len, const
  *   u  [dirs, B, L, D]   u[0] causal, u[1] anti-causal (= flip(conv(flip(x)))) */
 int rdx_dwconv_bidir_fwd(int dtype, const void* x, int64_t ldx, const float* w, const float* bias,
                          void* u, int B, int L, int D, int K, int dirs, void* stream);
-/* Backward. du [dirs, B, L, D]; writes dx (row stride lddx, overwritten), and per-(batch)
- * partial weight / bias gradients dw_part [B, D, K], db_part [B, D] (fp32; caller sums dim 0). */
+/* Backward. du [dirs, B, L, D]; writes dx (row stride lddx, overwritten), and partial weight / bias
+ * gradients per (time chunk, batch): dw_part [P, D, K], db_part [P, D] with P = rdx_dwconv_bidir_bwd_parts(L)
+ * * B (fp32; caller sums dim 0). */
+int rdx_dwconv_bidir_bwd_parts(int L);
 int rdx_dwconv_bidir_bwd(int dtype, const void* x, int64_t ldx, const float* w, const float* bias,
                          const void* du, void* dx, int64_t lddx, float* dw_part, float* db_part,
                          int B, int L, int D, int K, int dirs, void* stream);

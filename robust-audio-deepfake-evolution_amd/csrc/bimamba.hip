@@ -57,10 +57,13 @@ __device__ __forceinline__ float dsilu_from_pre(float p) {
   return s * (1.0f + p * (1.0f - s));
 }
 
-// Backward: one thread per (b, d, time segment), register sliding windows, 4 segments per block.
+// Backward: one thread per (b, d, time segment), register sliding windows, 4 segments of a DWC_CHUNK-step
+// time chunk per block (grid (D/64, B, chunks): ~280 blocks at the Phase-6 shapes instead of 40 with whole-
+// sequence segments). Weight / bias gradients leave one fp32 partial per (chunk, b, d); the caller sums them.
 // K is fixed to mamba's d_conv = 4 so every window is a statically indexed register array.
 constexpr int DWC_K = 4;
 constexpr int DWC_SEG = 4;
+constexpr int DWC_CHUNK = 32;
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv_bwd_kernel(
     const T* __restrict__ x, int64_t ldx, const float* __restrict__ w, const float* __restrict__ bias,
@@ -71,8 +74,9 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(
   const int d = blockIdx.x * 64 + dl;
   const int b = blockIdx.y;
   const bool active = d < D;
-  const int seglen = (L + DWC_SEG - 1) / DWC_SEG;
-  const int s0 = min(L, seg * seglen), s1 = min(L, s0 + seglen);
+  const int c0 = blockIdx.z * DWC_CHUNK, c1 = min(L, c0 + DWC_CHUNK);
+  const int seglen = (DWC_CHUNK + DWC_SEG - 1) / DWC_SEG;
+  const int s0 = min(c1, c0 + seg * seglen), s1 = min(c1, s0 + seglen);
   constexpr int KM1 = DWC_K - 1;
   float wk[DWC_K], dwa[DWC_K], dba = 0.f;
 #pragma unroll
@@ -145,8 +149,9 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(
 #pragma unroll
     for (int k = 0; k <= DWC_K; ++k) {
       float s = red[0][dl][k] + red[1][dl][k] + red[2][dl][k] + red[3][dl][k];
-      if (k < DWC_K) dw_part[((int64_t)b * D + d) * DWC_K + k] = s;
-      else db_part[(int64_t)b * D + d] = s;
+      const int64_t pb = (int64_t)blockIdx.z * B + b;
+      if (k < DWC_K) dw_part[(pb * D + d) * DWC_K + k] = s;
+      else db_part[pb * D + d] = s;
     }
   }
 }
@@ -525,13 +530,15 @@ extern "C" int rdx_dwconv_bidir_bwd(int dtype, const void* x, int64_t ldx, const
   RDX_REQUIRE(x && w && bias && du && dx && dw_part && db_part && B > 0 && L > 0 && D > 0);
   RDX_REQUIRE(ldx >= D && lddx >= D && (dirs == 1 || dirs == 2));
   if (K != DWC_K) return RDX_EUNSUPPORTED;
-  dim3 grid((D + 63) / 64, B);
+  dim3 grid((D + 63) / 64, B, (L + DWC_CHUNK - 1) / DWC_CHUNK);
   DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(dwconv_bwd_kernel<T>, grid, dim3(256), 0, as_stream(stream),
                                            (const T*)x, ldx, w, bias, (const T*)du, (T*)dx, lddx, dw_part,
                                            db_part, B, L, D, dirs));
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
+
+extern "C" int rdx_dwconv_bidir_bwd_parts(int L) { return (L + DWC_CHUNK - 1) / DWC_CHUNK; }
 
 extern "C" int64_t rdx_scan_ckpt_elems(int B, int L, int D, int N, int dirs) {
   int nck = (L + SCAN_CK - 1) / SCAN_CK;

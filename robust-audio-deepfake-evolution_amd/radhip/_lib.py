@@ -63,6 +63,7 @@ SIGNATURES = {
     "rdx_sincconv_absmaxpool_fwd_devmask": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_vp, c_int, c_vp,
                                                     c_vp]),
     "rdx_dwconv_bidir_fwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_dwconv_bidir_bwd_parts": (c_int, [c_int]),
     "rdx_dwconv_bidir_bwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                      c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_scan_ckpt_elems": (c_i64, [c_int, c_int, c_int, c_int, c_int]),

@@ -226,8 +226,9 @@ class DWConvBidir(torch.autograd.Function):
         K = w.shape[1]
         du = du.contiguous().to(x.dtype)
         dx = torch.empty(B, L, D, device=x.device, dtype=x.dtype)
-        dw_part = torch.empty(B, D, K, device=x.device, dtype=torch.float32)
-        db_part = torch.empty(B, D, device=x.device, dtype=torch.float32)
+        parts = lib().rdx_dwconv_bidir_bwd_parts(L) * B
+        dw_part = torch.empty(parts, D, K, device=x.device, dtype=torch.float32)
+        db_part = torch.empty(parts, D, device=x.device, dtype=torch.float32)
         check(lib().rdx_dwconv_bidir_bwd(_dtype_code(x), _p(x), _rowview_ld(x), _p(w), _p(b), _p(du), _p(dx), D,
                                          _p(dw_part), _p(db_part), B, L, D, K, ctx.dirs, _stream(x)),
               "dwconv_bidir_bwd")
