@@ -401,6 +401,14 @@ int rdx_fe_ln_gelu(void* io, int64_t rows, const float* gamma, const float* beta
  * ------------------------------------------------------------------------------------------ */
 int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, const float* bn, int N, int H, int W, int ci,
                   int co, int kh, int ph, void* stream);
+/* conv2's input gradient continued through conv1's frozen BN + SELU backward (Residual_block.forward,
+ * src/models/DualStreamSEMamba.py:182-200; replaces rdx_sconv_fwd on dY followed by rdx_bnselu_bwd): the
+ * 32-channel blocks (ci = co = 32, kh = 2). dO1 = conv(dy, w) (w: conv2's flipped, transposed kernel
+ * [kh*3][co][ci]; ph = kh - 1 - conv2's row padding) stays on chip; dc = bf16(dO1) * selu'(u) * invstd*gamma
+ * with the saved pre-activation c [N, Ho, W, co]; sums[3][co] += d conv1.bias | d bn.weight | d bn.bias.
+ * bn = [cb | mean | invstd*gamma | beta | invstd] (5 x co fp32); sums zeroed by the caller. */
+int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void* c, void* dc, const float* bn, float* sums,
+                           int N, int H, int W, int ci, int co, int kh, int ph, void* stream);
 int rdx_sconv_wgrad_nblk(int N, int Ho, int W);
 int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* part, int N, int H, int W, int ci, int co,
                     int kh, int ph, void* stream);

@@ -59,7 +59,10 @@ struct SConvArgs {
   const __hip_bfloat16* w;  // [KH*3][CO][CI] (tap-major, prepared on the host)
   __hip_bfloat16* y;        // [N, Ho, W, CO]
   __hip_bfloat16* y2;       // optional: selu(bn(y + cb)) [N, Ho, W, CO]
-  const float* bn;          // [4][CO]: conv bias cb, running mean, invstd * gamma, beta (frozen BN)
+  const float* bn;          // [4][CO]: conv bias cb, running mean, invstd * gamma, beta (frozen BN); the
+                            //   backward epilogue reads a fifth row, invstd
+  const __hip_bfloat16* c;  // backward epilogue: the saved pre-activation [N, Ho, W, CO]
+  float* sums;              // backward epilogue: [3][CO] d conv_bias | d gamma | d beta (fp32 atomics)
   int N, H, W, Ho, ph;
   int rows_per;             // output rows per workgroup (grid.z chunks of the Ho rows)
 };
@@ -89,7 +92,11 @@ __device__ __forceinline__ void sc_store_row(char* slot, const uint4* regs) {
   }
 }
 
-template <int CI, int CO, int KH>
+// kBnBwd: the convolution is conv2's input gradient dO1 (the same kernel on dY with the flipped weights) and
+// the epilogue continues it through the frozen BN + SELU backward of bnselu_bwd_kernel (csrc/sincnet.hip) on the
+// bf16-rounded dO1, as the unfused path would: y = dc, and the per-channel sums of dc, dc/s * xhat, dc/s go
+// to a.sums, so dO1 never goes through HBM.
+template <int CI, int CO, int KH, bool kBnBwd = false>
 __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sc_lds[];
   constexpr int NSLOT = KH + 1, SLOT = SC_PW * CI * 2, XCH = CI / 8;
@@ -113,6 +120,18 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   constexpr int NT = CO / 32;
   const int pw = wv * 32 + r;  // this lane's position within the strip (B operand row)
   const int p = p0 + pw;
+  // kBnBwd: per-lane sums [sum][t][g][e] over the rows this workgroup walks (channel t*32 + 8g + 4h + e)
+  float bsum[kBnBwd ? 3 : 1][NT][4][4];
+  if constexpr (kBnBwd) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bsum[q][t][g][e] = 0.f;
+  }
   for (int ho = ho0; ho < ho1; ++ho) {
     const bool more = ho + 1 < ho1;
     if (more) sc_load_row<CI>(pre, a.x, n, ho - a.ph + KH, a.H, a.W, p0);
@@ -148,6 +167,27 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
+          if constexpr (kBnBwd) {
+            const uint2 cc = *reinterpret_cast<const uint2*>(a.c + obase + co);
+            const float cv[4] = {__uint_as_float(cc.x << 16), __uint_as_float(cc.x & 0xffff0000u),
+                                 __uint_as_float(cc.y << 16), __uint_as_float(cc.y & 0xffff0000u)};
+            float dz[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // the arithmetic of bnselu_bwd_kernel
+              const int ch = co + e;
+              const float zc = (cv[e] + a.bn[ch]) - a.bn[CO + ch];
+              const float xhat = zc * a.bn[4 * CO + ch];
+              const float u = fmaf(zc, a.bn[2 * CO + ch], a.bn[3 * CO + ch]);
+              const float sd = u > 0.f ? 1.0507009873554805f : 1.0507009873554805f * 1.6732632423543772f * __expf(u);
+              const float du = sc_bf16(v[e]) * sd;
+              dz[e] = du * a.bn[2 * CO + ch];
+              bsum[0][t][g][e] += dz[e];
+              bsum[1][t][g][e] = fmaf(du, xhat, bsum[1][t][g][e]);
+              bsum[2][t][g][e] += du;
+            }
+            *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(dz[0], dz[1]), sc_pack2(dz[2], dz[3]));
+            continue;
+          }
           *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]));
           if (a.y2) {
             float u[4];
@@ -162,6 +202,37 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
     }
     if (more) sc_store_row<CI>(xs + ((ho + KH) % NSLOT) * SLOT, pre);
     __syncthreads();
+  }
+  if constexpr (kBnBwd) {
+    // the 32 lanes of a half-wave hold the same channels: reduce them, then the four waves through LDS (the
+    // weight image is no longer needed), then one atomic per (sum, channel) per workgroup
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = bsum[q][t][g][e];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o, 64);
+            bsum[q][t][g][e] = x;
+          }
+    float* red = reinterpret_cast<float*>(sc_lds);  // [4 waves][3][CO]
+    if (r == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[(wv * 3 + q) * CO + t * 32 + 8 * g + 4 * h + e] = bsum[q][t][g][e];
+    }
+    __syncthreads();
+    for (int i = tid; i < 3 * CO; i += SC_T)
+      atomicAdd(&a.sums[i], (red[i] + red[3 * CO + i]) + (red[6 * CO + i] + red[9 * CO + i]));
   }
 }
 
@@ -351,7 +422,7 @@ __global__ void sconv_wgrad_reduce2_kernel(const float* __restrict__ part2, int6
   dw[i] = s;
 }
 
-template <int CI, int CO, int KH>
+template <int CI, int CO, int KH, bool kBnBwd = false>
 static int sconv_fwd_launch(const SConvArgs& a, hipStream_t st) {
   const size_t smem = (size_t)(KH + 1) * SC_PW * CI * 2 + (size_t)KH * 3 * CO * CI * 2;
   const int strips = (a.W + SC_P - 1) / SC_P;
@@ -362,7 +433,7 @@ static int sconv_fwd_launch(const SConvArgs& a, hipStream_t st) {
   SConvArgs b = a;
   b.rows_per = (a.Ho + nz - 1) / nz;
   dim3 grid((unsigned)strips, (unsigned)a.N, (unsigned)((a.Ho + b.rows_per - 1) / b.rows_per));
-  hipLaunchKernelGGL((sconv_fwd_kernel<CI, CO, KH>), grid, dim3(SC_T), smem, st, b);
+  hipLaunchKernelGGL((sconv_fwd_kernel<CI, CO, KH, kBnBwd>), grid, dim3(SC_T), smem, st, b);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -404,6 +475,8 @@ extern "C" int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, co
   a.y = (__hip_bfloat16*)y;
   a.y2 = (__hip_bfloat16*)y2;
   a.bn = bn;
+  a.c = nullptr;
+  a.sums = nullptr;
   a.N = N;
   a.H = H;
   a.W = W;
@@ -412,6 +485,34 @@ extern "C" int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, co
   RDX_REQUIRE(a.Ho > 0 && N <= 65535);
   hipStream_t st = as_stream(stream);
   SC_DISPATCH(sconv_fwd_launch, a, st)
+}
+
+// conv2's input gradient continued through conv1's frozen BN + SELU backward (Residual_block, the 32-channel
+// blocks): dO1 = conv(dy[N, H, W, ci], w) (w: the flipped, transposed kernel, tap-major [kh*3][co][ci]; ph:
+// kh - 1 - conv2's row padding), never stored; dc[N, Ho, W, co] = bf16(dO1) * selu'(u) * s with the saved
+// pre-activation c, and sums[3][co] += (sum dc, sum dc/s * xhat, sum dc/s) — exactly rdx_bnselu_bwd on the
+// unfused dO1. bn = [cb | mean | invstd*gamma | beta | invstd] (5 x co fp32); sums zeroed by the caller.
+extern "C" int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void* c, void* dc, const float* bn,
+                                      float* sums, int N, int H, int W, int ci, int co, int kh, int ph, void* stream) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  RDX_REQUIRE(dy && w && c && dc && bn && sums && N > 0 && H > 0 && W > 0 && ph >= 0 && ph <= kh);
+  RDX_REQUIRE(al(dy) && al(w) && al(c) && al(dc) && N <= 65535);
+  if (!(ci == 32 && co == 32 && kh == 2)) return RDX_EUNSUPPORTED;
+  SConvArgs a;
+  a.x = (const __hip_bfloat16*)dy;
+  a.w = (const __hip_bfloat16*)w;
+  a.y = (__hip_bfloat16*)dc;
+  a.y2 = nullptr;
+  a.bn = bn;
+  a.c = (const __hip_bfloat16*)c;
+  a.sums = sums;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.ph = ph;
+  a.Ho = H + 2 * ph - kh + 1;
+  RDX_REQUIRE(a.Ho > 0);
+  return sconv_fwd_launch<32, 32, 2, true>(a, as_stream(stream));
 }
 
 // row chunks of the weight-gradient units: about 4 rows each, at least 2048 units where the shape allows

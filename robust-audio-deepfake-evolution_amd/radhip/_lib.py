@@ -99,6 +99,8 @@ SIGNATURES = {
                                       c_vp, c_vp]),
     "rdx_fe_conv0": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_int, c_int, c_vp, c_vp]),
     "rdx_fe_ln_gelu": (c_int, [c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp]),
+    "rdx_sconv_dgrad_bnselu": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_vp]),
     "rdx_sconv_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_sconv_wgrad_nblk": (c_int, [c_int, c_int, c_int]),
     "rdx_sconv_wgrad": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),

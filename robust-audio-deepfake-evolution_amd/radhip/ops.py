@@ -626,11 +626,15 @@ class Block0Convs(torch.autograd.Function):
 SCONV_CH = (32, 64)
 
 
-def sconv_ok(x, weight):
-    """The shapes csrc/sconv.hip covers: bf16-autocast NHWC input, C_in and C_out in {32, 64}, kernel (1|2) x 3."""
+def sconv_weight_ok(weight):
+    """The kernels csrc/sconv.hip has: C_in and C_out in {32, 64}, kernel (1|2) x 3 (RADHIP_SCONV=0: none)."""
     co, ci, kh, kw = weight.shape
-    return (x.is_cuda and x.dim() == 4 and x.shape[1] == ci and ci in SCONV_CH and co in SCONV_CH and kh in (1, 2)
-            and kw == 3 and os.environ.get("RADHIP_SCONV", "1") != "0")
+    return ci in SCONV_CH and co in SCONV_CH and kh in (1, 2) and kw == 3 and os.environ.get("RADHIP_SCONV", "1") != "0"
+
+
+def sconv_ok(x, weight):
+    """The shapes csrc/sconv.hip covers: bf16-autocast NHWC input on the GPU and a sconv_weight_ok kernel."""
+    return x.is_cuda and x.dim() == 4 and x.shape[1] == weight.shape[1] and sconv_weight_ok(weight)
 
 
 # Per-window cache of the SincNet convolution weight layouts (radhip/window.py sets it to a dict for the span
@@ -743,6 +747,98 @@ class SConvBnSelu(torch.autograd.Function):
                                    _p(sums), N * H * W, C, _stream(c)), "bnselu_bwd")
         dx, dw = _sconv_backward(x, dc, wd, shape, ph, ctx.needs_input_grad[0])
         return dx, dw.to(wdt), None, sums[0], None, None, sums[1], sums[2]
+
+
+def _conv2_grad_to_c(da, out1, c, wd2, w2_shape, bn5, f32):
+    """From conv2's output gradient da back to conv1's pre-activation c: dc (bf16, c's shape), the frozen
+    BN / conv1-bias sums [3][C] (d conv_bias, d gamma, d beta) and dw2. The 32-channel blocks run conv2's input
+    gradient and the BN + SELU backward as ONE kernel (rdx_sconv_dgrad_bnselu: dO1 stays on chip); otherwise
+    the input gradient and rdx_bnselu_bwd run one after the other."""
+    co2, ci2, kh2, _ = w2_shape
+    N, C, Ho, W = c.shape
+    dc = torch.empty_like(c)
+    sums = torch.zeros(3, C, device=c.device, dtype=torch.float32)
+    if ci2 == 32 and co2 == 32 and kh2 == 2 and os.environ.get("RADHIP_FUSED_DGRAD_BN", "1") != "0":
+        H = da.shape[2]
+        nbytes = 2.0 * (N * H * W * co2 + 2 * N * Ho * W * C)
+        with _timed("sconv_dgrad_bnselu", da, nbytes, shape=(N, H, W)):
+            check(lib().rdx_sconv_dgrad_bnselu(_p(da), _p(wd2), _p(c), _p(dc), _p(bn5), _p(sums), N, H, W, co2, ci2,
+                                               kh2, kh2 - 1, _stream(da)), "sconv_dgrad_bnselu")
+    else:
+        do1 = _sconv_run(da, wd2, co2, ci2, kh2, kh2 - 1)
+        cb, mean, invstd, w, b = f32
+        check(lib().rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(do1), _p(cb), _p(mean), _p(invstd), _p(w), _p(b),
+                                   _p(dc), _p(sums), N * Ho * W, C, _stream(c)), "bnselu_bwd")
+    _, dw2 = _sconv_backward(out1, da, wd2, w2_shape, 0, False)
+    return dc, sums, dw2
+
+
+def _bn_rows(conv_bias, mean, invstd, gamma, beta):
+    f32 = [t.detach().contiguous().float() for t in (conv_bias, mean, invstd, gamma, beta)]
+    bn5 = torch.stack([f32[0], f32[1], f32[2] * f32[3], f32[4], f32[2]]).contiguous()
+    return f32, bn5
+
+
+class SConvBnSeluSConv(torch.autograd.Function):
+    """conv2(selu(frozen_bn(conv1(x) + conv1_bias))) of Residual_block (no conv2 bias: ResTail adds it):
+    conv1 with the BN + SELU epilogue and conv2 on csrc/sconv.hip; the backward goes from conv2's output
+    gradient to conv1's pre-activation in one pass where the channels allow (_conv2_grad_to_c)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, ph1, conv_bias, mean, invstd, gamma, beta, w2):
+        _require_gpu(x)
+        x = _nhwc(x.to(torch.bfloat16))
+        co, ci, kh, _ = w1.shape
+        wf1, wd1 = _sconv_w(w1)
+        wf2, wd2 = _sconv_w(w2)
+        f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
+        N, _, H, W = x.shape
+        out1 = torch.empty(N, co, H + 2 * ph1 - kh + 1, W, device=x.device, dtype=torch.bfloat16,
+                           memory_format=torch.channels_last)
+        c = _sconv_run(x, wf1, ci, co, kh, ph1, y2=out1, bn=bn5[:4])
+        co2, ci2, kh2, _ = w2.shape
+        a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
+        ctx.save_for_backward(x, wd1, c, out1, wd2, bn5, *f32)
+        ctx.meta = (tuple(w1.shape), ph1, w1.dtype, tuple(w2.shape), w2.dtype)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        x, wd1, c, out1, wd2, bn5, *f32 = ctx.saved_tensors
+        s1, ph1, w1dt, s2, w2dt = ctx.meta
+        da = _nhwc(da.to(torch.bfloat16))
+        dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
+        dx, dw1 = _sconv_backward(x, dc, wd1, s1, ph1, ctx.needs_input_grad[0])
+        return dx, dw1.to(w1dt), None, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt)
+
+
+class BnSeluSConv(torch.autograd.Function):
+    """conv2(selu(frozen_bn(c + conv1_bias))) for block 0, whose conv1 runs in Block0Convs: BnSelu's forward,
+    conv2 on csrc/sconv.hip, and the fused backward of _conv2_grad_to_c."""
+
+    @staticmethod
+    def forward(ctx, c, conv_bias, mean, invstd, gamma, beta, w2):
+        _require_gpu(c)
+        c = _nhwc(c.to(torch.bfloat16))
+        N, C, H, W = c.shape
+        f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
+        out1 = torch.empty_like(c)
+        check(lib().rdx_bnselu_fwd(_dtype_code(c), _p(c), *[_p(t) for t in f32], _p(out1), N * H * W, C, _stream(c)),
+              "bnselu_fwd")
+        wf2, wd2 = _sconv_w(w2)
+        co2, ci2, kh2, _ = w2.shape
+        a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
+        ctx.save_for_backward(c, out1, wd2, bn5, *f32)
+        ctx.meta = (tuple(w2.shape), w2.dtype)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        c, out1, wd2, bn5, *f32 = ctx.saved_tensors
+        s2, w2dt = ctx.meta
+        da = _nhwc(da.to(torch.bfloat16))
+        dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
+        return dc, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt)
 
 
 # ------------------------------------------------------------ WavLM positional convolution ----

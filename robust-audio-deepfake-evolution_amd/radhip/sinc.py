@@ -12,7 +12,8 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import Block0Convs, BnSelu, ResTail, SConv, SConvBnSelu, sconv_ok, sincconv_absmaxpool
+from .ops import (Block0Convs, BnSelu, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
+                  sconv_weight_ok, sincconv_absmaxpool)
 
 
 def _bf16_autocast(x):
@@ -123,22 +124,33 @@ class Residual_block(nn.Module):
             bn = self.bn2
             bf = _bf16_autocast(x)
             invstd = torch.rsqrt(bn.running_var + bn.eps)
-            idn = None
+            bnp = (self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
+            w2 = self.conv2.weight
+            # conv1 -> bn2 -> selu -> conv2 as one autograd op on csrc/sconv.hip (its backward reaches conv1's
+            # pre-activation in one pass for the 32-channel blocks)
+            pair = bf and sconv_weight_ok(w2) and os.environ.get("RADHIP_SCONV_PAIR", "1") != "0"
+            idn, a = None, None
             if (self.first and self.downsample and x.shape[1] == 1 and bf
                     and os.environ.get("RADHIP_FUSED_B0", "1") != "0"):
                 # one input channel: both convs' backward in one HIP pass (radhip.ops.Block0Convs)
                 c, idn = Block0Convs.apply(x, self.conv1.weight, self.conv_downsample.weight)
-                out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
+                if pair:
+                    a = BnSeluSConv.apply(c, *bnp, w2)
+                else:
+                    out = BnSelu.apply(c, *bnp)
             elif bf and sconv_ok(x, self.conv1.weight):
-                out = SConvBnSelu.apply(x, self.conv1.weight, 1, self.conv1.bias, bn.running_mean, invstd,
-                                        bn.weight, bn.bias)
+                if pair:
+                    a = SConvBnSeluSConv.apply(x, self.conv1.weight, 1, *bnp, w2)
+                else:
+                    out = SConvBnSelu.apply(x, self.conv1.weight, 1, *bnp)
             else:
                 c = F.conv2d(x, self.conv1.weight, None, self.conv1.stride, self.conv1.padding)
-                out = BnSelu.apply(c, self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
-            if bf and sconv_ok(out, self.conv2.weight):
-                a = SConv.apply(out, self.conv2.weight, 0)
-            else:
-                a = F.conv2d(out, self.conv2.weight, None, self.conv2.stride, self.conv2.padding)
+                out = BnSelu.apply(c, *bnp)
+            if a is None:
+                if bf and sconv_ok(out, w2):
+                    a = SConv.apply(out, w2, 0)
+                else:
+                    a = F.conv2d(out, w2, None, self.conv2.stride, self.conv2.padding)
             if self.downsample:
                 if idn is None and bf and sconv_ok(x, self.conv_downsample.weight):
                     idn = SConv.apply(x, self.conv_downsample.weight, 0)

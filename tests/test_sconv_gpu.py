@@ -75,3 +75,69 @@ def test_sconv_bn_selu_matches_conv_then_bnselu():
     (got.float() * dy).sum().backward()
     for g, r, nm in zip((cb.grad, gamma.grad, beta.grad), ref_grads, ("dcb", "dgamma", "dbeta")):
         _close(g, r, 2e-2, nm)
+
+
+def _bn_params(tag, co):
+    cb = _t(f"{tag}.cb", (co,), 0.1).requires_grad_(True)
+    mean = _t(f"{tag}.m", (co,), 0.1)
+    invstd = 1.0 / torch.sqrt(_t(f"{tag}.v", (co,), 0.1).abs() + 0.5)
+    gamma = (1 + _t(f"{tag}.g", (co,), 0.1)).requires_grad_(True)
+    beta = _t(f"{tag}.b", (co,), 0.1).requires_grad_(True)
+    return cb, mean, invstd, gamma, beta
+
+
+@pytest.mark.parametrize("ci,co,W", [(32, 32, 300), (32, 32, 7163), (32, 64, 257), (64, 64, 129)])
+def test_sconv_pair_matches_unfused_ops(ci, co, W):
+    """conv1 -> BN -> SELU -> conv2 as one op (SConvBnSeluSConv; its backward fuses conv2's input gradient with
+    the BN + SELU backward for 32 channels) against SConvBnSelu followed by SConv (separate kernels): the same
+    forward bits; gradients equal up to the summation order of the fp32 channel sums."""
+    from radhip.ops import SConv, SConvBnSelu, SConvBnSeluSConv
+    N, H = 2, 23
+    x = _t(f"sp.x{ci}{W}", (N, ci, H, W), 1.0).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w1 = _t(f"sp.w1{ci}{co}", (co, ci, 2, 3), 0.1)
+    w2 = _t(f"sp.w2{co}", (co, co, 2, 3), 0.1)
+    prm = _bn_params(f"sp{co}", co)
+    dy = _t(f"sp.dy{co}{W}", (N, co, H, W), 1.0)
+
+    def run(fused):
+        xs = x.clone().requires_grad_(True)
+        a1, a2 = w1.clone().requires_grad_(True), w2.clone().requires_grad_(True)
+        for t in (prm[0], prm[3], prm[4]):
+            t.grad = None
+        if fused:
+            out = SConvBnSeluSConv.apply(xs, a1, 1, *prm, a2)
+        else:
+            out = SConv.apply(SConvBnSelu.apply(xs, a1, 1, *prm), a2, 0)
+        (out.float() * dy).sum().backward()
+        return out, [xs.grad, a1.grad, a2.grad] + [prm[i].grad.clone() for i in (0, 3, 4)]
+
+    ref, rg = run(False)
+    got, gg = run(True)
+    assert torch.equal(got, ref)
+    for g, r, nm in zip(gg, rg, ("dx", "dw1", "dw2", "dcb", "dgamma", "dbeta")):
+        _close(g, r, 2e-3, nm)
+
+
+def test_bnselu_sconv_block0_matches_unfused():
+    from radhip.ops import BnSelu, BnSeluSConv, SConv
+    N, C, H, W = 2, 32, 24, 1000
+    c = _t("b0p.c", (N, C, H, W), 1.0).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w2 = _t("b0p.w2", (C, C, 2, 3), 0.1)
+    prm = _bn_params("b0p", C)
+    dy = _t("b0p.dy", (N, C, H - 1, W), 1.0)
+
+    def run(fused):
+        cs = c.clone().requires_grad_(True)
+        a2 = w2.clone().requires_grad_(True)
+        for t in (prm[0], prm[3], prm[4]):
+            t.grad = None
+        out = BnSeluSConv.apply(cs, *prm, a2) if fused else SConv.apply(BnSelu.apply(cs, *prm), a2, 0)
+        (out.float() * dy).sum().backward()
+        return out, [cs.grad, a2.grad] + [prm[i].grad.clone() for i in (0, 3, 4)]
+
+    ref, rg = run(False)
+    got, gg = run(True)
+    assert torch.equal(got, ref)
+    assert torch.equal(gg[0], rg[0])           # dc: the same arithmetic on the same bf16 dO1
+    for g, r, nm in zip(gg[1:], rg[1:], ("dw2", "dcb", "dgamma", "dbeta")):
+        _close(g, r, 2e-3, nm)
