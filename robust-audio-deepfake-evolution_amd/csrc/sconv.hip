@@ -106,9 +106,19 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n = blockIdx.y, p0 = blockIdx.x * SC_P;
   const int ho0 = blockIdx.z * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
-  for (int i = tid; i < KH * 3 * CO * XCH; i += SC_T) {
-    const int ch = i % XCH, rowc = i / XCH;  // rowc = tap * CO + co
-    *reinterpret_cast<uint4*>(ws + sc_off<CI>(rowc, ch)) = *reinterpret_cast<const uint4*>(a.w + (int64_t)rowc * CI + ch * 8);
+  {  // weights: every load issued before the first LDS store (one round trip, not one per chunk)
+    constexpr int NWV = (KH * 3 * CO * XCH + SC_T - 1) / SC_T;
+    uint4 wr[NWV];
+#pragma unroll
+    for (int j = 0; j < NWV; ++j) {
+      const int i = tid + SC_T * j;
+      if (i < KH * 3 * CO * XCH) wr[j] = *reinterpret_cast<const uint4*>(a.w + (int64_t)(i / XCH) * CI + (i % XCH) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < NWV; ++j) {
+      const int i = tid + SC_T * j;  // row i / XCH = tap * CO + co
+      if (i < KH * 3 * CO * XCH) *reinterpret_cast<uint4*>(ws + sc_off<CI>(i / XCH, i % XCH)) = wr[j];
+    }
   }
   uint4 pre[NV];
 #pragma unroll
@@ -426,10 +436,23 @@ template <int CI, int CO, int KH, bool kBnBwd = false>
 static int sconv_fwd_launch(const SConvArgs& a, hipStream_t st) {
   const size_t smem = (size_t)(KH + 1) * SC_PW * CI * 2 + (size_t)KH * 3 * CO * CI * 2;
   const int strips = (a.W + SC_P - 1) / SC_P;
-  // about 1024 workgroups for 256 CUs: split the rows when strips x N alone is small (each split restages
-  // the weights and KH - 1 halo rows)
-  const int want = (int)((1024 + (int64_t)strips * a.N - 1) / ((int64_t)strips * a.N));
-  const int nz = want < 1 ? 1 : (want > a.Ho ? a.Ho : want);
+  // one round of resident workgroups (256 CUs x the workgroups the LDS image allows per CU: 4 at 32 x 32
+  // channels, 1 at 64 x 64): split the rows when strips x N alone is fewer (each split restages the weights
+  // and KH - 1 halo rows), never more (a second round would restage for nothing)
+  const int per_cu = (int)((160 * 1024) / smem) < 1 ? 1 : ((int)((160 * 1024) / smem) > 4 ? 4 : (int)((160 * 1024) / smem));
+  const int64_t slots = 256 * (int64_t)per_cu, pairs = (int64_t)strips * a.N;
+  // the row split that minimises rounds x (rows per workgroup + the restaging, ~KH + 1 row-equivalents)
+  int nz = 1;
+  int64_t best = -1;
+  for (int z = 1; z <= a.Ho && z <= 64; ++z) {
+    const int rp = (a.Ho + z - 1) / z;
+    if (z > 1 && (a.Ho + rp - 1) / rp < z) continue;  // the same split as a smaller z
+    const int64_t cost = ((pairs * z + slots - 1) / slots) * (rp + KH + 1);
+    if (best < 0 || cost < best) {
+      best = cost;
+      nz = z;
+    }
+  }
   SConvArgs b = a;
   b.rows_per = (a.Ho + nz - 1) / nz;
   dim3 grid((unsigned)strips, (unsigned)a.N, (unsigned)((a.Ho + b.rows_per - 1) / b.rows_per));
@@ -554,7 +577,12 @@ extern "C" int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* 
   a.rows_per = (a.Ho + a.nz - 1) / a.nz;
   a.nz = (a.Ho + a.rows_per - 1) / a.rows_per;
   a.units = (int64_t)N * a.strips * a.nz;
-  const int nblk = sc_wgrad_blocks(N, a.Ho, W);
+  // one resident round of workgroups (the LDS image sets how many fit on a CU), each walking several units:
+  // fewer workgroups write fewer fp32 partials (kh*3*co*ci each: 96 KB at 64 x 64 channels) for the reduction
+  const int64_t smem = (2 * (int64_t)SC_P * co + (int64_t)(kh + 1) * SC_XR * ci) * 2;
+  const int per_cu = (int)((160 * 1024) / smem) < 1 ? 1 : ((int)((160 * 1024) / smem) > 4 ? 4 : (int)((160 * 1024) / smem));
+  const int cap = sc_wgrad_blocks(N, a.Ho, W);
+  const int nblk = cap < 256 * per_cu ? cap : 256 * per_cu;
   hipStream_t st = as_stream(stream);
   int rc = RDX_EUNSUPPORTED;
   if (ci == 32 && co == 32 && kh == 2) rc = sconv_wgrad_launch<32, 32, 2>(a, nblk, st);

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     dev = "cuda"
+    from radhip import ops
+    ops.SCONV_WCACHE = {}     # weight layouts prepared once per weight, as inside a training window
     rows = []
     for B in a.batch:
         for name, ci, co, kh, ph, H, W in SHAPES:
