@@ -202,8 +202,12 @@ class Model(nn.Module):
         stream forked from the current one (reference order: WavLM, then SincNet, :728-750), so inside a
         captured HIP graph it is a parallel branch: its kernels (and, because autograd runs each backward
         op on its forward op's stream, its backward) fill the CUs the latency-bound WavLM kernels leave idle.
-        No RNG is drawn inside either stream (the band mask is drawn on the host), so the order is free."""
+        The branch is taken only when no RNG is drawn inside the SincNet stream (band mask off, or staged in
+        device memory by the graphed trainers): an eager Freq_aug forward draws its mask in the stream, after
+        the WavLM stream's SpecAugment / LayerDrop draws, so it runs the streams in the reference order."""
         side = _side_stream(x)
+        if Freq_aug and self.sinc_stream.conv_time.mask_dev is None:
+            side = None
         if side is None:
             return self.wavlm_stream(x), self.sinc_stream(x, freq_aug=Freq_aug)
         cur = torch.cuda.current_stream(x.device)
