@@ -162,34 +162,61 @@ struct Ln1Args {
   int64_t M;
 };
 
-template <bool kLora>
-__global__ __launch_bounds__(256) void wl_ln1_fwd_kernel(Ln1Args a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= a.M) return;
-  const int e0 = lane * WL_VPL;
-  float v[WL_VPL], gm[WL_VPL], bt[WL_VPL];
-  load16(a.h + m * WL_E + e0, v);
-  float mean, rstd;
-  row_stats(v, a.eps, mean, rstd);
-  load16(a.gamma + e0, gm);
-  load16(a.beta + e0, bt);
-#pragma unroll
-  for (int i = 0; i < WL_VPL; ++i) v[i] = bf16_round((v[i] - mean) * rstd * gm[i] + bt[i]);
-  store16_bf(a.x1 + m * a.ldx + e0, v);
-  if (lane == 0) {
-    a.mean[m] = mean;
-    a.rstd[m] = rstd;
+// LoRA-A of both adapters staged once per workgroup of WL_LN1_ROWS row-waves: [2r][E] bf16 (the cast autocast
+// applies to lora_A's weight), 32 KB. A row-wave reading the fp32 A from L2 itself moved 64 KB per token row
+// and left these kernels L2-bound (26 us of the 47 us forward at B = 32).
+constexpr int WL_LN1_ROWS = 8;
+constexpr int WL_LN1_THREADS = WL_LN1_ROWS * RDX_WAVE;
+
+__device__ __forceinline__ void stage_lora_a(__hip_bfloat16* sA, const float* Aq, const float* Av) {
+  // WL_R2 * WL_E floats over WL_LN1_THREADS threads, 4 float4 per pass
+  constexpr int kN = WL_R2 * WL_E / 4;
+  for (int i = threadIdx.x; i < kN; i += WL_LN1_THREADS) {
+    const int k = (4 * i) / WL_E, e = (4 * i) % WL_E;
+    const float* src = k < WL_R2 / 2 ? Aq + (int64_t)k * WL_E + e : Av + (int64_t)(k - WL_R2 / 2) * WL_E + e;
+    const float4 t = *reinterpret_cast<const float4*>(src);
+    const uint32_t w0 = bf16_bits(t.x) | (bf16_bits(t.y) << 16), w1 = bf16_bits(t.z) | (bf16_bits(t.w) << 16);
+    *reinterpret_cast<uint2*>(sA + 4 * i) = make_uint2(w0, w1);
   }
-  float z[8];
-  gate_z(a.g, v, lane, z);
-  if ((lane & 3) == 0) {
-    const int head = lane >> 2;
-    float ga = sigmoidf_(z[0] + z[1] + z[2] + z[3]);
-    float gb = sigmoidf_(z[4] + z[5] + z[6] + z[7]);
-    a.gate[m * (WL_E / 64) + head] = ga * (gb * a.g.gconst[head] - 1.0f) + 2.0f;
+}
+// 16 consecutive bf16 of an LDS row as fp32
+__device__ __forceinline__ void lds16_bf(const __hip_bfloat16* p, float* v) { load16_bf(p, v); }
+
+template <bool kLora>
+__global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
+  __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[kLora ? WL_R2 * WL_E : 8];
+  if (kLora) stage_lora_a(sA, a.Aq, a.Av);
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * WL_LN1_ROWS + (threadIdx.x >> 6);
+  const bool live = m < a.M;  // no early return: the LoRA part follows a barrier
+  const int e0 = lane * WL_VPL;
+  float v[WL_VPL];
+  if (live) {
+    float gm[WL_VPL], bt[WL_VPL];
+    load16(a.h + m * WL_E + e0, v);
+    float mean, rstd;
+    row_stats(v, a.eps, mean, rstd);
+    load16(a.gamma + e0, gm);
+    load16(a.beta + e0, bt);
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i) v[i] = bf16_round((v[i] - mean) * rstd * gm[i] + bt[i]);
+    store16_bf(a.x1 + m * a.ldx + e0, v);
+    if (lane == 0) {
+      a.mean[m] = mean;
+      a.rstd[m] = rstd;
+    }
+    float z[8];
+    gate_z(a.g, v, lane, z);
+    if ((lane & 3) == 0) {
+      const int head = lane >> 2;
+      float ga = sigmoidf_(z[0] + z[1] + z[2] + z[3]);
+      float gb = sigmoidf_(z[4] + z[5] + z[6] + z[7]);
+      a.gate[m * (WL_E / 64) + head] = ga * (gb * a.g.gconst[head] - 1.0f) + 2.0f;
+    }
   }
   if (kLora) {
+    __syncthreads();
+    if (!live) return;
     const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
     const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
     float mq[WL_VPL], mv[WL_VPL];
@@ -203,14 +230,11 @@ __global__ __launch_bounds__(256) void wl_ln1_fwd_kernel(Ln1Args a) {
 #pragma unroll
     for (int k = 0; k < WL_R2; ++k) {
       const float* x = k < WL_R2 / 2 ? mq : mv;
-      const float* arow = k < WL_R2 / 2 ? a.Aq + (int64_t)k * WL_E : a.Av + (int64_t)(k - WL_R2 / 2) * WL_E;
-      const float4* w = reinterpret_cast<const float4*>(arow + e0);
+      float w[WL_VPL];
+      lds16_bf(sA + k * WL_E + e0, w);
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float4 t = w[i];
-        s += t.x * x[4 * i] + t.y * x[4 * i + 1] + t.z * x[4 * i + 2] + t.w * x[4 * i + 3];
-      }
+      for (int i = 0; i < WL_VPL; ++i) s = fmaf(w[i], x[i], s);
       acc[k] = s;
     }
     float tot = wave_sum16(acc, lane);
@@ -412,19 +436,27 @@ struct Ln1BwdArgs {
 };
 
 template <bool kLora>
-__global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
+__global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[kLora ? WL_R2 * WL_E : 8];
+  if (kLora) {
+    stage_lora_a(sA, a.Aq, a.Av);
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
-  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= a.M) return;
+  const int64_t m = (int64_t)blockIdx.x * WL_LN1_ROWS + (threadIdx.x >> 6);
+  if (m >= a.M) return;  // after the only barrier
   const int e0 = lane * WL_VPL;
   const int part = lane & 3, head = lane >> 2;
-  float x[WL_VPL], x1[WL_VPL], gm[WL_VPL], bt[WL_VPL], dx[WL_VPL];
+  float x[WL_VPL], x1[WL_VPL], dx[WL_VPL];
   load16(a.h + m * WL_E + e0, x);
-  load16(a.gamma + e0, gm);
-  load16(a.beta + e0, bt);
   const float mean = a.mean[m], rstd = a.rstd[m];
+  {
+    float gm[WL_VPL], bt[WL_VPL];
+    load16(a.gamma + e0, gm);
+    load16(a.beta + e0, bt);
 #pragma unroll
-  for (int i = 0; i < WL_VPL; ++i) x1[i] = bf16_round((x[i] - mean) * rstd * gm[i] + bt[i]);
+    for (int i = 0; i < WL_VPL; ++i) x1[i] = bf16_round((x[i] - mean) * rstd * gm[i] + bt[i]);
+  }
   load16_bf(a.dx1 + m * a.ldx + e0, dx);
   // gate: gate = ga (gb c - 1) + 2
   float z[8];
@@ -449,45 +481,41 @@ __global__ __launch_bounds__(256) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
   if (kLora) {
     const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
     const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
-    float sq_[WL_VPL], sv_[WL_VPL], xq[WL_VPL], xv[WL_VPL], bq[WL_VPL], bv[WL_VPL];
+    if (a.xd) {  // the dropped LN output of each adapter (optional; first, so that x1 dies here)
 #pragma unroll
-    for (int i = 0; i < WL_VPL; ++i) {
-      const uint64_t idx = (uint64_t)m * WL_E + e0 + i;
-      sq_[i] = drop_scale(a.dq, sq, idx);
-      sv_[i] = drop_scale(a.dv, sv, idx);
-      xq[i] = x1[i] * sq_[i];
-      xv[i] = x1[i] * sv_[i];
-      bq[i] = 0.f;
-      bv[i] = 0.f;
-    }
-    if (a.xd) {
-      store16_bf(a.xd + m * WL_E + e0, xq);
-      store16_bf(a.xd + (a.M + m) * WL_E + e0, xv);
-    }
-    // q and v adapters in separate loops unrolled by 2: a full unroll hoists all 16 A rows (256 floats)
-    // into registers and leaves this memory-bound kernel at one wave per SIMD
+      for (int which = 0; which < 2; ++which) {
+        const Drop& dd = which ? a.dv : a.dq;
+        const uint64_t sd = which ? sv : sq;
+        float xm[WL_VPL];
 #pragma unroll
-    for (int which = 0; which < 2; ++which) {
-      float* acc = which ? bv : bq;
-      const float* A = which ? a.Av : a.Aq;
-#pragma unroll 2
-      for (int k = 0; k < WL_R2 / 2; ++k) {
-        const float da = __bfloat162float(a.dx1[m * a.ldx + WL_E + which * (WL_R2 / 2) + k]);
-        const float4* w = reinterpret_cast<const float4*>(A + (int64_t)k * WL_E + e0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float4 t = w[i];
-          acc[4 * i] += t.x * da;
-          acc[4 * i + 1] += t.y * da;
-          acc[4 * i + 2] += t.z * da;
-          acc[4 * i + 3] += t.w * da;
-        }
+        for (int i = 0; i < WL_VPL; ++i) xm[i] = x1[i] * drop_scale(dd, sd, (uint64_t)m * WL_E + e0 + i);
+        store16_bf(a.xd + (which * a.M + m) * WL_E + e0, xm);
       }
     }
+    // the 2r down-projection gradients of this row: one 32-byte broadcast read
+    float da[WL_R2];
+    load16_bf(a.dx1 + m * a.ldx + WL_E, da);
 #pragma unroll
-    for (int i = 0; i < WL_VPL; ++i) dx[i] += bq[i] * sq_[i] + bv[i] * sv_[i];
+    for (int which = 0; which < 2; ++which) {
+      float acc[WL_VPL];
+#pragma unroll
+      for (int i = 0; i < WL_VPL; ++i) acc[i] = 0.f;
+#pragma unroll 1
+      for (int k = 0; k < WL_R2 / 2; ++k) {
+        float w[WL_VPL];
+        lds16_bf(sA + (which * (WL_R2 / 2) + k) * WL_E + e0, w);
+        const float d = da[which * (WL_R2 / 2) + k];
+#pragma unroll
+        for (int i = 0; i < WL_VPL; ++i) acc[i] = fmaf(w[i], d, acc[i]);
+      }
+      const Drop& dd = which ? a.dv : a.dq;
+      const uint64_t sd = which ? sv : sq;
+#pragma unroll
+      for (int i = 0; i < WL_VPL; ++i) dx[i] += acc[i] * drop_scale(dd, sd, (uint64_t)m * WL_E + e0 + i);
+    }
   }
-  float o[WL_VPL], r[WL_VPL];
+  float o[WL_VPL], r[WL_VPL], gm[WL_VPL];
+  load16(a.gamma + e0, gm);  // reloaded (L1): keeps it out of the registers live across the LoRA loop
   ln_bwd_row(dx, x, mean, rstd, gm, o);
   load16(a.dres + m * WL_E + e0, r);
 #pragma unroll
@@ -646,6 +674,7 @@ static Drop mk_drop(const int64_t* seed_dev, int salt, float p) {
 }
 
 static int blocks_rows(int64_t M) { return (int)((M + 3) / 4); }
+static int blocks_ln1(int64_t M) { return (int)((M + WL_LN1_ROWS - 1) / WL_LN1_ROWS); }
 
 extern "C" {
 
@@ -660,9 +689,9 @@ int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float 
   Ln1Args a{h, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
             mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M};
   if (lora)
-    hipLaunchKernelGGL(wl_ln1_fwd_kernel<true>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(wl_ln1_fwd_kernel<true>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   else
-    hipLaunchKernelGGL(wl_ln1_fwd_kernel<false>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(wl_ln1_fwd_kernel<false>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return 0;
 }
@@ -733,9 +762,9 @@ int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float
                GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
                dres, dh, reinterpret_cast<__hip_bfloat16*>(xd), M};
   if (lora)
-    hipLaunchKernelGGL(wl_ln1_bwd_kernel<true>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(wl_ln1_bwd_kernel<true>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   else
-    hipLaunchKernelGGL(wl_ln1_bwd_kernel<false>, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(wl_ln1_bwd_kernel<false>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return 0;
 }

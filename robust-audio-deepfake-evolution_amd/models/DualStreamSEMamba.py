@@ -131,7 +131,9 @@ class PN_BiMambas_Encoder(nn.Module):
 
     def forward(self, x):
         m = self.mamba.bidirectional(self.norm1(x))     # == mamba(n) + flip(mamba(flip(n)))
-        return self.feed_forward(self.norm2(m)) + x
+        # bf16 FFN output (autocast) + fp32 residual: cast first, then a same-dtype add (ROCm's mixed-dtype
+        # add kernel took ~42 us on these [B, 201, 144] tensors; the cast and the add take ~5 us each)
+        return x + self.feed_forward(self.norm2(m)).to(x.dtype)
 
 
 class SELayer(nn.Module):
