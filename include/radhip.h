@@ -241,6 +241,13 @@ int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax, void* dx,
  * [N, H, W, C] = d conv_downsample output (NHWC); w1 fp32 [C][2][3], wd fp32 [C][3]. Writes dx fp32 [N, H, W]
  * and per-block partial weight gradients part fp32 [nblk][C][9] (taps 0..5 = conv1 kh*3+kw, 6..8 =
  * conv_downsample kw; the caller sums dim 0), nblk = rdx_sincnet_b0_nblk(N*H*W). C != 32: RDX_EUNSUPPORTED. */
+/* SincNet block 0 forward (same block, C = 32): conv1 and conv_downsample of the bf16 input x [N, H, W] with the
+ * bf16-valued weights w1 fp32 [C][2][3], wd fp32 [C][3] (fp32 accumulation), and conv1's frozen BN + SELU:
+ * bn fp32 [4][C] = (conv1 bias, running mean, invstd * gamma, beta). Writes NHWC bf16 c [N, H+1, W, C] (conv1
+ * output without bias), y [N, H+1, W, C] = selu((c + bias - mean) * invstd * gamma + beta) and idn [N, H, W, C]
+ * (conv_downsample output without bias). C != 32: RDX_EUNSUPPORTED. */
+int rdx_sincnet_b0_fwd(const void* x, const float* w1, const float* wd, const float* bn, void* c, void* y, void* idn,
+                       int N, int H, int W, int C, void* stream);
 int rdx_sincnet_b0_nblk(int64_t npix);
 int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di, const float* w1, const float* wd, float* dx,
                        float* part, int N, int H, int W, int C, void* stream);

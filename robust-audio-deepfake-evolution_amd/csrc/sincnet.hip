@@ -433,6 +433,70 @@ extern "C" int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax
   return RDX_OK;
 }
 
+// SincNet block 0 forward (one input channel, 32 output channels): conv1 (2 x 3, padding (1, 1)) and
+// conv_downsample (1 x 3, padding (0, 1)) of the bf16 input with bf16-valued weights and fp32 accumulation (what
+// autocast runs), plus conv1's frozen BN + SELU on the bf16-rounded conv1 output (bnselu_fwd_kernel's
+// arithmetic). A workgroup covers 64 conv1 output pixels (n, h, w), lane = pixel; wave g computes channel group g
+// (8 channels), so its 104 weight / BN constants are wave-uniform (scalar loads) and each lane stores one 16-byte
+// chunk of each NHWC output row: c (pre-activation, kept for the backward), y = selu(bn(c + cb)) and, for h < H,
+// idn (the bottom row of conv1's 2 x 3 window is the downsample's window). The four waves of a workgroup fill
+// the same 64-byte rows, which meet in L2. Replaces two MIOpen convolutions (each with its own output-zeroing
+// pass) and the separate BN + SELU pass.
+constexpr int B0F_PIX = 64;
+__global__ __launch_bounds__(B0F_PIX * (B0_C / SN_VEC)) void b0_fwd_kernel(
+    const __hip_bfloat16* __restrict__ x, const float* __restrict__ w1, const float* __restrict__ wd,
+    const float* __restrict__ bn, __hip_bfloat16* __restrict__ c, __hip_bfloat16* __restrict__ y,
+    __hip_bfloat16* __restrict__ idn, int N, int H, int W) {
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // channel group of this wave
+  const int pix = blockIdx.x * B0F_PIX + (threadIdx.x & 63);       // < 2^31: checked by the launcher
+  const int per = (H + 1) * W;
+  if (pix >= N * per) return;
+  const int n = pix / per;
+  const int rem = pix - n * per;
+  const int h = rem / W, w = rem - h * W;
+  float v[2][3];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const int r = h - 1 + kh;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int cc = w - 1 + kw;
+      v[kh][kw] = (r >= 0 && r < H && cc >= 0 && cc < W) ? __bfloat162float(x[((int64_t)n * H + r) * W + cc]) : 0.f;
+    }
+  }
+  float cv[SN_VEC], yv[SN_VEC], iv[SN_VEC];
+#pragma unroll
+  for (int k = 0; k < SN_VEC; ++k) {
+    const int co = g * SN_VEC + k;
+    const float* t = w1 + co * 6;
+    float acc = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) acc = fmaf(v[kh][kw], t[kh * 3 + kw], acc);
+    cv[k] = __bfloat162float(__float2bfloat16(acc));
+    yv[k] = selu_f(fmaf((cv[k] + bn[co]) - bn[B0_C + co], bn[2 * B0_C + co], bn[3 * B0_C + co]));
+    const float* u = wd + co * 3;
+    iv[k] = fmaf(v[1][0], u[0], fmaf(v[1][1], u[1], v[1][2] * u[2]));
+  }
+  Vec8<__hip_bfloat16>::store(c + (int64_t)pix * B0_C + g * SN_VEC, cv);
+  Vec8<__hip_bfloat16>::store(y + (int64_t)pix * B0_C + g * SN_VEC, yv);
+  if (h < H) Vec8<__hip_bfloat16>::store(idn + (((int64_t)n * H + h) * W + w) * B0_C + g * SN_VEC, iv);
+}
+
+extern "C" int rdx_sincnet_b0_fwd(const void* x, const float* w1, const float* wd, const float* bn, void* c, void* y,
+                                  void* idn, int N, int H, int W, int C, void* stream) {
+  RDX_REQUIRE(x && w1 && wd && bn && c && y && idn && N > 0 && H > 0 && W > 0);
+  if (C != B0_C) return RDX_EUNSUPPORTED;
+  const int64_t npix = (int64_t)N * (H + 1) * W;
+  RDX_REQUIRE(npix < ((int64_t)1 << 31));
+  hipLaunchKernelGGL(b0_fwd_kernel, dim3((unsigned)((npix + B0F_PIX - 1) / B0F_PIX)), dim3(B0F_PIX * (B0_C / SN_VEC)), 0,
+                     as_stream(stream), (const __hip_bfloat16*)x, w1, wd, bn, (__hip_bfloat16*)c, (__hip_bfloat16*)y,
+                     (__hip_bfloat16*)idn, N, H, W);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
 extern "C" int rdx_sincnet_b0_nblk(int64_t npix) {
   // about one block per (utterance, 32-column strip) unit at the bench shapes; the kernel grid-strides over units
   const int64_t b = (npix + B0_STRIP - 1) / B0_STRIP;

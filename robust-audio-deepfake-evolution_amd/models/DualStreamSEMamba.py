@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
+from radhip.linear import SideLinear
 from radhip.mamba import Mamba
 from radhip.ops import layer_weighted_sum
 from radhip.sinc import CONV, Residual_block, SincNetEncoder  # noqa: F401  (re-exported like the reference)
@@ -127,7 +128,7 @@ class PN_BiMambas_Encoder(nn.Module):
         self.mamba = Mamba(d_model, n_state)
         self.norm1 = nn.LayerNorm(d_model)
         self.norm2 = nn.LayerNorm(d_model)
-        self.feed_forward = nn.Sequential(nn.Linear(d_model, d_model * 4), nn.GELU(), nn.Linear(d_model * 4, d_model))
+        self.feed_forward = nn.Sequential(SideLinear(d_model, d_model * 4), nn.GELU(), SideLinear(d_model * 4, d_model))
 
     def forward(self, x):
         m = self.mamba.bidirectional(self.norm1(x))     # == mamba(n) + flip(mamba(flip(n)))
@@ -142,8 +143,8 @@ class SELayer(nn.Module):
     def __init__(self, channel: int, reduction: int = 16):
         super().__init__()
         self.avg_pool = nn.AdaptiveAvgPool1d(1)
-        self.fc = nn.Sequential(nn.Linear(channel, channel // reduction, bias=False), nn.ReLU(inplace=True),
-                                nn.Linear(channel // reduction, channel, bias=False), nn.Sigmoid())
+        self.fc = nn.Sequential(SideLinear(channel, channel // reduction, bias=False), nn.ReLU(inplace=True),
+                                SideLinear(channel // reduction, channel, bias=False), nn.Sigmoid())
 
     def forward(self, x: Tensor) -> Tensor:
         b, t, c = x.size()
@@ -159,9 +160,9 @@ class DualStreamFusion(nn.Module):
         super().__init__()
         self.ln_wavlm = nn.LayerNorm(wavlm_dim)
         self.ln_sinc = nn.LayerNorm(sinc_dim)
-        self.wavlm_proj = nn.Linear(wavlm_dim, out_dim)
-        self.sinc_proj = nn.Linear(sinc_dim, out_dim)
-        self.fusion_proj = nn.Linear(out_dim * 2, out_dim)
+        self.wavlm_proj = SideLinear(wavlm_dim, out_dim)
+        self.sinc_proj = SideLinear(sinc_dim, out_dim)
+        self.fusion_proj = SideLinear(out_dim * 2, out_dim)
         self.se_layer = SELayer(out_dim, reduction=reduction)
         self.norm = nn.LayerNorm(out_dim)
         self.dropout = nn.Dropout(0.1)
@@ -195,9 +196,9 @@ class Model(nn.Module):
         self.backbone_layers = nn.ModuleList([PN_BiMambas_Encoder(d_model=emb_size, n_state=d_state)
                                               for _ in range(num_encoders)])
         self.norm_f = nn.LayerNorm(emb_size)
-        self.attention_pool = nn.Linear(emb_size, 1)
+        self.attention_pool = SideLinear(emb_size, 1)
         self.dropout = nn.Dropout(0.1)
-        self.classifier = nn.Linear(emb_size, 2)
+        self.classifier = SideLinear(emb_size, 2)
 
     def _streams(self, x, Freq_aug):
         """The two streams are independent until the fusion. On the GPU the SincNet stream runs on a side

@@ -1,0 +1,138 @@
+"""Linear layers of the detector head (fusion, PN-BiMamba, pooling, classifier) with their weight gradients
+accumulated in fp32 straight into .grad.
+
+Under autocast an nn.Linear's backward computes the input gradient, the bf16 weight gradient (a long-K GEMM
+with a tiny output: [144 x 576] over the 1608 / 6432 token rows), its fp32 cast, the bias reduction and its
+cast, and then the trainer adds both into the flat fp32 gradient buffer. Here the weight gradient is ONE GEMM
+with bf16 operands and an fp32 output accumulated in place (beta = 1, torch's addmm out_dtype form) and the
+bias gradient one fp32 reduction added in place: no bf16 rounding of the weight gradient, no casts, no separate
+accumulation (RADHIP_SIDE_LINEAR=1 puts these on a side stream joined at the end of the backward: a parallel
+branch of the captured graphs, measured 3 % slower per step than the main stream on ROCm 7; =0: F.linear).
+
+Same math as F.linear under autocast (src/models/DualStreamSEMamba.py:445-531,537-637,700-770): the input
+and weight are cast to the autocast dtype, y = x W^T + b. The direct accumulation needs .grad to exist (the
+trainers' FlatGrads buffers); without it the gradients are returned to autograd as usual.
+"""
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+_SIDE = {}
+_JOIN_QUEUED = [False]
+
+
+def _side(device):
+    d = device.index if device.index is not None else torch.cuda.current_device()
+    if d not in _SIDE:
+        _SIDE[d] = torch.cuda.Stream(device=d)
+    return _SIDE[d]
+
+
+def _join(device):
+    def cb():
+        _JOIN_QUEUED[0] = False
+        torch.cuda.current_stream(device).wait_stream(_side(device))
+    return cb
+
+
+def _cast(t, dt):
+    """t in dtype dt; fp32 parameters go through the window's weight-cast cache (radhip/window.py: the
+    clean pass casts, the window's adversarial passes reuse; the parameters do not change within a window)."""
+    if t is None or t.dtype == dt:
+        return t
+    cache = ops.SCONV_WCACHE
+    if cache is not None and isinstance(t, nn.Parameter):
+        hit = cache.get(("lin", id(t)))
+        if hit is not None and hit[0] is t:
+            return hit[1]
+        c = t.to(dt)
+        cache[("lin", id(t))] = (t, c)
+        return c
+    return t.to(dt)
+
+
+def direct_grad(p):
+    """True for parameters whose gradient SideLinear accumulates into .grad itself (window.py keeps their
+    .grad bound during a pass instead of handing it over through autograd)."""
+    return getattr(p, "_radhip_direct_grad", False)
+
+
+class SideLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, dt):
+        xc, wc, bc = x.to(dt), _cast(weight, dt), _cast(bias, dt)
+        y = F.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.x_dtype = x.dtype
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        weight, bias = ctx.params
+        dy = dy.to(wc.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(dy, wc).to(ctx.x_dtype)
+        need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = xc.reshape(-1, xc.shape[-1])
+        direct = (dy.is_cuda and need_w and weight.grad is not None and weight.grad.dtype == torch.float32
+                  and (not need_b or (bias.grad is not None and bias.grad.dtype == torch.float32)))
+        if not direct:
+            gw = torch.matmul(dy2.t(), x2).to(weight.dtype) if need_w else None
+            gb = dy2.sum(0, dtype=torch.float32).to(bias.dtype) if need_b else None
+            return dx, gw, gb, None
+        dev = dy.device
+        cur = torch.cuda.current_stream(dev)
+        side = _side(dev) if _MODE != "2" else cur
+        if side is not cur:
+            side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            if dy2.dtype == torch.float32:
+                weight.grad.addmm_(dy2.t(), x2)
+            else:
+                torch.ops.aten.addmm.dtype_out(weight.grad, dy2.t(), x2, torch.float32, beta=1, alpha=1,
+                                               out=weight.grad)
+            if need_b:
+                bias.grad.add_(dy2.sum(0, dtype=torch.float32))
+        if side is cur:
+            return dx, None, None, None
+        dy2.record_stream(side)
+        x2.record_stream(side)
+        if not _JOIN_QUEUED[0]:
+            _JOIN_QUEUED[0] = True
+            torch.autograd.Variable._execution_engine.queue_callback(_join(dev))
+        return dx, None, None, None
+
+
+_MODE = os.environ.get("RADHIP_SIDE_LINEAR", "2")   # "2": main stream; "1": side stream; "0": F.linear
+_ON = _MODE != "0"
+
+
+def side_linear(x, weight, bias=None):
+    """F.linear(x, weight, bias) with the weight / bias gradients on the side stream (CUDA, autocast on or
+    off); anything else is F.linear (and everything with RADHIP_SIDE_LINEAR=0)."""
+    if not (_ON and x.is_cuda and torch.is_grad_enabled() and (weight.requires_grad or (bias is not None and bias.requires_grad))):
+        return F.linear(x, weight, bias)
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+    with torch.autocast("cuda", enabled=False):
+        return SideLinearFn.apply(x, weight, bias, dt)
+
+
+class SideLinear(nn.Linear):
+    """nn.Linear (same parameters and state_dict keys) whose forward is side_linear."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        self.weight._radhip_direct_grad = True
+        if self.bias is not None:
+            self.bias._radhip_direct_grad = True
+
+    def forward(self, x):
+        return side_linear(x, self.weight, self.bias)

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .linear import SideLinear, side_linear
 from .ops import BiGate, DWConvBidir, SelectiveScan, SplitLast
 
 
@@ -34,11 +35,11 @@ class Mamba(nn.Module):
         self.expand = expand
         self.d_inner = int(expand * d_model)
         self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
-        self.in_proj = nn.Linear(d_model, self.d_inner * 2, bias=bias, **fk)
+        self.in_proj = SideLinear(d_model, self.d_inner * 2, bias=bias, **fk)
         self.conv1d = nn.Conv1d(self.d_inner, self.d_inner, bias=conv_bias, kernel_size=d_conv,
                                 groups=self.d_inner, padding=d_conv - 1, **fk)
-        self.x_proj = nn.Linear(self.d_inner, self.dt_rank + 2 * d_state, bias=False, **fk)
-        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner, bias=True, **fk)
+        self.x_proj = SideLinear(self.d_inner, self.dt_rank + 2 * d_state, bias=False, **fk)
+        self.dt_proj = SideLinear(self.dt_rank, self.d_inner, bias=True, **fk)
         # mamba_ssm initialisation of dt_proj (keeps softplus(bias) in [dt_min, dt_max])
         std = self.dt_rank ** -0.5 * dt_scale
         with torch.no_grad():
@@ -55,16 +56,16 @@ class Mamba(nn.Module):
         self.A_log._no_weight_decay = True
         self.D = nn.Parameter(torch.ones(self.d_inner, device=device))
         self.D._no_weight_decay = True
-        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias, **fk)
+        self.out_proj = SideLinear(self.d_inner, d_model, bias=bias, **fk)
 
     def _run(self, x, dirs):
         Di, R, N = self.d_inner, self.dt_rank, self.d_state
         xz = self.in_proj(x)                                    # [B, L, 2*Di]
         xi, z = SplitLast.apply(xz, Di, Di)                     # views; backward is one concatenation
         u = DWConvBidir.apply(xi, self.conv1d.weight, self.conv1d.bias, dirs)  # [dirs, B, L, Di]
-        x_dbl = F.linear(u, self.x_proj.weight)                 # [dirs, B, L, R + 2N]
+        x_dbl = side_linear(u, self.x_proj.weight)                # [dirs, B, L, R + 2N]
         dt, Bm, Cm = SplitLast.apply(x_dbl, R, N, N)
-        delta = F.linear(dt, self.dt_proj.weight)               # bias + softplus are fused in the scan
+        delta = side_linear(dt, self.dt_proj.weight)              # bias + softplus are fused in the scan
         y = SelectiveScan.apply(u, delta, self.A_log, Bm, Cm, self.D, self.dt_proj.bias)  # [dirs, B, L, Di] fp32
         g = BiGate.apply(y, z)                                  # (sum_dir y) * silu(z)
         return self.out_proj(g)

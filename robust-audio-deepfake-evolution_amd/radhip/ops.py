@@ -841,6 +841,56 @@ class BnSeluSConv(torch.autograd.Function):
         return dc, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt)
 
 
+class Block0Front(torch.autograd.Function):
+    """SincNet block 0 up to conv2 (Residual_block.forward, src/models/DualStreamSEMamba.py:182-200, one input
+    channel): c = conv1(x), idn = conv_downsample(x), out1 = selu(frozen_bn(c + conv1_bias)) in ONE HIP pass
+    (rdx_sincnet_b0_fwd), then a = conv2(out1) on csrc/sconv.hip. Backward: conv2's input gradient with the
+    BN + SELU backward (_conv2_grad_to_c), then both convolutions' backward in one pass (rdx_sincnet_b0_bwd).
+    Returns (a, idn); the biases of conv2 / conv_downsample are added by ResTail."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd, conv_bias, mean, invstd, gamma, beta, w2):
+        _require_gpu(x)
+        xb = x.to(torch.bfloat16).contiguous()                       # one channel: [N, H, W] in memory
+        N, _, H, W = xb.shape
+        C = w1.shape[0]
+        w1b = w1.detach().to(torch.bfloat16).float().reshape(C, 6).contiguous()   # autocast's bf16 weights
+        wdb = wd.detach().to(torch.bfloat16).float().reshape(C, 3).contiguous()
+        f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
+        c = torch.empty(N, C, H + 1, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        out1 = torch.empty_like(c)
+        idn = torch.empty(N, C, H, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        with _timed("sincnet_b0_fwd", x, 2.0 * (xb.numel() + 2 * c.numel() + idn.numel())):
+            check(lib().rdx_sincnet_b0_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(c), _p(out1), _p(idn), N, H, W, C,
+                                           _stream(x)), "sincnet_b0_fwd")
+        wf2, wd2 = _sconv_w(w2)
+        co2, ci2, kh2, _ = w2.shape
+        a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
+        ctx.save_for_backward(xb, w1b, wdb, c, out1, wd2, bn5, *f32)
+        ctx.meta = (tuple(w1.shape), tuple(wd.shape), x.dtype, tuple(w2.shape), w2.dtype)
+        return a, idn
+
+    @staticmethod
+    def backward(ctx, da, di):
+        xb, w1b, wdb, c, out1, wd2, bn5, *f32 = ctx.saved_tensors
+        w1_shape, wd_shape, x_dtype, s2, w2dt = ctx.meta
+        N, H, W = xb.shape[0], xb.shape[2], xb.shape[3]
+        C = w1_shape[0]
+        da = _nhwc(da.to(torch.bfloat16))
+        dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
+        di = _nhwc(di.to(torch.bfloat16)) if di is not None else torch.zeros(N, C, H, W, device=xb.device,
+                                                                             dtype=torch.bfloat16,
+                                                                             memory_format=torch.channels_last)
+        dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
+        part = torch.empty(lib().rdx_sincnet_b0_nblk(N * H * W), C * 9, device=xb.device, dtype=torch.float32)
+        with _timed("sincnet_b0_bwd", dc, 2 * (dc.numel() + di.numel()) + 4 * dx.numel() + 2 * xb.numel()):
+            check(lib().rdx_sincnet_b0_bwd(_p(xb), _p(dc), _p(di), _p(w1b), _p(wdb), _p(dx), _p(part), N, H, W, C,
+                                           _stream(dc)), "sincnet_b0_bwd")
+        dw = part.sum(0).view(C, 9)
+        return (dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape), sums[0], None, None, sums[1],
+                sums[2], dw2.to(w2dt))
+
+
 # ------------------------------------------------------------ WavLM positional convolution ----
 def posconv_weights(weight):
     """Conv weight [1024, 64, 128] (weight_norm applied) -> the two bf16 operand layouts of csrc/posconv.hip:

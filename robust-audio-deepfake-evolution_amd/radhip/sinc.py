@@ -12,7 +12,7 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import (Block0Convs, BnSelu, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
+from .ops import (Block0Convs, Block0Front, BnSelu, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
                   sconv_weight_ok, sincconv_absmaxpool)
 
 
@@ -132,12 +132,16 @@ class Residual_block(nn.Module):
             idn, a = None, None
             if (self.first and self.downsample and x.shape[1] == 1 and bf
                     and os.environ.get("RADHIP_FUSED_B0", "1") != "0"):
-                # one input channel: both convs' backward in one HIP pass (radhip.ops.Block0Convs)
-                c, idn = Block0Convs.apply(x, self.conv1.weight, self.conv_downsample.weight)
-                if pair:
-                    a = BnSeluSConv.apply(c, *bnp, w2)
+                # one input channel: both convolutions (and conv1's BN + SELU) in one HIP pass each way
+                # (radhip.ops.Block0Front; Block0Convs + BnSeluSConv with RADHIP_B0_FWD=0)
+                if pair and os.environ.get("RADHIP_B0_FWD", "1") != "0":
+                    a, idn = Block0Front.apply(x, self.conv1.weight, self.conv_downsample.weight, *bnp, w2)
                 else:
-                    out = BnSelu.apply(c, *bnp)
+                    c, idn = Block0Convs.apply(x, self.conv1.weight, self.conv_downsample.weight)
+                    if pair:
+                        a = BnSeluSConv.apply(c, *bnp, w2)
+                    else:
+                        out = BnSelu.apply(c, *bnp)
             elif bf and sconv_ok(x, self.conv1.weight):
                 if pair:
                     a = SConvBnSeluSConv.apply(x, self.conv1.weight, 1, *bnp, w2)

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import ops
+from .linear import direct_grad
 from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay
 from .wavlm import compute_time_mask
 
@@ -86,7 +87,7 @@ class WindowStep:
         # the fused WavLM layer accumulates into .grad itself): during a pass their .grad is unset, so
         # autograd hands each gradient over instead of launching one fp32 add per parameter into the flat
         # buffer; one multi-tensor add per pass then accumulates them (_pass_grads)
-        self.handed = [p for n, p in m.named_parameters() if p.requires_grad and "lora_" not in n]
+        self.handed = [p for n, p in m.named_parameters() if p.requires_grad and "lora_" not in n and not direct_grad(p)]
         self.ring = _PinnedRing(8192 + 2 * N * 8 + N * (T + nl + 16) + self.K * (self.B * T + nl + 64))
         self.graphs = None
         self._wcache = {}

@@ -453,6 +453,45 @@ def test_sincnet_block0_backward_kernel(N, H, W):
         assert ((got.float() - ref).norm() / ref.norm()).item() < 1e-3
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 23, 301), (3, 1, 34), (1, 4, 2)])
+def test_sincnet_block0_front(N, H, W):
+    """radhip.ops.Block0Front (rdx_sincnet_b0_fwd + conv2 on sconv.hip; backward _conv2_grad_to_c +
+    rdx_sincnet_b0_bwd) vs torch fp32 of the same bf16-rounded operands: conv1 / conv_downsample of the one-channel
+    input, frozen BN + SELU on the bf16 conv1 output, conv2 (2 x 3, padding (0, 1)). Outputs and the gradients of
+    x, the three conv weights, conv1's bias and the BN affine."""
+    from radhip.ops import Block0Front
+    torch.manual_seed(4)
+    x = torch.randn(N, 1, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    w1 = (0.3 * torch.randn(32, 1, 2, 3, device=DEV)).requires_grad_()
+    wd = (0.3 * torch.randn(32, 1, 1, 3, device=DEV)).requires_grad_()
+    w2 = (0.1 * torch.randn(32, 32, 2, 3, device=DEV)).requires_grad_()
+    cb = (0.1 * torch.randn(32, device=DEV)).requires_grad_()
+    mean, var = 0.1 * torch.randn(32, device=DEV), torch.rand(32, device=DEV) + 0.5
+    invstd = torch.rsqrt(var + 1e-5)
+    gamma = (torch.rand(32, device=DEV) + 0.5).requires_grad_()
+    beta = (0.1 * torch.randn(32, device=DEV)).requires_grad_()
+    a, idn = Block0Front.apply(x, w1, wd, cb, mean, invstd, gamma, beta, w2)
+    assert a.shape == (N, 32, H, W) and idn.shape == (N, 32, H, W)
+    ga = torch.randn(a.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gi = torch.randn(idn.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    torch.autograd.backward([a, idn], [ga, gi])
+    bf = lambda t: t.detach().to(torch.bfloat16).float().requires_grad_()  # noqa: E731
+    xr, w1r, wdr, w2r = bf(x), bf(w1), bf(wd), bf(w2)
+    cbr, gr, br = (t.detach().clone().requires_grad_() for t in (cb, gamma, beta))
+    cr = F.conv2d(xr, w1r, None, 1, (1, 1))
+    c16 = cr + (cr.to(torch.bfloat16).float() - cr).detach()        # the bf16-rounded conv1 output, identity grad
+    o1 = F.selu(((c16 + cbr[None, :, None, None]) - mean[None, :, None, None]) * invstd[None, :, None, None]
+                * gr[None, :, None, None] + br[None, :, None, None])
+    ar = F.conv2d(o1.to(torch.bfloat16).float(), w2r, None, 1, (0, 1))
+    ir = F.conv2d(xr, wdr, None, 1, (0, 1))
+    torch.autograd.backward([ar, ir], [ga.float(), gi.float()])
+    assert ((a.float() - ar).norm() / ar.norm()).item() < 1e-2
+    assert ((idn.float() - ir).norm() / ir.norm()).item() < 1e-2
+    for got, ref in ((x.grad, xr.grad), (w1.grad, w1r.grad), (wd.grad, wdr.grad), (w2.grad, w2r.grad),
+                     (cb.grad, cbr.grad), (gamma.grad, gr.grad), (beta.grad, br.grad)):
+        assert ((got.float() - ref).norm() / ref.norm()).item() < 2e-2
+
+
 def test_attention_rejects_non_toeplitz_bias():
     """The kernels take the bias as a relative-position table; a bias that is not a function of key - query
     is refused loudly rather than silently mis-read."""
