@@ -199,6 +199,15 @@ class Model(nn.Module):
         self.attention_pool = SideLinear(emb_size, 1)
         self.dropout = nn.Dropout(0.1)
         self.classifier = SideLinear(emb_size, 2)
+        # set by radhip/window.py for an adversarial pass: its SincNet output (a leaf), from one batched pass
+        self.sinc_given = None
+
+    @staticmethod
+    def sinc_side_stream(x):
+        """The stream the SincNet branch runs on (None: in order on the current stream). radhip/window.py puts
+        its batched adversarial SincNet pass on it too, so every SincNet launch of a window (and the per-window
+        weight layouts they share through radhip.ops.SCONV_WCACHE) is ordered on one stream."""
+        return _side_stream(x)
 
     def _streams(self, x, Freq_aug):
         """The two streams are independent until the fusion. On the GPU the SincNet stream runs on a side
@@ -208,6 +217,13 @@ class Model(nn.Module):
         The branch is taken only when no RNG is drawn inside the SincNet stream (band mask off, or staged in
         device memory by the graphed trainers): an eager Freq_aug forward draws its mask in the stream, after
         the WavLM stream's SpecAugment / LayerDrop draws, so it runs the streams in the reference order."""
+        if self.sinc_given is not None:      # radhip/window.py: this pass's SincNet output, computed batched
+            return self.wavlm_stream(x), self.sinc_given
+        if os.environ.get("RADHIP_PROBE_NO_SINC") == "1":   # timing probe only (tools): WavLM stream alone
+            T2 = (x.shape[-1] - self.sinc_stream.conv_time.kernel_size + 1) // 3
+            for _ in range(6):
+                T2 //= 3
+            return self.wavlm_stream(x), x.new_zeros(x.shape[0], T2, self.sinc_stream.out_dim)
         side = _side_stream(x)
         if Freq_aug and self.sinc_stream.conv_time.mask_dev is None:
             side = None

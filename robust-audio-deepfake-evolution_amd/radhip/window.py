@@ -10,10 +10,16 @@ tensors, so after the batched backward the copies hold g_1..g_K. The K ADVERSARI
 sequential, exactly as the reference orders them:
     for k: fp.grad += g_k; FGM.attack() (accumulated grad, incl. adversarial passes < k); adv pass k
            (B utterances, the clean pass's frozen-CNN features of group k); FGM.restore()
-then one optimizer step. Per-call random decisions (SincConv band mask, SpecAugment, LayerDrop,
+then one optimizer step. The SincNet stream does not depend on the FGM perturbation (it sees the same mixed
+input; only its band mask is drawn per pass), so the K adversarial passes' SincNet forwards run as ONE batched
+pass in the clean graph (each row with its pass's mask) and their backward as ONE batched pass after the last
+adversarial pass, from the output gradients the K passes leave in a [K*B, T', 64] buffer (the SincNet backward
+is linear in its output gradient at fixed activations; BN is frozen). Per-call random decisions (SincConv band mask, SpecAugment, LayerDrop,
 mixup) are drawn on the host in the reference's per-micro-batch order and staged into device
 buffers; the clean pass reads them per utterance row. With HIP graphs the window is 1 + K replays.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -64,9 +70,20 @@ class WindowStep:
         self.c_tmask = torch.zeros(N, T, dtype=torch.bool, device=dev)
         self.c_keep = torch.ones(N, nl, dtype=torch.bool, device=dev)
         self.a_mask = torch.zeros(self.K, 2, dtype=torch.int32, device=dev)
+        self.a_mask_rows = torch.zeros(N, 2, dtype=torch.int32, device=dev)   # a_mask[k] on micro-batch k's rows
         self.a_tmask = torch.zeros(self.K, self.B, T, dtype=torch.bool, device=dev)
         self.a_keep = torch.ones(self.K, nl, dtype=torch.bool, device=dev)
         self.adv = tr.fgm is not None
+        # batched adversarial SincNet passes (see the module docstring; RADHIP_SINC_BATCH=0: per pass)
+        self.sinc_batched = (self.adv and hasattr(m, "sinc_given") and hasattr(m, "sinc_stream")
+                             and os.environ.get("RADHIP_SINC_BATCH", "1") != "0")
+        self.f_adv = None
+        self.f_adv_leaf = None
+        self.dfa = None
+        # the model's SincNet stream: the clean pass's SincNet branch and this batched pass share the window's
+        # SincNet weight layouts (ops.SCONV_WCACHE), so they must be ordered on one stream
+        self._sinc_side = (m.sinc_side_stream(self.x) if self.sinc_batched and hasattr(m, "sinc_side_stream")
+                           else None)
         # feature_projection: the real tensors and K leaf copies whose grads live in one flat buffer
         fp = self.core.feature_projection
         self.fp_real = [fp.layer_norm.weight, fp.layer_norm.bias, fp.projection.weight, fp.projection.bias]
@@ -102,7 +119,8 @@ class WindowStep:
         self._host = dict(ya=np.zeros(N, np.int64), yb=np.zeros(N, np.int64), lam=np.ones(K, np.float32),
                           c_mask=np.zeros((N, 2), np.int32), c_tmask=np.zeros((N, T), bool),
                           c_keep=np.ones((N, nl), bool), a_mask=np.zeros((K, 2), np.int32),
-                          a_tmask=np.zeros((K, B, T), bool), a_keep=np.ones((K, nl), bool))
+                          a_tmask=np.zeros((K, B, T), bool), a_keep=np.ones((K, nl), bool),
+                          a_mask_rows=np.zeros((N, 2), np.int32))
         self._added = 0
 
     def _draw_pass(self):
@@ -139,13 +157,15 @@ class WindowStep:
         if self.adv:
             tm, keep, mk = self._draw_pass()
             h["a_tmask"][k], h["a_keep"][k], h["a_mask"][k] = tm, keep, mk
+            h["a_mask_rows"][sl] = mk[None, :]
         self._added += 1
 
     def _stage(self):
         h = self._host
         self.ring.stage([(h["ya"], self.ya), (h["yb"], self.yb), (h["lam"], self.lam), (h["c_mask"], self.c_mask),
                          (h["c_tmask"], self.c_tmask), (h["c_keep"], self.c_keep), (h["a_mask"], self.a_mask),
-                         (h["a_tmask"], self.a_tmask), (h["a_keep"], self.a_keep)])
+                         (h["a_tmask"], self.a_tmask), (h["a_keep"], self.a_keep),
+                         (h["a_mask_rows"], self.a_mask_rows)])
 
     # ------------------------------------------------------------------ passes ----------------
     def _amp(self):
@@ -200,8 +220,44 @@ class WindowStep:
         ops.SCONV_WCACHE = self._wcache
         self._pass_grads(self._clean_pass_body)
 
+    def _sinc_adv_forward(self):
+        """The K adversarial passes' SincNet forwards as one pass over the window's rows (row block k with
+        adversarial pass k's band mask). Leaves one [B, T', 64] leaf per pass whose .grad is a view of dfa."""
+        tr, B = self.tr, self.B
+        self.conv.mask_dev = self.a_mask_rows
+        side = self._sinc_side
+        if side is not None:       # a parallel branch of the clean pass (joined at its end, _sinc_join)
+            cur = torch.cuda.current_stream(self.x.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                f = tr.model.sinc_stream(self.x, freq_aug=tr.freq_aug)
+            f.record_stream(cur)
+        else:
+            f = tr.model.sinc_stream(self.x, freq_aug=tr.freq_aug)
+        if self.dfa is None or self.dfa.shape != f.shape or self.dfa.dtype != f.dtype:
+            self.dfa = torch.zeros_like(f)
+        else:
+            self.dfa.zero_()
+        self.f_adv = f
+        self.f_adv_leaf = []
+        for k in range(self.K):
+            leaf = f[k * B:(k + 1) * B].detach().requires_grad_()
+            leaf.grad = self.dfa[k * B:(k + 1) * B]
+            self.f_adv_leaf.append(leaf)
+
+    def _sinc_join(self):
+        if self.sinc_batched and self._sinc_side is not None:
+            torch.cuda.current_stream(self.x.device).wait_stream(self._sinc_side)
+
+    def _sinc_adv_backward(self):
+        """The batched SincNet backward of the K adversarial passes (after the last one)."""
+        f, self.f_adv = self.f_adv, None
+        torch.autograd.backward(f, self.dfa)
+
     def _clean_pass_body(self):
         tr, core, B = self.tr, self.core, self.B
+        if self.sinc_batched:
+            self._sinc_adv_forward()
         with torch.no_grad():
             torch._foreach_copy_(self._flat_copies, self._flat_real)
             self.fp_grad.zero_()
@@ -217,14 +273,20 @@ class WindowStep:
             tr.scaler.scale(loss).backward()
             tr.loss_sum.add_(loss.detach().double() * (tr.accum * B))
         finally:
+            self._sinc_join()
             core.fp_groups = None
             self.feats = core._cnn_feats[1] if core._cnn_feats is not None else None
             core.cnn_reuse = None
 
     def _adv_pass(self, k):
         ops.SCONV_WCACHE = self._wcache
+
+        def body():
+            self._adv_pass_body(k)
+            if self.sinc_batched and k == self.K - 1:
+                self._sinc_adv_backward()
         try:
-            self._pass_grads(lambda: self._adv_pass_body(k))
+            self._pass_grads(body)
         finally:
             ops.SCONV_WCACHE = None
 
@@ -235,6 +297,8 @@ class WindowStep:
         core.encoder.keep_dev = self.a_keep[k]
         if self.feats is not None:
             core.cnn_feats_given = self.feats[k * B:(k + 1) * B]
+        if self.sinc_batched:
+            tr.model.sinc_given = self.f_adv_leaf[k]
         try:
             with self._amp():
                 _, out = tr.model(self.x[k * B:(k + 1) * B], Freq_aug=tr.freq_aug)
@@ -242,6 +306,8 @@ class WindowStep:
             tr.scaler.scale(adv).backward()
         finally:
             core.cnn_feats_given = None
+            if self.sinc_batched:
+                tr.model.sinc_given = None
 
     def _unbind(self):
         ops.SCONV_WCACHE = None
