@@ -127,7 +127,8 @@ int rdx_bigate_bwd(int dtype, const void* dg, const void* z, int64_t ldz, const 
  * ------------------------------------------------------------------------------------------ */
 int rdx_layer_wsum_fwd(int dtype, int nl, const void* const* hs, const float* w, void* out,
                        int64_t n, void* stream);
-/* Backward: dhs[l] = softmax(w)_l * g (dtype, overwritten), dot_part [nblk, nl] fp32 partial
+/* Backward: dhs[l] = softmax(w)_l * g (dtype, overwritten; dhs[l] == NULL: not written, the consumer
+ * applies softmax(w)_l * g itself, e.g. rdx_wl_ln1_bwd's state gradient), dot_part [nblk, nl] fp32 partial
  * sums of <g, h_l>; nblk = rdx_layer_wsum_nblk(n). dw follows on the host side from the dots. */
 int rdx_layer_wsum_nblk(int64_t n);
 int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, const float* w, const void* g,
@@ -339,6 +340,23 @@ int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float
                    const float* gconst, const float* lora_aq, const float* lora_av, int r,
                    const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
                    void* stream);
+/* rdx_wl_res_ln1_fwd: rdx_wl_ln1_fwd of h = h2 + drop(delta) (the residual of the previous layer, computed here
+ *   and written to hout): one pass instead of rdx_wl_residual then rdx_wl_ln1_fwd. */
+int rdx_wl_res_ln1_fwd(const float* h2, const void* delta, int salt_res, float p_res, float* hout,
+                       const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
+                       const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                       int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean,
+                       float* rstd, int64_t M, int E, void* stream);
+/* rdx_wl_ln1_bwd_ex: rdx_wl_ln1_bwd plus (state_grad, state_weight non-null) dh += state_weight[0] * state_grad,
+ *   the gradient the layer input receives as a hidden state of the layer-weighted sum (see
+ *   rdx_layer_wsum_bwd's NULL dhs[l]), and (ddrop_prev non-null) ddrop_prev = drop(dh) bf16 with the previous
+ *   layer's hidden dropout (salt_prev, p_prev): that layer's rdx_wl_dropout_bwd, fused. */
+int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
+                      const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
+                      const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                      int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd,
+                      const float* state_grad, const float* state_weight, int salt_prev, float p_prev,
+                      void* ddrop_prev, int64_t M, int E, void* stream);
 int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx, const void* dx1, int64_t ldd,
                      const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, float scale, float* daq,
                      float* dbq, float* dav, float* dbv, int64_t M, int E, int r, void* stream);

@@ -107,13 +107,13 @@ __global__ __launch_bounds__(LWS_THREADS) void lws_bwd_kernel(PtrTable hs, MutPt
       Vec4<T>::load(h, v * 4, hv);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { dot = fmaf(gv[j], hv[j], dot); o[j] = p * gv[j]; }
-      Vec4<T>::store(dh, v * 4, o);
+      if (dh) Vec4<T>::store(dh, v * 4, o);
     }
     if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
       int64_t i = (n & ~(int64_t)3) + threadIdx.x;
       float gg = ld(g, i);
       dot = fmaf(gg, ld(h, i), dot);
-      st(dh, i, p * gg);
+      if (dh) st(dh, i, p * gg);
     }
     dot = wave_sum(dot);
     if (lane == 0) s_red[wid][l] = dot;
@@ -177,8 +177,8 @@ extern "C" int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, cons
   PtrTable t{};
   MutPtrTable dt{};
   for (int l = 0; l < nl; ++l) {
-    RDX_REQUIRE(hs[l] != nullptr && dhs[l] != nullptr);
-    if (!aligned16(hs[l]) || !aligned16(dhs[l])) return RDX_EUNSUPPORTED;
+    RDX_REQUIRE(hs[l] != nullptr);   // dhs[l] == nullptr: that state's gradient p_l * g is not written
+    if (!aligned16(hs[l]) || (dhs[l] && !aligned16(dhs[l]))) return RDX_EUNSUPPORTED;
     t.p[l] = hs[l];
     dt.p[l] = dhs[l];
   }

@@ -160,6 +160,12 @@ struct Ln1Args {
   float* mean;
   float* rstd;
   int64_t M;
+  // optional residual prologue (the previous layer's last step): h = h2 + drop(delta) is computed here and
+  // written to hout (h is then unused)
+  const float* h2;
+  const __hip_bfloat16* delta;
+  Drop dres;
+  float* hout;
 };
 
 // LoRA-A of both adapters staged once per workgroup of WL_LN1_ROWS row-waves: [2r][E] bf16 (the cast autocast
@@ -193,7 +199,18 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
   float v[WL_VPL];
   if (live) {
     float gm[WL_VPL], bt[WL_VPL];
-    load16(a.h + m * WL_E + e0, v);
+    if (a.h2) {
+      float dl[WL_VPL];
+      load16(a.h2 + m * WL_E + e0, v);
+      load16_bf(a.delta + m * WL_E + e0, dl);
+      const uint64_t sr = a.dres.thr ? attn_seed(a.dres.seed_dev, a.dres.salt) : 0;
+#pragma unroll
+      for (int i = 0; i < WL_VPL; ++i)
+        v[i] += dl[i] * (a.dres.thr ? drop_scale(a.dres, sr, (uint64_t)m * WL_E + e0 + i) : 1.0f);
+      store16(a.hout + m * WL_E + e0, v);
+    } else {
+      load16(a.h + m * WL_E + e0, v);
+    }
     float mean, rstd;
     row_stats(v, a.eps, mean, rstd);
     load16(a.gamma + e0, gm);
@@ -433,6 +450,13 @@ struct Ln1BwdArgs {
   float* dh;
   __hip_bfloat16* xd;  // [2, M, E] or null
   int64_t M;
+  // optional: the gradient this layer's INPUT receives as a hidden state of the layer-weighted sum,
+  // sw[0] * sg (sw a device scalar: softmax(w)_l), added into dh
+  const float* sg;
+  const float* sw;
+  // optional: ddrop = drop_prev(dh) bf16, the gradient of the previous layer's dropped FFN output
+  Drop dprev;
+  __hip_bfloat16* ddrop;
 };
 
 template <bool kLora>
@@ -520,7 +544,20 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a
   load16(a.dres + m * WL_E + e0, r);
 #pragma unroll
   for (int i = 0; i < WL_VPL; ++i) o[i] += r[i];
+  if (a.sg) {
+    const float pw = a.sw[0];
+    load16(a.sg + m * WL_E + e0, r);
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i) o[i] = fmaf(pw, r[i], o[i]);
+  }
   store16(a.dh + m * WL_E + e0, o);
+  if (a.ddrop) {
+    const uint64_t sp = a.dprev.thr ? attn_seed(a.dprev.seed_dev, a.dprev.salt) : 0;
+#pragma unroll
+    for (int i = 0; i < WL_VPL; ++i)
+      o[i] *= a.dprev.thr ? drop_scale(a.dprev, sp, (uint64_t)m * WL_E + e0 + i) : 1.0f;
+    store16_bf(a.ddrop + m * WL_E + e0, o);
+  }
 }
 
 // LoRA weight gradients of one layer, ACCUMULATED into the fp32 .grad buffers:
@@ -676,6 +713,17 @@ static Drop mk_drop(const int64_t* seed_dev, int salt, float p) {
 static int blocks_rows(int64_t M) { return (int)((M + 3) / 4); }
 static int blocks_ln1(int64_t M) { return (int)((M + WL_LN1_ROWS - 1) / WL_LN1_ROWS); }
 
+static int ln1_fwd_launch(const Ln1Args& a, bool lora, void* stream) {
+  const int64_t M = a.M;
+  if (lora)
+    hipLaunchKernelGGL(wl_ln1_fwd_kernel<true>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(wl_ln1_fwd_kernel<false>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
+  RDX_LAUNCH_CHECK();
+  return 0;
+}
+
+
 extern "C" {
 
 int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
@@ -687,13 +735,24 @@ int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float 
   RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
   RDX_REQUIRE(ldx % 8 == 0);
   Ln1Args a{h, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
-            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M};
-  if (lora)
-    hipLaunchKernelGGL(wl_ln1_fwd_kernel<true>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
-  else
-    hipLaunchKernelGGL(wl_ln1_fwd_kernel<false>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
-  RDX_LAUNCH_CHECK();
-  return 0;
+            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M,
+            nullptr, nullptr, mk_drop(nullptr, 0, 0.f), nullptr};
+  return ln1_fwd_launch(a, lora, stream);
+}
+
+int rdx_wl_res_ln1_fwd(const float* h2, const void* delta, int salt_res, float p_res, float* hout,
+                       const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
+                       const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                       int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean,
+                       float* rstd, int64_t M, int E, void* stream) {
+  RDX_REQUIRE(h2 && delta && hout && gamma && beta && wg && bg && gconst && x1 && gate && mean && rstd && M > 0);
+  const bool lora = lora_aq != nullptr;
+  RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
+  RDX_REQUIRE(ldx % 8 == 0);
+  Ln1Args a{nullptr, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
+            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M,
+            h2, reinterpret_cast<const __hip_bfloat16*>(delta), mk_drop(seed_dev, salt_res, p_res), hout};
+  return ln1_fwd_launch(a, lora, stream);
 }
 
 int rdx_wl_add_ln_fwd(const float* h, const void* delta, const int64_t* seed_dev, int salt, float p, float* h2,
@@ -750,23 +809,35 @@ int rdx_wl_ln_bwd(const void* dx, int64_t ldd, const float* h, const float* mean
   return 0;
 }
 
-int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
-                   const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
-                   const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
-                   int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
-                   void* stream) {
+int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
+                      const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
+                      const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                      int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd,
+                      const float* state_grad, const float* state_weight, int salt_prev, float p_prev,
+                      void* ddrop_prev, int64_t M, int E, void* stream) {
   RDX_REQUIRE(dx1 && dgate && h && mean && rstd && gamma && beta && wg && bg && gconst && dres && dh && M > 0);
+  RDX_REQUIRE((state_grad == nullptr) == (state_weight == nullptr));
   const bool lora = lora_aq != nullptr;
   RDX_REQUIRE(E == WL_E && ldx % 8 == 0 && (!lora || (2 * r == WL_R2 && lora_av && ldx >= E + 2 * r)));
   Ln1BwdArgs a{reinterpret_cast<const __hip_bfloat16*>(dx1), ldx, dgate, h, mean, rstd, gamma, beta,
                GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
-               dres, dh, reinterpret_cast<__hip_bfloat16*>(xd), M};
+               dres, dh, reinterpret_cast<__hip_bfloat16*>(xd), M, state_grad, state_weight,
+               mk_drop(seed_dev, salt_prev, p_prev), reinterpret_cast<__hip_bfloat16*>(ddrop_prev)};
   if (lora)
     hipLaunchKernelGGL(wl_ln1_bwd_kernel<true>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   else
     hipLaunchKernelGGL(wl_ln1_bwd_kernel<false>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return 0;
+}
+
+int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
+                   const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                   int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
+                   void* stream) {
+  return rdx_wl_ln1_bwd_ex(dx1, ldx, dgate, h, mean, rstd, gamma, beta, wg, bg, gconst, lora_aq, lora_av, r, seed_dev,
+                           salt_q, salt_v, p_lora, dres, dh, xd, nullptr, nullptr, 0, 0.f, nullptr, M, E, stream);
 }
 
 int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx, const void* dx1, int64_t ldd,

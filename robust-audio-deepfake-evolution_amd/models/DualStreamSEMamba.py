@@ -115,8 +115,10 @@ class WavLMFrontend(nn.Module):
     def forward(self, x, layerdrop=None):
         if x.ndim == 3:
             x = x.squeeze(-1)
-        _, states = self._core()(x.float(), layerdrop=layerdrop)
-        return layer_weighted_sum(states, self.layer_weights)
+        core = self._core()
+        _, states = core(x.float(), layerdrop=layerdrop)
+        # fused encoder layers take their hidden-state gradients from the sum's backward (radhip/wavlm_fused.py)
+        return layer_weighted_sum(states, self.layer_weights, deferred=getattr(core.encoder, "state_defer", None))
 
 
 class PN_BiMambas_Encoder(nn.Module):

@@ -130,6 +130,10 @@ SIGNATURES = {
                       c_i64, c_int, c_vp]),
     "rdx_wl_ln1_bwd": (c_int, [c_vp, c_i64] + [c_vp] * 11 + [c_int, c_vp, c_int,
                        c_int, c_f32, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "rdx_wl_ln1_bwd_ex": (c_int, [c_vp, c_i64] + [c_vp] * 11 + [c_int, c_vp, c_int, c_int, c_f32] + [c_vp] * 3
+                          + [c_vp, c_vp, c_int, c_f32, c_vp, c_i64, c_int, c_vp]),
+    "rdx_wl_res_ln1_fwd": (c_int, [c_vp, c_vp, c_int, c_f32, c_vp, c_vp, c_vp, c_f32] + [c_vp] * 5
+                           + [c_int, c_vp, c_int, c_int, c_f32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
     "rdx_wl_lora_grad": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_f32, c_f32,
                                  c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_wl_lora_pack": (c_int, [c_int, c_vp, c_vp, c_vp, c_i64, c_int,

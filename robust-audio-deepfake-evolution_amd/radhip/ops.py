@@ -323,10 +323,15 @@ class BiGate(torch.autograd.Function):
 
 # ------------------------------------------------------------------- layer-weighted sum ------
 class LayerWeightedSum(torch.autograd.Function):
-    """sum_l softmax(w)_l * h_l over the WavLM hidden states, without stacking them."""
+    """sum_l softmax(w)_l * h_l over the WavLM hidden states, without stacking them.
+
+    `deferred` (radhip.wavlm_fused.EncoderChain, or None): states whose gradient softmax(w)_l * g the backward
+    does NOT write; it leaves g and softmax(w) on the object instead, and the fused layer that takes that state
+    as its input adds the term inside its LN1 backward (rdx_wl_ln1_bwd_ex), so no [M, E] gradient is written
+    and no autograd add runs per layer."""
 
     @staticmethod
-    def forward(ctx, w, *hs):
+    def forward(ctx, w, deferred, *hs):
         _require_gpu(w, *hs)
         h0 = hs[0]
         dt = h0.dtype
@@ -337,28 +342,34 @@ class LayerWeightedSum(torch.autograd.Function):
             check(lib().rdx_layer_wsum_fwd(_dtype_code(h0), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
                                            _p(out), out.numel(), _stream(out)), "layer_wsum_fwd")
         ctx.save_for_backward(wf, *hs)
+        ctx.deferred = deferred
         return out
 
     @staticmethod
     def backward(ctx, g):
         wf, *hs = ctx.saved_tensors
+        dfr = ctx.deferred
+        skip = dfr.indices if dfr is not None and g.dtype == torch.float32 and hs[0].dtype == torch.float32 else ()
         g = g.contiguous().to(hs[0].dtype)
-        dhs = [torch.empty_like(h) for h in hs]
+        dhs = [None if l in skip else torch.empty_like(h) for l, h in enumerate(hs)]
         n = g.numel()
         nblk = lib().rdx_layer_wsum_nblk(n)
         dots = torch.empty(nblk, len(hs), device=g.device, dtype=torch.float32)
-        with _timed("layer_wsum_bwd", g, (2 * len(hs) + 1) * n * g.element_size()):
+        nwrite = sum(d is not None for d in dhs)
+        with _timed("layer_wsum_bwd", g, (len(hs) + nwrite + 1) * n * g.element_size()):
             check(lib().rdx_layer_wsum_bwd(_dtype_code(g), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
-                                           _p(g), ptr_array([d.data_ptr() for d in dhs]), _p(dots), n, _stream(g)),
-                  "layer_wsum_bwd")
+                                           _p(g), ptr_array([d.data_ptr() if d is not None else 0 for d in dhs]),
+                                           _p(dots), n, _stream(g)), "layer_wsum_bwd")
         dots = dots.sum(0)
         p = torch.softmax(wf, 0)
+        if skip:
+            dfr.g, dfr.p = g, p.contiguous()
         dw = p * (dots - (p * dots).sum())
-        return (dw, *dhs)
+        return (dw, None, *dhs)
 
 
-def layer_weighted_sum(hidden_states, layer_weights):
-    return LayerWeightedSum.apply(layer_weights, *hidden_states)
+def layer_weighted_sum(hidden_states, layer_weights, deferred=None):
+    return LayerWeightedSum.apply(layer_weights, deferred, *hidden_states)
 
 
 class SplitLast(torch.autograd.Function):

@@ -426,10 +426,14 @@ class Encoder(nn.Module):
             loras = runner.prepare(h.device)
             pb = runner.position_bias(h.shape[1], h.device)
             h = h.float()
+        # fused layers that always run back to back (no LayerDrop skip / select) chain their residuals and
+        # gradients through each other (wavlm_fused.EncoderChain); the frontend's layer-weighted sum reads it
+        chain = wavlm_fused.EncoderChain(len(self.layers)) if fused and (p == 0 or not self.training) else None
+        self.state_defer = chain
 
         def run(i, layer, h, pos):
             if fused:
-                return runner.layer(i, h, pb, loras, seed), None
+                return runner.layer(i, h, pb, loras, seed, chain), None
             return layer(h, pos)
         for i, layer in enumerate(self.layers):
             states.append(h)

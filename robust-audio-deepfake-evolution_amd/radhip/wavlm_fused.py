@@ -119,12 +119,31 @@ class _LayerCache:
         self.key = key
 
 
+class EncoderChain:
+    """Per-forward state of a fused encoder whose layers run back to back (no LayerDrop selection between them):
+      * layer i leaves its residual h_{i+1} = h2 + drop(fo) to layer i+1's LN1 forward (rdx_wl_res_ln1_fwd),
+        which computes it into layer i's (returned) output tensor: one pass instead of two;
+      * the layer-weighted sum's backward does not write the gradients of states 0..n-1 (the layers' inputs);
+        it leaves g and softmax(w) here and layer i's LN1 backward adds softmax(w)_i * g (rdx_wl_ln1_bwd_ex):
+        no [M, E] gradient per layer and no autograd add;
+      * layer i+1's LN1 backward also writes layer i's dropped FFN-output gradient drop_i(dh), which layer i's
+        backward then takes instead of running its dropout backward."""
+
+    def __init__(self, n):
+        self.n = n
+        self.indices = frozenset(range(n))
+        self.pending_res = None
+        self.g = None
+        self.p = None
+        self.dfo = {}
+
+
 class WavLMLayerFn(torch.autograd.Function):
     """h_out = layer(h) for one stable-LN WavLM layer; inputs h fp32 [B, T, E] and the LoRA factors
     (lora_A q, lora_B q, lora_A v, lora_B v, fp32 leaves, or None)."""
 
     @staticmethod
-    def forward(ctx, h, aq, bq, av, bv, layer, cache, rel, seed, index, p_hidden, p_attn, p_lora, scale):
+    def forward(ctx, h, aq, bq, av, bv, layer, cache, rel, seed, index, p_hidden, p_attn, p_lora, scale, chain):
         B, T, E = h.shape
         H = E // 64
         M = B * T
@@ -142,10 +161,21 @@ class WavLMLayerFn(torch.autograd.Function):
         gate = torch.empty(M, H, device=dev, dtype=torch.float32)
         mean1 = torch.empty(M, device=dev, dtype=torch.float32)
         rstd1 = torch.empty_like(mean1)
-        check(lib().rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg),
-                                   _p(cache.gconst), _p(aq) if lora else None, _p(av) if lora else None, 8,
-                                   sdp, salt + 3, salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1),
-                                   _p(rstd1), M, E, st), "wl_ln1_fwd")
+        pend = chain.pending_res if chain is not None else None
+        if pend is not None and pend[0] == hf.data_ptr():
+            # the previous layer's residual, computed here into its output (= this layer's input) tensor
+            chain.pending_res = None
+            _, h2p, fop, salt_res, p_res = pend
+            check(lib().rdx_wl_res_ln1_fwd(_p(h2p), _p(fop), salt_res, float(p_res), _p(hf), _p(ln1.weight),
+                                           _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
+                                           _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3,
+                                           salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1), _p(rstd1), M,
+                                           E, st), "wl_res_ln1_fwd")
+        else:
+            check(lib().rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg),
+                                       _p(cache.bg), _p(cache.gconst), _p(aq) if lora else None,
+                                       _p(av) if lora else None, 8, sdp, salt + 3, salt + 4, float(p_lora), _p(x1),
+                                       ldx, _p(gate), _p(mean1), _p(rstd1), M, E, st), "wl_ln1_fwd")
         qkv = F.linear(x1, cache.wext, cache.bqkv)                          # [M, 3E] (LoRA folded in)
         o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(B, H, T, device=dev, dtype=torch.float32)
@@ -168,9 +198,13 @@ class WavLMLayerFn(torch.autograd.Function):
         check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
         fo = F.linear(v, cache.w2, cache.b2)
         out = torch.empty(M, E, device=dev, dtype=torch.float32)
-        check(lib().rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st), "wl_residual")
+        if chain is not None and index < chain.n - 1:
+            chain.pending_res = (out.data_ptr(), h2, fo, salt + 2, float(p_hidden))   # -> the next LN1 forward
+        else:
+            check(lib().rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st),
+                  "wl_residual")
         ctx.save_for_backward(hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, rel, aq, av)
-        ctx.layer, ctx.cache, ctx.mask = layer, cache, mask
+        ctx.layer, ctx.cache, ctx.mask, ctx.chain = layer, cache, mask, chain
         ctx.lora_b = (bq, bv)
         ctx.meta = (B, T, E, H, index, float(p_hidden), float(p_attn), float(p_lora), float(scale), lora,
                     sd is not None)
@@ -188,8 +222,13 @@ class WavLMLayerFn(torch.autograd.Function):
         salt = SALT_BASE + 8 * index
         ldx = x1.shape[1]
         g = dout.contiguous().view(M, E).float()
-        dfo = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
-        check(lib().rdx_wl_dropout_bwd(_p(g), sdp, salt + 2, p_hidden, _p(dfo), M * E, st), "wl_dropout_bwd")
+        chain = ctx.chain
+        rec = chain.dfo.pop(index, None) if chain is not None else None
+        if rec is not None and rec[0] == g.data_ptr():
+            dfo = rec[1]                  # written by the next layer's LN1 backward along with g
+        else:
+            dfo = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+            check(lib().rdx_wl_dropout_bwd(_p(g), sdp, salt + 2, p_hidden, _p(dfo), M * E, st), "wl_dropout_bwd")
         dv = torch.mm(dfo, cache.w2)
         du = torch.empty_like(u)
         check(lib().rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
@@ -209,10 +248,20 @@ class WavLMLayerFn(torch.autograd.Function):
                             _off(dqkv, 2 * E), 3 * E, dgate, B, T, H, st)
         dx1 = torch.mm(dqkv, cache.wext)                                     # [M, E + 2r]
         dh = torch.empty(M, E, device=dev, dtype=torch.float32)
-        check(lib().rdx_wl_ln1_bwd(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
-                                   _p(ln1.bias), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
-                                   _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3, salt + 4,
-                                   p_lora, _p(dh2), _p(dh), None, M, E, st), "wl_ln1_bwd")
+        sgp = swp = ddp = None
+        if chain is not None and chain.g is not None and index in chain.indices:
+            sgp = _p(chain.g)                                   # this input's layer-weighted-sum gradient
+            swp = ctypes.c_void_p(chain.p.data_ptr() + 4 * index)
+        if chain is not None and index > 0:
+            ddrop = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+            ddp = _p(ddrop)
+        check(lib().rdx_wl_ln1_bwd_ex(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
+                                      _p(ln1.bias), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
+                                      _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3, salt + 4,
+                                      p_lora, _p(dh2), _p(dh), None, sgp, swp, salt - 8 + 2, p_hidden, ddp, M, E, st),
+              "wl_ln1_bwd")
+        if ddp is not None:
+            chain.dfo[index - 1] = (dh.data_ptr(), ddrop)
         if lora:
             # the four LoRA weight gradients in one launch, accumulated straight into .grad (fp32; with
             # FlatGrads these are views of the flat all-reduce buffer) instead of returned to autograd
@@ -225,7 +274,7 @@ class WavLMLayerFn(torch.autograd.Function):
             check(lib().rdx_wl_lora_grad(_p(dqkv), 3 * E, _p(x1), ldx, _p(dx1), ldx, sdp, salt + 3, salt + 4,
                                          p_lora, scale, _p(gs[0]), _p(gs[1]), _p(gs[2]), _p(gs[3]), M, E, 8, st),
                   "wl_lora_grad")
-        return (dh.view(B, T, E),) + (None,) * 13
+        return (dh.view(B, T, E),) + (None,) * 14
 
 
 class FusedEncoderRunner:
@@ -267,7 +316,7 @@ class FusedEncoderRunner:
                                      _stream(self.tab)), "wl_lora_pack")
         return loras
 
-    def layer(self, i, h, pb, loras, seed):
+    def layer(self, i, h, pb, loras, seed, chain=None):
         layer = self.encoder.layers[i]
         cfg = self.encoder.cfg
         tr = layer.training
@@ -287,4 +336,4 @@ class FusedEncoderRunner:
         if (p_hidden > 0 or p_attn > 0 or p_lora > 0) and seed is None:
             raise RuntimeError("fused WavLM layer: dropout needs the encoder's device seed")
         return WavLMLayerFn.apply(h, aq, bq, av, bv, layer, self.caches[i], pb, seed, i, p_hidden, p_attn, p_lora,
-                                  scale)
+                                  scale, chain)
