@@ -42,8 +42,8 @@ __device__ __forceinline__ uint32_t sc_pack2(float a, float b) {
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
 }
 __device__ __forceinline__ float sc_bf16(float x) { return __bfloat162float(__float2bfloat16(x)); }
-__device__ __forceinline__ float sc_selu(float u) {  // as sincnet.hip selu_f
-  return 1.0507009873554805f * (u > 0.f ? u : 1.6732632423543772f * expm1f(u));
+__device__ __forceinline__ float sc_selu(float u) {  // as sincnet.hip selu_fast (bf16-rounded output)
+  return 1.0507009873554805f * (u > 0.f ? u : 1.6732632423543772f * (__expf(u) - 1.0f));
 }
 
 // LDS byte offset of the 16-byte chunk `ch` (8 channels) of row `row` in a [rows][C] bf16 image; chunks are

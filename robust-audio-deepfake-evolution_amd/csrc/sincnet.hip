@@ -59,6 +59,11 @@ template <> struct Vec8<float> {
 };
 
 __device__ __forceinline__ float selu_f(float u) { return SELU_SCALE * (u > 0.f ? u : SELU_ALPHA * expm1f(u)); }
+// selu with exp(u) - 1 on the hardware exp for the forward-only passes whose output is rounded to bf16 (b0_fwd):
+// the absolute error of exp(u) - 1 near u = 0 (~1e-7) is far below a bf16 ulp of the result
+__device__ __forceinline__ float selu_fast(float u) {
+  return SELU_SCALE * (u > 0.f ? u : SELU_ALPHA * (__expf(u) - 1.0f));
+}
 __device__ __forceinline__ float selu_d(float u) { return u > 0.f ? SELU_SCALE : SELU_SCALE * SELU_ALPHA * __expf(u); }
 
 // per-channel constants of the frozen BN with the conv bias folded: zc = c + cb - mean,
@@ -436,62 +441,81 @@ extern "C" int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax
 // SincNet block 0 forward (one input channel, 32 output channels): conv1 (2 x 3, padding (1, 1)) and
 // conv_downsample (1 x 3, padding (0, 1)) of the bf16 input with bf16-valued weights and fp32 accumulation (what
 // autocast runs), plus conv1's frozen BN + SELU on the bf16-rounded conv1 output (bnselu_fwd_kernel's
-// arithmetic). A workgroup covers 64 conv1 output pixels (n, h, w), lane = pixel; wave g computes channel group g
-// (8 channels), so its 104 weight / BN constants are wave-uniform (scalar loads) and each lane stores one 16-byte
-// chunk of each NHWC output row: c (pre-activation, kept for the backward), y = selu(bn(c + cb)) and, for h < H,
-// idn (the bottom row of conv1's 2 x 3 window is the downsample's window). The four waves of a workgroup fill
-// the same 64-byte rows, which meet in L2. Replaces two MIOpen convolutions (each with its own output-zeroing
-// pass) and the separate BN + SELU pass.
-constexpr int B0F_PIX = 64;
-__global__ __launch_bounds__(B0F_PIX * (B0_C / SN_VEC)) void b0_fwd_kernel(
+// arithmetic, exp(u) - 1 on the hardware exp). Lane = (8-pixel run, 8-channel group): the lane's 104 weight /
+// BN constants are loaded once into registers, and it walks B0F_RUN consecutive conv1 output pixels of a row
+// with a sliding 2 x 3 input window (two new input values per pixel; index math once per run). Each store
+// instruction of a wave writes 16 runs' 64-byte NHWC rows: c (pre-activation, kept for the backward),
+// y = selu(bn(c + cb)) and, for h < H, idn (the bottom row of conv1's window is the downsample's window).
+// Replaces two MIOpen convolutions (each with its own output-zeroing pass) and the separate BN + SELU pass.
+constexpr int B0F_RUN = 8;
+__device__ __forceinline__ float b0_x(const __hip_bfloat16* x, int n, int r, int cc, int H, int W) {
+  return (r >= 0 && r < H && cc >= 0 && cc < W) ? __bfloat162float(x[((int64_t)n * H + r) * W + cc]) : 0.f;
+}
+__global__ __launch_bounds__(SN_THREADS) void b0_fwd_kernel(
     const __hip_bfloat16* __restrict__ x, const float* __restrict__ w1, const float* __restrict__ wd,
     const float* __restrict__ bn, __hip_bfloat16* __restrict__ c, __hip_bfloat16* __restrict__ y,
     __hip_bfloat16* __restrict__ idn, int N, int H, int W) {
-  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // channel group of this wave
-  const int pix = blockIdx.x * B0F_PIX + (threadIdx.x & 63);       // < 2^31: checked by the launcher
-  const int per = (H + 1) * W;
-  if (pix >= N * per) return;
-  const int n = pix / per;
-  const int rem = pix - n * per;
-  const int h = rem / W, w = rem - h * W;
-  float v[2][3];
-#pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
-    const int r = h - 1 + kh;
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int cc = w - 1 + kw;
-      v[kh][kw] = (r >= 0 && r < H && cc >= 0 && cc < W) ? __bfloat162float(x[((int64_t)n * H + r) * W + cc]) : 0.f;
-    }
-  }
-  float cv[SN_VEC], yv[SN_VEC], iv[SN_VEC];
+  const int g = threadIdx.x & 3;
+  float t1[SN_VEC][6], td[SN_VEC][3], cb[SN_VEC], mu[SN_VEC], sc[SN_VEC], sh[SN_VEC];
 #pragma unroll
   for (int k = 0; k < SN_VEC; ++k) {
     const int co = g * SN_VEC + k;
-    const float* t = w1 + co * 6;
-    float acc = 0.f;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
+    for (int j = 0; j < 6; ++j) t1[k][j] = w1[co * 6 + j];
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) acc = fmaf(v[kh][kw], t[kh * 3 + kw], acc);
-    cv[k] = __bfloat162float(__float2bfloat16(acc));
-    yv[k] = selu_f(fmaf((cv[k] + bn[co]) - bn[B0_C + co], bn[2 * B0_C + co], bn[3 * B0_C + co]));
-    const float* u = wd + co * 3;
-    iv[k] = fmaf(v[1][0], u[0], fmaf(v[1][1], u[1], v[1][2] * u[2]));
+    for (int j = 0; j < 3; ++j) td[k][j] = wd[co * 3 + j];
+    cb[k] = bn[co];
+    mu[k] = bn[B0_C + co];
+    sc[k] = bn[2 * B0_C + co];
+    sh[k] = bn[3 * B0_C + co];
   }
-  Vec8<__hip_bfloat16>::store(c + (int64_t)pix * B0_C + g * SN_VEC, cv);
-  Vec8<__hip_bfloat16>::store(y + (int64_t)pix * B0_C + g * SN_VEC, yv);
-  if (h < H) Vec8<__hip_bfloat16>::store(idn + (((int64_t)n * H + h) * W + w) * B0_C + g * SN_VEC, iv);
+  const int runs_per_row = (W + B0F_RUN - 1) / B0F_RUN;
+  const int run = blockIdx.x * (SN_THREADS / 4) + (threadIdx.x >> 2);   // over N * (H + 1) * runs_per_row
+  const int nrow = run / runs_per_row;
+  if (nrow >= N * (H + 1)) return;
+  const int n = nrow / (H + 1), h = nrow - n * (H + 1);
+  const int w0 = (run - nrow * runs_per_row) * B0F_RUN;
+  float v0[3], v1[3];   // input rows h - 1 and h, columns w - 1 .. w + 1
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    v0[kw] = b0_x(x, n, h - 1, w0 - 1 + kw, H, W);
+    v1[kw] = b0_x(x, n, h, w0 - 1 + kw, H, W);
+  }
+  const int64_t pbase = (int64_t)nrow * W;
+  const int64_t ibase = ((int64_t)n * H + h) * W;
+#pragma unroll
+  for (int st = 0; st < B0F_RUN; ++st) {
+    const int w = w0 + st;
+    if (w >= W) break;
+    float cv[SN_VEC], yv[SN_VEC], iv[SN_VEC];
+#pragma unroll
+    for (int k = 0; k < SN_VEC; ++k) {
+      float acc = v0[0] * t1[k][0];
+      acc = fmaf(v0[1], t1[k][1], acc);
+      acc = fmaf(v0[2], t1[k][2], acc);
+      acc = fmaf(v1[0], t1[k][3], acc);
+      acc = fmaf(v1[1], t1[k][4], acc);
+      acc = fmaf(v1[2], t1[k][5], acc);
+      cv[k] = __bfloat162float(__float2bfloat16(acc));
+      yv[k] = selu_fast(fmaf((cv[k] + cb[k]) - mu[k], sc[k], sh[k]));
+      iv[k] = fmaf(v1[0], td[k][0], fmaf(v1[1], td[k][1], v1[2] * td[k][2]));
+    }
+    Vec8<__hip_bfloat16>::store(c + (pbase + w) * B0_C + g * SN_VEC, cv);
+    Vec8<__hip_bfloat16>::store(y + (pbase + w) * B0_C + g * SN_VEC, yv);
+    if (h < H) Vec8<__hip_bfloat16>::store(idn + (ibase + w) * B0_C + g * SN_VEC, iv);
+    v0[0] = v0[1]; v0[1] = v0[2]; v0[2] = b0_x(x, n, h - 1, w + 2, H, W);
+    v1[0] = v1[1]; v1[1] = v1[2]; v1[2] = b0_x(x, n, h, w + 2, H, W);
+  }
 }
 
 extern "C" int rdx_sincnet_b0_fwd(const void* x, const float* w1, const float* wd, const float* bn, void* c, void* y,
                                   void* idn, int N, int H, int W, int C, void* stream) {
   RDX_REQUIRE(x && w1 && wd && bn && c && y && idn && N > 0 && H > 0 && W > 0);
   if (C != B0_C) return RDX_EUNSUPPORTED;
-  const int64_t npix = (int64_t)N * (H + 1) * W;
-  RDX_REQUIRE(npix < ((int64_t)1 << 31));
-  hipLaunchKernelGGL(b0_fwd_kernel, dim3((unsigned)((npix + B0F_PIX - 1) / B0F_PIX)), dim3(B0F_PIX * (B0_C / SN_VEC)), 0,
-                     as_stream(stream), (const __hip_bfloat16*)x, w1, wd, bn, (__hip_bfloat16*)c, (__hip_bfloat16*)y,
+  const int64_t nruns = (int64_t)N * (H + 1) * ((W + B0F_RUN - 1) / B0F_RUN);
+  RDX_REQUIRE(nruns * 4 < ((int64_t)1 << 31));
+  hipLaunchKernelGGL(b0_fwd_kernel, dim3((unsigned)((nruns + SN_THREADS / 4 - 1) / (SN_THREADS / 4))), dim3(SN_THREADS),
+                     0, as_stream(stream), (const __hip_bfloat16*)x, w1, wd, bn, (__hip_bfloat16*)c, (__hip_bfloat16*)y,
                      (__hip_bfloat16*)idn, N, H, W);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
