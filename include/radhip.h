@@ -121,6 +121,19 @@ int rdx_bigate_bwd(int dtype, const void* dg, const void* z, int64_t ldz, const 
                    float* dy, void* dz, int64_t lddz, int B, int L, int D, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * LayerNorm over the last dimension, C <= 1024 (the detector head's norms: PN-BiMamba norm1/norm2, the
+ * fusion's ln_wavlm / ln_sinc / norm, norm_f; src/models/DualStreamSEMamba.py:445-486,537-637,700-770).
+ * Forward: x [M, C] (dtype_x) -> y (dtype_y; bf16 when the consumer is a bf16 linear), mean / rstd [M] fp32
+ * (biased variance, as torch). Backward: dx (dtype_x) = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma;
+ * dgamma += sum dy xhat, dbeta += sum dy (fp32, ACCUMULATED into the caller's buffers). C > 1024:
+ * RDX_EUNSUPPORTED.
+ * ------------------------------------------------------------------------------------------ */
+int rdx_row_ln_fwd(int dtype_x, const void* x, const float* gamma, const float* beta, float eps, int dtype_y, void* y,
+                   float* mean, float* rstd, int64_t M, int C, void* stream);
+int rdx_row_ln_bwd(int dtype_dy, const void* dy, int dtype_x, const void* x, const float* mean, const float* rstd,
+                   const float* gamma, void* dx, float* dgamma, float* dbeta, int64_t M, int C, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * WavLM layer-weighted sum, replaces WavLMFrontend.forward's stack + softmax-weighted sum
  * (src/models/DualStreamSEMamba.py:427-437).  hs: host array of `nl` device pointers, each
  * [n] elements; w: device [nl] fp32 raw layer weights (softmax taken in-kernel). nl <= 64.

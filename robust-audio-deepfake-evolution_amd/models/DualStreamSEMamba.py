@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
-from radhip.linear import SideLinear
+from radhip.linear import RowLayerNorm, SideLinear
 from radhip.mamba import Mamba
 from radhip.ops import layer_weighted_sum
 from radhip.sinc import CONV, Residual_block, SincNetEncoder  # noqa: F401  (re-exported like the reference)
@@ -128,8 +128,8 @@ class PN_BiMambas_Encoder(nn.Module):
         super().__init__()
         self.d_model = d_model
         self.mamba = Mamba(d_model, n_state)
-        self.norm1 = nn.LayerNorm(d_model)
-        self.norm2 = nn.LayerNorm(d_model)
+        self.norm1 = RowLayerNorm(d_model, to_linear=True)
+        self.norm2 = RowLayerNorm(d_model, to_linear=True)
         self.feed_forward = nn.Sequential(SideLinear(d_model, d_model * 4), nn.GELU(), SideLinear(d_model * 4, d_model))
 
     def forward(self, x):
@@ -160,13 +160,13 @@ class DualStreamFusion(nn.Module):
 
     def __init__(self, wavlm_dim: int, sinc_dim: int, out_dim: int, reduction: int = 16):
         super().__init__()
-        self.ln_wavlm = nn.LayerNorm(wavlm_dim)
-        self.ln_sinc = nn.LayerNorm(sinc_dim)
+        self.ln_wavlm = RowLayerNorm(wavlm_dim, to_linear=True)
+        self.ln_sinc = RowLayerNorm(sinc_dim, to_linear=True)
         self.wavlm_proj = SideLinear(wavlm_dim, out_dim)
         self.sinc_proj = SideLinear(sinc_dim, out_dim)
         self.fusion_proj = SideLinear(out_dim * 2, out_dim)
         self.se_layer = SELayer(out_dim, reduction=reduction)
-        self.norm = nn.LayerNorm(out_dim)
+        self.norm = RowLayerNorm(out_dim)
         self.dropout = nn.Dropout(0.1)
 
     def forward(self, f_wavlm: Tensor, f_sinc: Tensor) -> Tensor:
@@ -197,7 +197,7 @@ class Model(nn.Module):
                                        out_dim=emb_size, reduction=16)
         self.backbone_layers = nn.ModuleList([PN_BiMambas_Encoder(d_model=emb_size, n_state=d_state)
                                               for _ in range(num_encoders)])
-        self.norm_f = nn.LayerNorm(emb_size)
+        self.norm_f = RowLayerNorm(emb_size, to_linear=True)
         self.attention_pool = SideLinear(emb_size, 1)
         self.dropout = nn.Dropout(0.1)
         self.classifier = SideLinear(emb_size, 2)

@@ -89,6 +89,8 @@ SIGNATURES = {
     "rdx_bnselu_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
     "rdx_res_tail_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_res_tail_bwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "rdx_row_ln_fwd": (c_int, [c_int, c_vp, c_vp, c_vp, c_f32, c_int, c_vp, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "rdx_row_ln_bwd": (c_int, [c_int, c_vp, c_int] + [c_vp] * 7 + [c_i64, c_int, c_vp]),
     "rdx_sincnet_b0_fwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),
     "rdx_sincnet_b0_nblk": (c_int, [c_i64]),
     "rdx_sincnet_b0_bwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),

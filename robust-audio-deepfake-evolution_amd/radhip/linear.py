@@ -136,3 +136,79 @@ class SideLinear(nn.Linear):
 
     def forward(self, x):
         return side_linear(x, self.weight, self.bias)
+
+
+_ROWLN = os.environ.get("RADHIP_ROW_LN", "1") != "0"
+
+
+class RowLNFn(torch.autograd.Function):
+    """LayerNorm over the last dimension on csrc/rowln.hip; output in `out_dtype`."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, out_dtype):
+        from ._lib import check, lib
+        C = x.shape[-1]
+        xc = x.contiguous()
+        M = xc.numel() // C
+        y = torch.empty(x.shape, device=x.device, dtype=out_dtype)
+        mean = torch.empty(M, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        w, b = weight.detach().float().contiguous(), bias.detach().float().contiguous()
+        check(lib().rdx_row_ln_fwd(ops._dtype_code(xc), ops._p(xc), ops._p(w), ops._p(b), float(eps),
+                                   ops._dtype_code(y), ops._p(y), ops._p(mean), ops._p(rstd), M, C, ops._stream(xc)),
+              "row_ln_fwd")
+        ctx.save_for_backward(xc, mean, rstd, w)
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ._lib import check, lib
+        xc, mean, rstd, w = ctx.saved_tensors
+        weight, bias = ctx.params
+        C = xc.shape[-1]
+        M = xc.numel() // C
+        dy = dy.contiguous()
+        if dy.dtype not in (torch.float32, torch.bfloat16):
+            dy = dy.float()
+        dx = torch.empty_like(xc)
+        direct = all(p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                     for p in (weight, bias))
+        if direct:
+            dgw, dgb = weight.grad, bias.grad
+        else:
+            dgw, dgb = torch.zeros(C, device=xc.device), torch.zeros(C, device=xc.device)
+        check(lib().rdx_row_ln_bwd(ops._dtype_code(dy), ops._p(dy), ops._dtype_code(xc), ops._p(xc), ops._p(mean),
+                                   ops._p(rstd), ops._p(w), ops._p(dx), ops._p(dgw), ops._p(dgb), M, C,
+                                   ops._stream(xc)), "row_ln_bwd")
+        if direct:
+            return dx, None, None, None, None
+        return dx, dgw.to(weight.dtype), dgb.to(bias.dtype), None, None
+
+
+class RowLayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters and state_dict keys) on csrc/rowln.hip for C <= 1024 on the GPU: one kernel
+    each way instead of torch's layer_norm forward, its three backward kernels and the casts around them. Its
+    gamma / beta gradients are accumulated in fp32 straight into .grad (like SideLinear). `to_linear`: the only
+    consumers are linears, so under bf16 autocast the output is written in bf16 — the value the linear's input
+    cast would produce from torch's fp32 output."""
+
+    def __init__(self, *args, to_linear=False, **kw):
+        super().__init__(*args, **kw)
+        self.to_linear = to_linear
+        if self.elementwise_affine:
+            self.weight._radhip_direct_grad = True
+            if self.bias is not None:
+                self.bias._radhip_direct_grad = True
+
+    def forward(self, x):
+        if not (_ROWLN and x.is_cuda and len(self.normalized_shape) == 1 and x.shape[-1] <= 1024 and self.elementwise_affine
+                and self.bias is not None and x.dtype in (torch.float32, torch.bfloat16)):
+            return super().forward(x)
+        ac = torch.is_autocast_enabled("cuda")
+        if ac:
+            out = torch.bfloat16 if (self.to_linear and torch.get_autocast_dtype("cuda") == torch.bfloat16) else torch.float32
+        else:
+            out = x.dtype
+        with torch.autocast("cuda", enabled=False):
+            return RowLNFn.apply(x, self.weight, self.bias, self.eps, out)

@@ -492,6 +492,38 @@ def test_sincnet_block0_front(N, H, W):
         assert ((got.float() - ref).norm() / ref.norm()).item() < 2e-2
 
 
+@pytest.mark.parametrize("C,dt_in,to_linear", [(144, torch.float32, True), (144, torch.bfloat16, True),
+                                               (64, torch.bfloat16, True), (1024, torch.float32, True),
+                                               (144, torch.float32, False), (36, torch.float32, False)])
+def test_row_layer_norm(C, dt_in, to_linear):
+    """radhip.linear.RowLayerNorm (csrc/rowln.hip) under bf16 autocast vs torch fp32 layer_norm of the same input:
+    output (bf16 when it feeds a linear, else fp32), input gradient, and gamma / beta gradients both accumulated
+    into existing fp32 .grad buffers and returned to autograd."""
+    from radhip.linear import RowLayerNorm
+    torch.manual_seed(6)
+    ln = RowLayerNorm(C, to_linear=to_linear).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.rand(C) + 0.5)
+        ln.bias.copy_(0.1 * torch.randn(C))
+    x = (torch.randn(3, 201, C, device=DEV) * 2 + 0.3).to(dt_in).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ln(x)
+    assert y.dtype == (torch.bfloat16 if to_linear else torch.float32)
+    gy = torch.randn(y.shape, device=DEV).to(y.dtype)
+    ln.weight.grad = torch.full_like(ln.weight, 0.5)      # accumulation on top of existing values:
+    ln.bias.grad = torch.zeros_like(ln.bias) if C != 36 else None   # in place (direct) / returned to autograd
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_()
+    wr, br = ln.weight.detach().clone().requires_grad_(), ln.bias.detach().clone().requires_grad_()
+    yr = F.layer_norm(xr, (C,), wr, br, ln.eps)
+    yr.backward(gy.float())
+    tol = 1e-2 if to_linear or dt_in == torch.bfloat16 else 1e-5
+    assert ((y.float() - yr).norm() / yr.norm()).item() < tol
+    assert ((x.grad.float() - xr.grad).norm() / xr.grad.norm()).item() < (2e-2 if dt_in == torch.bfloat16 else 1e-4)
+    assert ((ln.weight.grad - 0.5 - wr.grad).norm() / wr.grad.norm()).item() < 1e-4
+    assert ((ln.bias.grad - br.grad).norm() / br.grad.norm()).item() < 1e-4
+
+
 def test_attention_rejects_non_toeplitz_bias():
     """The kernels take the bias as a relative-position table; a bias that is not a function of key - query
     is refused loudly rather than silently mis-read."""
