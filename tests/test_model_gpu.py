@@ -165,7 +165,8 @@ def test_fgm_cnn_feature_reuse_is_exact(golden):
         torch.cuda.synchronize()
         flats.append(tr.grads.flat.clone())
     err = ((flats[0] - flats[1]).norm() / flats[1].norm()).item()
-    # two recomputing runs differ by the fp32 atomic-accumulation order of the scan/attention backward
-    # (dB/dC, dgate); reuse must sit within that run-to-run floor
+    # two recomputing runs differ by the fp32 atomic-accumulation order of the scan/attention/LayerNorm backward
+    # (dB/dC, dgate, dgamma): measured 2e-6 .. 5.5e-5 between runs of the same process, so one sampled pair can
+    # undershoot the floor; reuse must sit within it (a wrong feature tensor gives O(1) differences)
     noise = ((flats[2] - flats[1]).norm() / flats[1].norm()).item()
-    assert err < max(5e-5, 4 * noise), (err, noise)
+    assert err < max(2e-4, 4 * noise), (err, noise)

@@ -89,6 +89,20 @@ def main():
         o["gelu_fwd"] = timed(lambda: check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "g"))
         o["gelu_bwd"] = timed(lambda: check(lib().rdx_wl_gelu(1, _p(u), _p(u), _p(v), u.numel(), st), "g"))
         o["copy_u_bf16"] = timed(lambda: u.clone())
+        # the gated attention forward (C ABI, p = 0.1 with the keep-mask words the fused backward reads)
+        from radhip.ops import attn_keep_mask
+        qkv = torch.randn(M, 3 * E, device=dev).to(torch.bfloat16)
+        ob = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, 201, device=dev)
+        rel = torch.randn(H, 2 * 201 - 1, device=dev) * 0.1
+        km = attn_keep_mask(B, 201, H, 0.1, dev)
+
+        def attn():
+            check(lib().rdx_attn_fwd(_p(qkv), 3 * E, ctypes.c_void_p(qkv.data_ptr() + 2 * E), 3 * E,
+                                     ctypes.c_void_p(qkv.data_ptr() + 4 * E), 3 * E, _p(gate), _p(rel), _p(seed), 0,
+                                     0.1, 0.125, _p(ob), E, _p(lse), _p(km) if km is not None else None, B, 201, H, 64,
+                                     st), "attn_fwd")
+        o["attn_fwd"] = timed(attn)
         # the layer's hipBLASLt GEMMs (forward and input gradients)
         wext = torch.randn(3 * E, E + 16, device=dev).to(torch.bfloat16)
         bq = torch.randn(3 * E, device=dev).to(torch.bfloat16)
