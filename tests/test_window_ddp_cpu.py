@@ -43,9 +43,16 @@ class _Conv(torch.nn.Module):
 
 
 class _Sinc(torch.nn.Module):
+    """A trainable stand-in for the SincNet stream: the window batches the adversarial passes' forwards and
+    backwards of this stream (radhip/window.py::_sinc_adv_forward / _sinc_adv_backward)."""
+
     def __init__(self):
         super().__init__()
         self.conv_time = _Conv()
+        self.proj = torch.nn.Linear(FR, 6)
+
+    def forward(self, x, freq_aug=False):
+        return torch.tanh(self.proj(x.view(x.shape[0], -1, FR)))
 
 
 class _FP(torch.nn.Module):
@@ -112,9 +119,11 @@ class ToyDual(torch.nn.Module):
         self.sinc_stream = _Sinc()
         self.wavlm_stream = _WavLM()
         self.classifier = torch.nn.Linear(6, 2)
+        self.sinc_given = None
 
     def forward(self, x, Freq_aug=False):
-        h = self.wavlm_stream.core(x).mean(dim=1)
+        s = self.sinc_given if self.sinc_given is not None else self.sinc_stream(x, freq_aug=Freq_aug)
+        h = self.wavlm_stream.core(x).mean(dim=1) + s.mean(dim=1)
         return h, self.classifier(h)
 
 
