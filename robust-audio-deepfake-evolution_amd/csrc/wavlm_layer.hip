@@ -168,10 +168,13 @@ struct Ln1Args {
   float* hout;
 };
 
-// LoRA-A of both adapters staged once per workgroup of WL_LN1_ROWS row-waves: [2r][E] bf16 (the cast autocast
+// LoRA-A of both adapters staged once per workgroup of WL_LN1_ROWS row-waves (4): [2r][E] bf16 (the cast autocast
 // applies to lora_A's weight), 32 KB. A row-wave reading the fp32 A from L2 itself moved 64 KB per token row
 // and left these kernels L2-bound (26 us of the 47 us forward at B = 32).
-constexpr int WL_LN1_ROWS = 8;
+#ifndef WL_LN1_ROWS_DEF
+#define WL_LN1_ROWS_DEF 4   // measured: 4 rows beat 8 and 2 at both pass sizes (tools/bench_wl.py)
+#endif
+constexpr int WL_LN1_ROWS = WL_LN1_ROWS_DEF;
 constexpr int WL_LN1_THREADS = WL_LN1_ROWS * RDX_WAVE;
 
 __device__ __forceinline__ void stage_lora_a(__hip_bfloat16* sA, const float* Aq, const float* Av) {
