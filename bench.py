@@ -350,11 +350,12 @@ def main():
                 w.capture()
                 w.reset_host()
             capture(window)
-            window_t = WindowStep(trainer, B, graphs=True)
             prev = os.environ.get("RADHIP_SINC_BRANCH")
             os.environ["RADHIP_SINC_BRANCH"] = "0"
             ops.CAPTURE_TIMING = graph_timer
             try:
+                # built under the switch: the window picks its batched adversarial SincNet stream at construction
+                window_t = WindowStep(trainer, B, graphs=True)
                 capture(window_t)
             finally:
                 ops.CAPTURE_TIMING = None
