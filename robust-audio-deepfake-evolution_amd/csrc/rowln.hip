@@ -5,7 +5,7 @@
 //   forward  one wave per row: mean / rstd (two-pass, biased variance, as torch), y = (x - mean) rstd gamma +
 //            beta written in the requested dtype (bf16 when the consumer is a bf16 linear: the same value the
 //            cast would produce), mean / rstd saved.
-//   backward one wave per row, ROWS_PER_WAVE rows: dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma;
+//   backward one wave per ROWS_PER_WAVE rows (the next row prefetched): dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy gamma;
 //            dgamma = sum dy xhat, dbeta = sum dy accumulated per lane, reduced over the workgroup's waves in
 //            LDS and ADDED into the fp32 gradient buffers with one atomic per (channel, workgroup).
 #include <type_traits>
@@ -16,7 +16,10 @@ namespace rdx {
 
 constexpr int RL_MAXV = 16;            // C <= 64 * 16
 constexpr int RL_WAVES = 4;
-constexpr int RL_ROWS_PER_WAVE = 8;
+#ifndef RL_RPW
+#define RL_RPW 8
+#endif
+constexpr int RL_ROWS_PER_WAVE = RL_RPW;
 
 template <typename T>
 __device__ __forceinline__ float rl_ld(const T* p, int64_t i) {
@@ -65,50 +68,74 @@ __global__ __launch_bounds__(RL_WAVES * 64) void row_ln_fwd_kernel(const TI* __r
   }
 }
 
-template <typename TG, typename TX>
+template <typename TG, typename TX, int V>
 __global__ __launch_bounds__(RL_WAVES * 64) void row_ln_bwd_kernel(const TG* __restrict__ dy, const TX* __restrict__ x,
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ rstd,
                                                                   const float* __restrict__ gamma, TX* __restrict__ dx,
                                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                   int64_t M, int C) {
-  __shared__ float red[2][RL_WAVES][RL_MAXV * 64];
+  // V = values per lane (C <= 64 V). The next row's dy / x are loaded while the current row is reduced, so a
+  // wave's rows do not serialize on HBM latency.
+  __shared__ float red[2][RL_WAVES][V * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float dg[RL_MAXV], db[RL_MAXV], gm[RL_MAXV];
+  float dg[V], db[V], gm[V];
 #pragma unroll
-  for (int j = 0; j < RL_MAXV; ++j) {
+  for (int j = 0; j < V; ++j) {
     const int c = lane + 64 * j;
     dg[j] = db[j] = 0.f;
     gm[j] = c < C ? gamma[c] : 0.f;
   }
   const int64_t m0 = ((int64_t)blockIdx.x * RL_WAVES + wv) * RL_ROWS_PER_WAVE;
-  for (int rr = 0; rr < RL_ROWS_PER_WAVE; ++rr) {
+  const int nrow = (int)(M - m0 < RL_ROWS_PER_WAVE ? (M - m0 > 0 ? M - m0 : 0) : RL_ROWS_PER_WAVE);
+  float dn[V], xn[V];
+  if (nrow > 0) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = lane + 64 * j;
+      dn[j] = c < C ? rl_ld(dy, m0 * C + c) : 0.f;
+      xn[j] = c < C ? rl_ld(x, m0 * C + c) : 0.f;
+    }
+  }
+  for (int rr = 0; rr < nrow; ++rr) {
     const int64_t m = m0 + rr;
-    if (m >= M) break;
+    float d[V], xv[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      d[j] = dn[j];
+      xv[j] = xn[j];
+    }
+    if (rr + 1 < nrow) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = lane + 64 * j;
+        dn[j] = c < C ? rl_ld(dy, (m + 1) * C + c) : 0.f;
+        xn[j] = c < C ? rl_ld(x, (m + 1) * C + c) : 0.f;
+      }
+    }
     const float mu = mean[m], rs = rstd[m];
-    float xh[RL_MAXV], g[RL_MAXV];
+    float xh[V], g[V];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < RL_MAXV; ++j) {
+    for (int j = 0; j < V; ++j) {
       const int c = lane + 64 * j;
-      const float d = c < C ? rl_ld(dy, m * C + c) : 0.f;
-      xh[j] = c < C ? (rl_ld(x, m * C + c) - mu) * rs : 0.f;
-      g[j] = d * gm[j];
+      xh[j] = c < C ? (xv[j] - mu) * rs : 0.f;
+      g[j] = d[j] * gm[j];
       s1 += g[j];
       s2 += g[j] * xh[j];
-      dg[j] = fmaf(d, xh[j], dg[j]);
-      db[j] += d;
+      dg[j] = fmaf(d[j], xh[j], dg[j]);
+      db[j] += d[j];
     }
     s1 = wave_sum(s1) / C;
     s2 = wave_sum(s2) / C;
 #pragma unroll
-    for (int j = 0; j < RL_MAXV; ++j) {
+    for (int j = 0; j < V; ++j) {
       const int c = lane + 64 * j;
       if (c < C) rl_st(dx, m * C + c, rs * (g[j] - s1 - xh[j] * s2));
     }
   }
 #pragma unroll
-  for (int j = 0; j < RL_MAXV; ++j) {
+  for (int j = 0; j < V; ++j) {
     red[0][wv][lane + 64 * j] = dg[j];
     red[1][wv][lane + 64 * j] = db[j];
   }
@@ -157,9 +184,15 @@ extern "C" int rdx_row_ln_bwd(int dtype_dy, const void* dy, int dtype_x, const v
   const int64_t rows_per_block = (int64_t)RL_WAVES * RL_ROWS_PER_WAVE;
   const dim3 grid((unsigned)((M + rows_per_block - 1) / rows_per_block)), block(RL_WAVES * 64);
   hipStream_t st = as_stream(stream);
-#define RL_BWD(TG, TX)                                                                                            \
-  hipLaunchKernelGGL((row_ln_bwd_kernel<TG, TX>), grid, block, 0, st, (const TG*)dy, (const TX*)x, mean, rstd, \
-                     gamma, (TX*)dx, dgamma, dbeta, M, C)
+#define RL_BWD(TG, TX)                                                                                           \
+  do {                                                                                                          \
+    if (C <= 64 * 3)                                                                                           \
+      hipLaunchKernelGGL((row_ln_bwd_kernel<TG, TX, 3>), grid, block, 0, st, (const TG*)dy, (const TX*)x, mean, \
+                         rstd, gamma, (TX*)dx, dgamma, dbeta, M, C);                                          \
+    else                                                                                                        \
+      hipLaunchKernelGGL((row_ln_bwd_kernel<TG, TX, RL_MAXV>), grid, block, 0, st, (const TG*)dy, (const TX*)x, \
+                         mean, rstd, gamma, (TX*)dx, dgamma, dbeta, M, C);                                    \
+  } while (0)
   if (dtype_dy == RDX_F32 && dtype_x == RDX_F32) RL_BWD(float, float);
   else if (dtype_dy == RDX_F32) RL_BWD(float, __hip_bfloat16);
   else if (dtype_x == RDX_F32) RL_BWD(__hip_bfloat16, float);
