@@ -17,7 +17,7 @@ namespace rdx {
 constexpr int RL_MAXV = 16;            // C <= 64 * 16
 constexpr int RL_WAVES = 4;
 #ifndef RL_RPW
-#define RL_RPW 8
+#define RL_RPW 4
 #endif
 constexpr int RL_ROWS_PER_WAVE = RL_RPW;
 
