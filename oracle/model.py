@@ -21,8 +21,10 @@ class OWavLM(nn.Module):
         self.model = WavLMModel(WavLMConfig(**cfg_dict))
         self.layer_weights = nn.Parameter(torch.zeros(self.model.config.num_hidden_layers + 1))
 
-    def forward(self, x):
-        hs = self.model(x, output_hidden_states=True).hidden_states
+    def forward(self, x, time_mask=None):
+        """time_mask: the SpecAugment mask of a training forward ([B, T] bool; HF _mask_hidden_states), given
+        explicitly so the oracle uses the product's host draw."""
+        hs = self.model(x, output_hidden_states=True, mask_time_indices=time_mask).hidden_states
         w = F.softmax(self.layer_weights, dim=0)
         return (w.view(-1, 1, 1, 1) * torch.stack(hs)).sum(0)
 
@@ -127,14 +129,56 @@ class OracleModel(nn.Module):
         self.dropout = nn.Dropout(0.1)
         self.classifier = nn.Linear(emb_size, 2)
 
-    def forward(self, x, mask=None):
-        f = self.fusion(self.wavlm_stream(x), self.sinc_stream(x, mask))
+    def forward(self, x, mask=None, time_mask=None):
+        f = self.fusion(self.wavlm_stream(x, time_mask), self.sinc_stream(x, mask))
         for layer in self.backbone_layers:
             f = layer(f)
         f = self.norm_f(f)
         a = F.softmax(self.attention_pool(f), dim=1)
         feats = self.dropout(torch.matmul(a.transpose(1, 2), f).squeeze(1))
         return feats, self.classifier(feats)
+
+
+class OLoraLinear(nn.Module):
+    """peft lora.Linear as the reference injects it (src/main.py:103-158: LoraConfig(r, lora_alpha,
+    target_modules=[q_proj, v_proj], lora_dropout) + get_peft_model): base(x) + B(A(dropout(x))) * alpha / r,
+    with peft's state-dict layout (base_layer, lora_A.default, lora_B.default). Dropout is left out: the
+    oracle is compared with it off."""
+
+    def __init__(self, base, r=8, alpha=32):
+        super().__init__()
+        self.base_layer = base
+        self.lora_A = nn.ModuleDict({"default": nn.Linear(base.in_features, r, bias=False)})
+        self.lora_B = nn.ModuleDict({"default": nn.Linear(r, base.out_features, bias=False)})
+        self.scaling = alpha / r
+
+    def forward(self, x):
+        return self.base_layer(x) + self.lora_B["default"](self.lora_A["default"](x)) * self.scaling
+
+
+def apply_lora(model, r=8, alpha=32, targets=("q_proj", "v_proj")):
+    """Wrap every target linear of the oracle's WavLM in OLoraLinear (base weights frozen, as peft does)."""
+    wl = model.wavlm_stream.model
+    for p in wl.parameters():
+        p.requires_grad_(False)
+    for layer in wl.encoder.layers:
+        att = layer.attention
+        for t in targets:
+            setattr(att, t, OLoraLinear(getattr(att, t), r, alpha))
+    return model
+
+
+def from_peft_state(sd):
+    """The product's peft-wrapped WavLM keys (wavlm_stream.model.base_model.model.<path>) -> the oracle's."""
+    return {k.replace("wavlm_stream.model.base_model.model.", "wavlm_stream.model."): v for k, v in sd.items()}
+
+
+def focal_loss(logits, y, alpha=0.9, gamma=2.5):
+    """kornia FocalLoss(alpha, gamma, reduction='mean') with per-class alpha [1 - alpha, alpha] (src/main.py:
+    297-305; the default 'per_class' restatement of radhip.train.FocalLoss): the mean runs over B x C."""
+    lp = F.log_softmax(logits, dim=1).gather(1, y[:, None]).squeeze(1)
+    a = torch.where(y == 0, 1.0 - alpha, alpha).to(lp.dtype)
+    return (-a * (1.0 - lp.exp()) ** gamma * lp).sum() / (logits.shape[0] * logits.shape[1])
 
 
 def tiny_wavlm_config(js):

@@ -33,7 +33,8 @@ __device__ __forceinline__ float focal_row(const T* z, int C, int y, float alpha
   const float omp = 1.0f - p;
   const float w = powf(omp, gamma);
   const float a = alpha < 0.f ? 1.0f : (mode == 0 ? (y == 0 ? 1.0f - alpha : alpha) : alpha);
-  const float k = w - gamma * powf(omp, gamma - 1.0f) * p * lp;
+  // d/dp of (1 - p)^gamma is 0 at gamma == 0 and taken as 0 at p == 1 (torch pow backward; no 0 * inf)
+  const float k = (gamma == 0.f || omp == 0.f) ? w : w - gamma * powf(omp, gamma - 1.0f) * p * lp;
   for (int j = 0; j < C; ++j) {
     const float pj = expf(ld(z, j) - lse);
     dz[j] += wgt * (-a) * ((j == y ? 1.0f : 0.0f) - pj) * k;

@@ -15,8 +15,10 @@ Extra flags: --amp {bf16,fp16,fp32} (the reference's fp16 autocast + GradScaler 
 the MI355X default), --eager (no HIP graphs), --loader-threads.
 
 Differences, all documented in DESIGN.md:
-  * data-parallel: one process per GPU (RCCL); the train list is sharded per global batch, the
-    per-rank micro-batch is `batch_size`, and eval shards the protocol and all-gathers the scores;
+  * data-parallel: one process per GPU (RCCL); the train list is sharded per global micro-step; by default
+    an optimizer step keeps the reference's batch_size x accumulation_steps utterances, split over the ranks
+    (radhip.train.ddp_micro_batches; --ddp_batch per_rank gives every rank the whole recipe), and eval
+    shards the protocol and all-gathers the scores;
   * the train dataset is decoded natively and augmented on the GPU (radhip.data.TrainFeeder), with
     the reference's per-utterance host RNG order;
   * the optimizer window of `accumulation_steps` micro-batches runs as one batched clean pass plus the
@@ -51,7 +53,7 @@ from radhip.data import (Dataset_ASVspoof2019_devNeval, Dataset_ASVspoof2021_eva
 from radhip.evaluation import calculate_EER_2021, calculate_tDCF_EER  # noqa: E402
 from radhip.infer import produce_evaluation_file_sharded  # noqa: E402
 from radhip.train import (Augmenter, GraphedMicroStep, Trainer, build_criterion,  # noqa: E402
-                          swa_bn_update, total_optimizer_steps)
+                          ddp_micro_batches, swa_bn_update, total_optimizer_steps)
 from radhip.window import WindowStep, window_eligible  # noqa: E402
 
 AMP = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
@@ -242,20 +244,30 @@ class Runner:
         per-micro-batch graphs (GraphedMicroStep), or eager launches."""
         if self.args.eager or not hasattr(trainer.model, "wavlm_stream"):
             return "eager", None        # the captured steps drive the dual-stream model's device-side draws
-        if not self.args.no_window and window_eligible(trainer):
-            w = WindowStep(trainer, B)
-            for k in range(w.K):            # capture needs one staged window of draws
-                w.add(k, np.zeros(B, dtype=np.int64))
-            w.capture()
-            w.reset_host()
-            return "window", w
-        g = GraphedMicroStep(trainer, B)
-        g.capture()
-        return "graph", g
+        # capture stages a dummy window (SpecAugment, LayerDrop and band-mask draws from numpy, torch CPU and
+        # python random): put the host RNGs back afterwards, so a seeded run's first micro-batch draws what the
+        # reference's first micro-batch draws
+        rng = (random.getstate(), np.random.get_state(), torch.get_rng_state())
+        try:
+            if not self.args.no_window and window_eligible(trainer):
+                w = WindowStep(trainer, B)
+                for k in range(w.K):            # capture needs one staged window of draws
+                    w.add(k, np.zeros(B, dtype=np.int64))
+                w.capture()
+                w.reset_host()
+                return "window", w
+            g = GraphedMicroStep(trainer, B)
+            g.capture()
+            return "graph", g
+        finally:
+            random.setstate(rng[0])
+            np.random.set_state(rng[1])
+            torch.set_rng_state(rng[2])
 
     def train_epoch(self, trainer, stepper, feeder, aug):
         """One pass of train_epoch (src/main.py:998-1126) over this rank's micro-batches."""
         kind, st = stepper
+        trainer.begin_epoch()
         n_micro = len(feeder)
         K = st.K if kind == "window" else 1
         full = (n_micro // K) * K                  # micro-batches that fill whole windows
@@ -320,8 +332,16 @@ class Runner:
         self.log("no. training files:", len(file_train))
         dc = config.get("data_config", {})
         aug = Augmenter(self.device, algo=int(dc.get("rawboost_algo", 0)), rawboost_p=float(dc.get("rawboost_p", 1.0)),
-                        use_codec=str_to_bool(dc.get("use_codec_aug", "False")), codec_p=float(dc.get("codec_p", 0.5)))
+                        use_codec=str_to_bool(dc.get("use_codec_aug", "False")), codec_p=float(dc.get("codec_p", 0.5)),
+                        exact_noise=args.exact_rawboost)
         B = int(config["batch_size"])
+        if self.world > 1 and args.ddp_batch == "global":
+            # the reference's optimizer step (batch_size x accumulation_steps utterances) split over the ranks
+            glob = B * max(1, int(self.tc.get("accumulation_steps", 1)))
+            B, acc = ddp_micro_batches(B, self.tc.get("accumulation_steps", 1), self.world)
+            self.tc["accumulation_steps"] = acc
+            self.log(f"[DDP] global batch {glob} per optimizer step: per-rank micro-batch {B} x accumulation {acc} "
+                     f"x {self.world} ranks")
         feeder = TrainFeeder(file_train, d_label_trn, self.database_path / "ASVspoof2019_{}_train/".format(self.track),
                              B, aug, args.seed, threads=self.threads, rank=self.rank, world=self.world)
         if len(feeder) == 0:
@@ -503,6 +523,13 @@ def parse_args(argv=None):
                              "exact --resume")
     parser.add_argument("--loader-threads", dest="loader_threads", type=int, default=8,
                         help="host threads of the native FLAC batch decoder")
+    parser.add_argument("--ddp_batch", default="global", choices=["global", "per_rank"],
+                        help="data parallel: 'global' keeps the reference's batch_size x accumulation_steps utterances "
+                             "per optimizer step split over the ranks (default); 'per_rank' gives every rank "
+                             "batch_size x accumulation_steps (weak scaling, as bench.py)")
+    parser.add_argument("--exact_rawboost", action="store_true",
+                        help="draw the RawBoost ISD / SSI noise with the reference's numpy calls (randn / choice per "
+                             "sample) instead of one Philox seed per call")
     return parser.parse_args(argv)
 
 

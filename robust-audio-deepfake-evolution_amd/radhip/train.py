@@ -228,9 +228,14 @@ class Augmenter:
     (Dataset_ASVspoof2019_train.__getitem__, data_utils.py:163-184), executed as one batched kernel
     per stage on the GPU, then pad_random/tile + mixup gather into the [B, 64600] model input."""
 
-    def __init__(self, device, algo=0, rawboost_p=1.0, use_codec=False, codec_p=0.5, max_len=MAX_LEN):
+    def __init__(self, device, algo=0, rawboost_p=1.0, use_codec=False, codec_p=0.5, max_len=MAX_LEN,
+                 exact_noise=False):
         self.device = torch.device(device)
         self.algo, self.rawboost_p = int(algo), float(rawboost_p)
+        # exact_noise: the ISD / SSI noise is the reference's own numpy draws (randn / choice per sample,
+        # src/rawboost.py:66-95), uploaded per micro-batch; otherwise one numpy seed per call keys a device
+        # Philox stream (the bench and the default train path)
+        self.exact_noise = bool(exact_noise)
         self.use_codec, self.codec_p = bool(use_codec), float(codec_p)
         self.max_len = max_len
         self.algo_ids = [1, 2, 3, 4] if self.algo == 5 else [self.algo]
@@ -245,7 +250,8 @@ class Augmenter:
 
     # --- host draws (mirror rawboost.py / data_utils.py draw order; per-sample noise -> Philox seed)
     def _draw_rawboost(self, n):
-        return draw_rawboost(n, self.algo_ids[np.random.randint(0, len(self.algo_ids))])
+        """The record, or (record, isd noise, ssi noise) with exact_noise."""
+        return draw_rawboost(n, self.algo_ids[np.random.randint(0, len(self.algo_ids))], exact=self.exact_noise)
 
     def codec_len(self, n, sr):
         _, _, ogd, ngd = self.kinfo[(16000, sr)]
@@ -285,15 +291,28 @@ class Augmenter:
             acc += int(n)
         cur_lens = list(lens)
         packed = work
-        recs = []
+        recs, isd, ssi = [], None, None
         for b, (rec, _, _) in enumerate(plan):
+            if isinstance(rec, tuple):          # exact_noise draws: (record, isd noise*mask, ssi noise)
+                rec, nm, nz = rec
+                for arr, name in ((nm, "isd"), (nz, "ssi")):
+                    if arr is None:
+                        continue
+                    if name == "isd":
+                        isd = np.zeros(total) if isd is None else isd
+                        isd[offs[b]:offs[b] + lens[b]] = arr
+                    else:
+                        ssi = np.zeros(total) if ssi is None else ssi
+                        ssi[offs[b]:offs[b] + lens[b]] = arr
             r = rec if rec is not None else _lib.RawboostUtt()
             r.offset, r.len = int(offs[b]), int(lens[b])
             if rec is None:
                 r.algo = 0
             recs.append(r)
         if any(r.algo != 0 for r in recs):
-            work = rawboost_batch(packed, recs)
+            work = rawboost_batch(packed, recs,
+                                  noise_isd=None if isd is None else torch.from_numpy(isd).to(self.device),
+                                  noise_ssi=None if ssi is None else torch.from_numpy(ssi).to(self.device))
         codec = [(b, sr) for b, (_, sr, _) in enumerate(plan) if sr is not None]
         if codec:
             jobs_d, jobs_u, mid_off, out_off = [], [], 0, 0
@@ -385,7 +404,8 @@ class Trainer:
         self.ema = EMA(model, tc.get("ema_decay", 0.999)) if tc.get("use_ema", False) else None
         self.grads = FlatGrads(model.parameters())
         self.params = self.grads.params
-        self.micro = 0
+        self.micro = 0              # micro-batches since construction (resume state)
+        self.epoch_micro = 0        # micro-batches of the current epoch: the reference's i + 1 (begin_epoch)
         self.loss_sum = torch.zeros((), device=self.device, dtype=torch.float64)
         self.n_seen = 0
 
@@ -425,6 +445,17 @@ class Trainer:
             if drop:
                 core._cnn_feats = None
 
+    def begin_epoch(self):
+        """train_epoch's loop index restarts every epoch (src/main.py:1030): the optimizer steps when
+        (i + 1) % accumulation_steps == 0 or at the epoch's last micro-batch (:1100), counted per epoch."""
+        self.epoch_micro = 0
+
+    def count_micro(self, n=1, last_in_epoch=False):
+        """Account n micro-batches; True when the optimizer steps after them (the reference's do_step)."""
+        self.micro += n
+        self.epoch_micro += n
+        return self.epoch_micro % self.accum == 0 or last_in_epoch
+
     def micro_step(self, x, y, lam=1.0, perm=None, last_in_epoch=False):
         """One micro-batch: x [B, 64600] already mixed (perm/lam are those used for the mix)."""
         self.train_mode()
@@ -441,11 +472,10 @@ class Trainer:
             self.scaler.scale(adv).backward()
             self.fgm.restore()
         self.cnn_reuse(None, drop=True)
-        self.micro += 1
         B = x.shape[0]
         self.loss_sum += loss.detach().double() * self.accum * B
         self.n_seen += B
-        if self.micro % self.accum == 0 or last_in_epoch:
+        if self.count_micro(1, last_in_epoch):
             self.optimizer_step()
         return loss
 
@@ -498,6 +528,7 @@ def swa_bn_update(model, feeder, augmenter, device):
         return 0
     was_training = model.training
     momenta = {}
+    tracked0 = {m: m.num_batches_tracked.clone() for m in bns if m.num_batches_tracked is not None}
     for m in bns:
         m.running_mean.zero_()      # in place: captured HIP graphs keep pointing at the same buffers
         m.running_var.fill_(1.0)
@@ -519,6 +550,24 @@ def swa_bn_update(model, feeder, augmenter, device):
         n += b
     for m in bns:
         m.momentum = momenta[m]
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        # each rank averaged its own shard: the cumulative averages combine weighted by the ranks' sample
+        # counts into the average over the whole train set, as the reference's single-process pass computes
+        cnt = torch.tensor([float(n)], dtype=torch.float64, device=bns[0].running_mean.device)
+        dist.all_reduce(cnt)
+        total = float(cnt.item())
+        for m in bns:
+            st = torch.cat([m.running_mean.double(), m.running_var.double()]) * float(n)
+            dist.all_reduce(st)
+            st /= max(total, 1.0)
+            c = m.running_mean.numel()
+            m.running_mean.copy_(st[:c])
+            m.running_var.copy_(st[c:])
+            if m.num_batches_tracked is not None:       # batches counted by this pass, over all ranks
+                nb = m.num_batches_tracked - tracked0[m]
+                dist.all_reduce(nb)
+                m.num_batches_tracked.copy_(tracked0[m] + nb)
+        n = int(total)
     model.train(was_training)
     return n
 
@@ -719,10 +768,28 @@ class GraphedMicroStep:
             self._fgm()
             self.graphs[1].replay()
             self._restore()
-        tr.micro += 1
         tr.n_seen += self.B
-        if tr.micro % tr.accum == 0 or last_in_epoch:
+        if tr.count_micro(1, last_in_epoch):
             tr.optimizer_step()
+
+
+def ddp_micro_batches(batch_size, accum, world):
+    """Per-rank (micro-batch, accumulation) that keeps the reference's global batch under data parallelism
+    (SURVEY.md §8e): one optimizer step sees batch_size * accum utterances (src/main.py:1100-1117; 8 x 4 = 32
+    for Phase 6) split evenly over `world` ranks, the per-rank micro-batch as large as possible (at most
+    batch_size, mixup permutes within it) and at least 2 (mixup is skipped at B = 1, src/main.py:1038).
+    1-4 ranks: 8 x 4/world; 8 ranks: 4 x 1."""
+    batch_size, accum, world = int(batch_size), max(1, int(accum)), max(1, int(world))
+    if world == 1:
+        return batch_size, accum
+    glob = batch_size * accum
+    if glob % world:
+        raise ValueError(f"global batch {batch_size} x {accum} = {glob} does not split over {world} ranks")
+    share = glob // world
+    for b in range(min(batch_size, share), 1, -1):
+        if share % b == 0:
+            return b, share // b
+    raise ValueError(f"{share} utterances per rank and step: a per-rank micro-batch of at least 2 is needed")
 
 
 def total_optimizer_steps(num_epochs, micro_batches_per_epoch, accum):

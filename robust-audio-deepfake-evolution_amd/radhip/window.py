@@ -422,7 +422,7 @@ class WindowStep:
                 self._clean_pass()
                 self._adv_chain(self._adv_pass)
             self._unbind()
-        tr.micro += self.K
+        tr.count_micro(self.K)      # a whole window: K micro-batches, then the step (epoch_micro % K == 0)
         tr.n_seen += self.N
         tr.optimizer_step()
         self.reset_host()

@@ -49,11 +49,13 @@ def test_mixup_focal_matches_module(mode, dtype, K):
     np.testing.assert_allclose(g, r, rtol=tol, atol=tol * float(np.abs(r).max()))
 
 
-def test_mixup_focal_upstream_scale_and_confident_rows():
-    """p -> 1 rows give (1 - p)^gamma = 0 (no NaN), and the backward scales by the upstream gradient."""
+@pytest.mark.parametrize("gamma", [2.5, 0.0])
+def test_mixup_focal_upstream_scale_and_confident_rows(gamma):
+    """p -> 1 rows give (1 - p)^gamma = 0 (no NaN), also at gamma = 0 where the (1 - p)^(gamma - 1) term is
+    0 * inf in fp32; and the backward scales by the upstream gradient."""
     from radhip.ops import mixup_focal
     from radhip.train import FocalLoss
-    focal = FocalLoss(0.9, 2.5)
+    focal = FocalLoss(0.9, gamma)
     z = torch.tensor([[40.0, -40.0], [-40.0, 40.0], [0.3, -0.2], [1.0, 1.0]], device=DEV)
     ya = torch.tensor([0, 1, 1, 0], device=DEV)
     lam = torch.ones(1, device=DEV)

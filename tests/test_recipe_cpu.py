@@ -1,0 +1,220 @@
+"""Training-recipe semantics on CPU: the per-epoch optimizer-step boundaries of train_epoch
+(src/main.py:1030,1100), the data-parallel global batch of SURVEY.md §8e (src/main.py:1100-1117: one step
+= batch_size x accumulation_steps utterances), and the SWA BatchNorm refresh over sharded ranks
+(torchcontrib bn_update after swap_swa_sgd, src/main.py:669-672). gloo, world size 2."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class Toy(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.feature_projection = torch.nn.Linear(6, 5)
+        self.body = torch.nn.Linear(5, 4)
+        self.classifier = torch.nn.Linear(4, 2)
+
+    def forward(self, x, Freq_aug=False):
+        h = torch.tanh(self.body(torch.tanh(self.feature_projection(x))))
+        return h, self.classifier(h)
+
+
+CFG = {"loss": "Focal", "freq_aug": "False",
+       "optim_config": {"base_lr": 5e-3, "wavlm_lr": 1e-2, "weight_decay": 1e-4, "scheduler": "cosine",
+                        "scheduler_config": {"eta_min": 1e-6}},
+       "training_config": {"use_mixup": False, "accumulation_steps": 4, "use_ema": True, "ema_decay": 0.9,
+                           "use_fgm": False, "warmup_steps": 1, "warmup_init_factor": 0.1,
+                           "freeze_bn": True, "focal_alpha": 0.9, "focal_gamma": 2.5}}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _trainer(accum, total_steps, init):
+    import copy
+    from radhip.train import Trainer
+    m = Toy()
+    m.load_state_dict(init)
+    cfg = copy.deepcopy(CFG)
+    cfg["training_config"]["accumulation_steps"] = accum
+    groups = [{"params": list(m.feature_projection.parameters()), "lr": 1e-2},
+              {"params": list(m.body.parameters()) + list(m.classifier.parameters()), "lr": 5e-3}]
+    return m, Trainer(m, cfg, "cpu", total_steps=total_steps, amp_dtype=torch.float32, param_groups=groups)
+
+
+def _reference_steps(n_micro, accum, epochs):
+    """The micro-batch indices after which the reference's train_epoch steps, per epoch (src/main.py:1100)."""
+    return [[i for i in range(n_micro) if (i + 1) % accum == 0 or i + 1 == n_micro] for _ in range(epochs)]
+
+
+def test_optimizer_steps_restart_every_epoch():
+    """7 micro-batches per epoch with accumulation 4 (7 % 4 == 3): the reference steps after micro-batch 3 and
+    after the last one, in every epoch. A counter that ran on across epochs would step after 3, 6, 7(=i 0 of
+    epoch 1), ... and overrun the cosine schedule sized for 2 steps per epoch."""
+    torch.manual_seed(1)
+    init = {k: v.clone() for k, v in Toy().state_dict().items()}
+    n_micro, accum, epochs = 7, 4, 3
+    from radhip.train import total_optimizer_steps
+    m, tr = _trainer(accum, total_optimizer_steps(epochs, n_micro, accum), init)
+    steps, cur = [], {}
+    real = tr.optimizer_step
+
+    def spy():
+        steps[-1].append(cur["i"])
+        real()
+    tr.optimizer_step = spy
+    rng = np.random.default_rng(0)
+    for _ in range(epochs):
+        tr.begin_epoch()
+        steps.append([])
+        for i in range(n_micro):
+            cur["i"] = i
+            x = torch.from_numpy(rng.standard_normal((4, 6)).astype(np.float32))
+            y = torch.from_numpy(rng.integers(0, 2, 4))
+            tr.micro_step(x, y, last_in_epoch=(i + 1 == n_micro))
+    assert steps == _reference_steps(n_micro, accum, epochs)
+    assert tr.sched.last_epoch == total_optimizer_steps(epochs, n_micro, accum)
+
+
+def test_ddp_micro_batches():
+    from radhip.train import ddp_micro_batches
+    assert ddp_micro_batches(8, 4, 1) == (8, 4)
+    assert ddp_micro_batches(8, 4, 2) == (8, 2)
+    assert ddp_micro_batches(8, 4, 4) == (8, 1)
+    assert ddp_micro_batches(8, 4, 8) == (4, 1)          # the 8 x MI355X Phase-6 recipe
+    assert ddp_micro_batches(8, 1, 4) == (2, 1)
+    assert ddp_micro_batches(24, 1, 8) == (3, 1)
+    with pytest.raises(ValueError):
+        ddp_micro_batches(8, 4, 3)                       # 32 does not split over 3 ranks
+    with pytest.raises(ValueError):
+        ddp_micro_batches(8, 1, 8)                       # 1 utterance per rank: mixup needs >= 2
+
+
+def _feeder_chunks(n_keys, B, world, rank, order):
+    """TrainFeeder.epoch's split (radhip/data.py): global micro-step i covers order[i*B*world:(i+1)*B*world],
+    rank r takes its r-th block of B."""
+    gb = B * world
+    return [order[i * gb:(i + 1) * gb][rank * B:(rank + 1) * B] for i in range(n_keys // gb)]
+
+
+def _run_recipe(rank, world, xs, ys, init, batch, accum, epochs):
+    from radhip.train import ddp_micro_batches, total_optimizer_steps
+    B, acc = ddp_micro_batches(batch, accum, world)
+    n = xs.shape[0]
+    n_micro = n // (B * world)
+    total = total_optimizer_steps(epochs, n_micro, acc)
+    m, tr = _trainer(acc, total, init)
+    rng = np.random.default_rng(7)
+    for _ in range(epochs):
+        order = rng.permutation(n).tolist()
+        tr.begin_epoch()
+        chunks = _feeder_chunks(n, B, world, rank, order)
+        for i, idx in enumerate(chunks):
+            tr.micro_step(torch.from_numpy(xs[idx]), torch.from_numpy(ys[idx]), last_in_epoch=(i + 1 == len(chunks)))
+    return ({k: v.detach().clone() for k, v in m.state_dict().items()}, tr.ema.state_dict(), total,
+            tr.sched.last_epoch, [pg["lr"] for pg in tr.opt.param_groups])
+
+
+def _recipe_worker(rank, world, port, xs, ys, init, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.save(_run_recipe(rank, world, xs, ys, init, 4, 4, 2), os.path.join(out, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_global_batch_recipe_matches_single_process():
+    """Two ranks under the global-batch recipe (micro-batch 4 x accumulation 2 per rank) take the same
+    optimizer steps, over the same 16 utterances each, as one process with micro-batch 4 x accumulation 4:
+    equal schedule length, parameters, EMA and learning rates after two epochs. (Mixup and FGM are off: mixup
+    pairs within a micro-batch and the FGM chain is sequential per process, so neither splits exactly.)"""
+    rng = np.random.default_rng(3)
+    xs = rng.standard_normal((64, 6)).astype(np.float32)
+    ys = rng.integers(0, 2, 64).astype(np.int64)
+    torch.manual_seed(1)
+    init = {k: v.clone() for k, v in Toy().state_dict().items()}
+    ref = _run_recipe(0, 1, xs, ys, init, 4, 4, 2)
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_recipe_worker, args=(2, _free_port(), xs, ys, init, out), nprocs=2, join=True,
+                           start_method="spawn")
+        got = [torch.load(os.path.join(out, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    for r in range(2):
+        params, ema, total, last, lrs = got[r]
+        assert total == ref[2] == 8 and last == ref[3] == 8
+        np.testing.assert_allclose(lrs, ref[4], rtol=1e-12)
+        for k, v in ref[0].items():
+            torch.testing.assert_close(params[k], v, rtol=2e-5, atol=1e-6, msg=f"rank{r} {k}")
+        for k, v in ref[1].items():
+            torch.testing.assert_close(ema[k], v, rtol=2e-5, atol=1e-6, msg=f"rank{r} ema {k}")
+
+
+class BNNet(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.bn = torch.nn.BatchNorm1d(3)
+
+    def forward(self, x):
+        return self.bn(x)
+
+
+class _Feeder:
+    def __init__(self, batches):
+        self.batches = batches
+
+    def epoch(self):
+        return iter(range(len(self.batches)))
+
+    def load(self, i, device):
+        x = self.batches[i]
+        return x, None, [x.shape[0]], None
+
+
+class _Aug:
+    def draw(self, lens):
+        return None
+
+    def run(self, flat, offs, lens, plan):
+        return flat
+
+
+def _bn_worker(rank, world, port, batches, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from radhip.train import swa_bn_update
+        m = BNNet()
+        n = swa_bn_update(m, _Feeder(batches[rank::world]), _Aug(), "cpu")
+        torch.save({"mean": m.bn.running_mean, "var": m.bn.running_var, "nbt": m.bn.num_batches_tracked, "n": n},
+                   os.path.join(out, f"bn{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_swa_bn_update_combines_rank_shards():
+    """Each rank refreshes the BatchNorm statistics over its own shard; afterwards every rank holds the
+    statistics one process computes over all batches (the reference's single-process bn_update)."""
+    from radhip.train import swa_bn_update
+    rng = np.random.default_rng(5)
+    batches = [torch.from_numpy((rng.standard_normal((b, 3)) * [1, 2, 3] + [0, 1, -1]).astype(np.float32))
+               for b in (4, 6, 4, 2, 5, 3)]
+    ref = BNNet()
+    n_ref = swa_bn_update(ref, _Feeder(batches), _Aug(), "cpu")
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_bn_worker, args=(2, _free_port(), batches, out), nprocs=2, join=True,
+                           start_method="spawn")
+        got = [torch.load(os.path.join(out, f"bn{r}.pt"), weights_only=True) for r in range(2)]
+    for g in got:
+        assert g["n"] == n_ref == 24
+        torch.testing.assert_close(g["mean"], ref.bn.running_mean, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(g["var"], ref.bn.running_var, rtol=1e-5, atol=1e-6)
+        assert int(g["nbt"]) == int(ref.bn.num_batches_tracked) == 6

@@ -118,7 +118,10 @@ def test_window_matches_sequential_bf16_and_graph_replay(golden):
     eager, leager = _grads_window(golden, torch.bfloat16, graphs=False)
     graph, lgraph = _grads_window(golden, torch.bfloat16, graphs=True)
     e_seq = _rel(seq16, ref32)
+    # absolute cap: the bf16 rounding of this tiny model measured 5.6 % (sequential) — a kernel bug shared by
+    # both bf16 runs must not hide behind the relative bound
+    assert e_seq < 0.1, e_seq
     for got in (eager, graph):
-        assert _rel(got, ref32) < 1.5 * e_seq + 1e-3, (_rel(got, ref32), e_seq)
+        assert _rel(got, ref32) < min(1.5 * e_seq + 1e-3, 0.1), (_rel(got, ref32), e_seq)
     assert lgraph == pytest.approx(leager, rel=1e-2)
     assert leager == pytest.approx(lref, rel=1e-2)
