@@ -87,6 +87,9 @@ def parse():
                          "3 warm-up + 10 timed steps each (~8 min on 16 threads)")
     ap.add_argument("--cpu-only", action="store_true", help="run only the CPU baseline leg (no GPU)")
     ap.add_argument("--config", default="Phase6_Proposed.conf")
+    ap.add_argument("--lora-mode", default="reference", choices=["reference", "active"],
+                    help="reference: the LoRA adapters are bypassed, as the reference's HF WavLM bypasses them "
+                         "(DESIGN.md §2); active: the adapters are applied and trained")
     ap.add_argument("--eager", action="store_true",
                     help="launch the micro-step kernel by kernel instead of replaying it as HIP graphs")
     ap.add_argument("--no-window", action="store_true",
@@ -316,6 +319,7 @@ def main():
     config = load_config(args.config)
     tc = config["training_config"]
     tc["accumulation_steps"] = args.accum
+    tc["lora_mode"] = args.lora_mode
     config["batch_size"] = args.micro_batch
     amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.amp]
     model = build(config, dev, args.layerdrop)
@@ -468,7 +472,7 @@ def main():
                        "micro_batch": B, "accumulation": args.accum, "global_batch": ws * B * args.accum,
                        "seq_len": 64600, "parallelism": f"dp{ws}", "fgm": True, "mixup": True,
                        "rawboost_algo": dc.get("rawboost_algo"), "codec_p": dc.get("codec_p"),
-                       "wavlm_layerdrop": args.layerdrop, "hip_graphs": not args.eager,
+                       "wavlm_layerdrop": args.layerdrop, "lora_mode": args.lora_mode, "hip_graphs": not args.eager,
                        "window_batched_clean_passes": window is not None},
             "roofline": roof,
             "step_mfma_frac": round(value / ws * TRAIN_FLOP_PER_UTT / 2.5e15, 4),

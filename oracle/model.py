@@ -141,22 +141,40 @@ class OracleModel(nn.Module):
 
 class OLoraLinear(nn.Module):
     """peft lora.Linear as the reference injects it (src/main.py:103-158: LoraConfig(r, lora_alpha,
-    target_modules=[q_proj, v_proj], lora_dropout) + get_peft_model): base(x) + B(A(dropout(x))) * alpha / r,
-    with peft's state-dict layout (base_layer, lora_A.default, lora_B.default). Dropout is left out: the
-    oracle is compared with it off."""
+    target_modules=[q_proj, v_proj], lora_dropout) + get_peft_model), with peft's state-dict layout
+    (base_layer, lora_A.default, lora_B.default). peft's tuner layer exposes its base layer's `weight` and
+    `bias` as properties (BaseTunerLayer.weight / .bias; in peft < 0.7 the layer subclasses nn.Linear and
+    keeps the base tensors itself): transformers' WavLMAttention reads exactly those (q_proj.weight and the
+    concatenated biases go to F.multi_head_attention_forward) and never calls the layer, so in the reference
+    the adapter does not enter the forward and its weights get no gradient.
 
-    def __init__(self, base, r=8, alpha=32):
+    merged=True is the oracle of the product's lora_mode "active": `weight` returns base + (alpha/r) B A, the
+    adapter's contribution with dropout off, so HF's attention applies it."""
+
+    def __init__(self, base, r=8, alpha=32, merged=False):
         super().__init__()
         self.base_layer = base
         self.lora_A = nn.ModuleDict({"default": nn.Linear(base.in_features, r, bias=False)})
         self.lora_B = nn.ModuleDict({"default": nn.Linear(r, base.out_features, bias=False)})
         self.scaling = alpha / r
+        self.merged = merged
+
+    @property
+    def weight(self):
+        w = self.base_layer.weight
+        if self.merged:
+            w = w + self.scaling * (self.lora_B["default"].weight @ self.lora_A["default"].weight)
+        return w
+
+    @property
+    def bias(self):
+        return self.base_layer.bias
 
     def forward(self, x):
         return self.base_layer(x) + self.lora_B["default"](self.lora_A["default"](x)) * self.scaling
 
 
-def apply_lora(model, r=8, alpha=32, targets=("q_proj", "v_proj")):
+def apply_lora(model, r=8, alpha=32, targets=("q_proj", "v_proj"), merged=False):
     """Wrap every target linear of the oracle's WavLM in OLoraLinear (base weights frozen, as peft does)."""
     wl = model.wavlm_stream.model
     for p in wl.parameters():
@@ -164,7 +182,7 @@ def apply_lora(model, r=8, alpha=32, targets=("q_proj", "v_proj")):
     for layer in wl.encoder.layers:
         att = layer.attention
         for t in targets:
-            setattr(att, t, OLoraLinear(getattr(att, t), r, alpha))
+            setattr(att, t, OLoraLinear(getattr(att, t), r, alpha, merged))
     return model
 
 

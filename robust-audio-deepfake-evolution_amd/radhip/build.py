@@ -50,7 +50,15 @@ def get_model(model_config, device, extra=None):
     return model.to(device)
 
 
+LORA_MODES = ("reference", "active")
+
+
 def apply_lora_to_wavlm(model, training_config):
+    """training_config "lora_mode": "reference" (default) injects the adapters the way the reference's HF
+    WavLM ends up using them, i.e. bypassed (radhip.wavlm.LoraLinear); "active" applies them."""
+    mode = training_config.get("lora_mode", "reference")
+    if mode not in LORA_MODES:
+        raise ValueError(f"lora_mode must be one of {LORA_MODES}, got {mode!r}")
     if not training_config.get("use_lora", False):
         return model
     if not (hasattr(model, "wavlm_stream") and hasattr(model.wavlm_stream, "model")):
@@ -62,7 +70,8 @@ def apply_lora_to_wavlm(model, training_config):
         p.requires_grad = False
     wrapped, n = inject_lora(base, r=training_config.get("lora_r", 8), alpha=training_config.get("lora_alpha", 32),
                              dropout=training_config.get("lora_dropout", 0.1),
-                             targets=tuple(training_config.get("lora_target_modules", ["q_proj", "v_proj"])))
+                             targets=tuple(training_config.get("lora_target_modules", ["q_proj", "v_proj"])),
+                             active=(mode == "active"))
     if n == 0:
         raise RuntimeError("LoRA: no target modules found")
     model.wavlm_stream.model = wrapped

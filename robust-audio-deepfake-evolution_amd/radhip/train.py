@@ -402,7 +402,9 @@ class Trainer:
         self.sched_on = oc.get("scheduler", "cosine") in ("cosine", "keras_decay")
         self.scaler = torch.amp.GradScaler("cuda", enabled=(amp_dtype == torch.float16))
         self.ema = EMA(model, tc.get("ema_decay", 0.999)) if tc.get("use_ema", False) else None
-        self.grads = FlatGrads(model.parameters())
+        from .wavlm import inert_lora_params
+        inert = {id(p) for p in inert_lora_params(model)}      # bypassed adapters: no gradient, as in the reference
+        self.grads = FlatGrads([p for p in model.parameters() if id(p) not in inert])
         self.params = self.grads.params
         self.micro = 0              # micro-batches since construction (resume state)
         self.epoch_micro = 0        # micro-batches of the current epoch: the reference's i + 1 (begin_epoch)

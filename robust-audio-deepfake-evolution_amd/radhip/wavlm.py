@@ -106,10 +106,18 @@ def frozen_linear(x, lin, cache):
 class LoraLinear(nn.Module):
     """peft lora.Linear look-alike: base_layer + lora_A/lora_B/lora_dropout ModuleDicts keyed by
     adapter name ('default'); y = base(x) + (alpha/r) * B(A(dropout(x))). A ~ kaiming_uniform(a=sqrt 5),
-    B = 0 (peft's init)."""
+    B = 0 (peft's init). Like peft's layer it exposes the base layer's `weight` / `bias`.
 
-    def __init__(self, base, r=8, alpha=32, dropout=0.1, adapter="default"):
+    active=False reproduces what the reference actually computes: transformers' WavLMAttention never calls
+    q_proj / v_proj as modules, it hands `q_proj.weight` and the concatenated `.bias` to
+    F.multi_head_attention_forward (modeling_wavlm.py, torch_multi_head_self_attention), and on a peft layer
+    those are the base layer's tensors. So the adapters injected by src/main.py:103-158 never enter the
+    forward: the outputs are the base model's and the LoRA weights get no gradient (AdamW skips them).
+    active=True applies the adapter (what LoRA is meant to do; training_config "lora_mode": "active")."""
+
+    def __init__(self, base, r=8, alpha=32, dropout=0.1, adapter="default", active=True):
         super().__init__()
+        self.active = bool(active)
         self.base_layer = base
         self.in_features, self.out_features = base.in_features, base.out_features
         self.adapter = adapter
@@ -136,7 +144,7 @@ class LoraLinear(nn.Module):
         return self.lora_B[a](self.lora_A[a](self.lora_dropout[a](x))) * self.scaling[a]
 
     def forward(self, x):
-        return self.base_layer(x) + self.delta(x)
+        return self.base_layer(x) + self.delta(x) if self.active else self.base_layer(x)
 
 
 def _base(lin):
@@ -311,11 +319,11 @@ class Attention(nn.Module):
             qq, kk, vv = qkv.split(E, dim=-1)
         else:
             qq, kk, vv = bq(h), bk(h), bv(h)
-        if isinstance(q, LoraLinear):
+        if isinstance(q, LoraLinear) and q.active:
             qq = qq + q.delta(h)
-        if isinstance(k, LoraLinear):
+        if isinstance(k, LoraLinear) and k.active:
             kk = kk + k.delta(h)
-        if isinstance(v, LoraLinear):
+        if isinstance(v, LoraLinear) and v.active:
             vv = vv + v.delta(h)
         return qq, kk, vv
 
@@ -580,16 +588,26 @@ class PeftWrapped(nn.Module):
         return self.base_model.model(*a, **k)
 
 
-def inject_lora(model, r=8, alpha=32, dropout=0.1, targets=("q_proj", "v_proj")):
+def inject_lora(model, r=8, alpha=32, dropout=0.1, targets=("q_proj", "v_proj"), active=True):
     """Replace every nn.Linear whose attribute name is in `targets` by a LoraLinear (peft semantics:
     base frozen by the caller, LoRA trainable). Returns the wrapped model and the adapter count."""
     n = 0
     for mod in list(model.modules()):
         for name, child in list(mod.named_children()):
             if name in targets and isinstance(child, nn.Linear):
-                setattr(mod, name, LoraLinear(child, r, alpha, dropout))
+                setattr(mod, name, LoraLinear(child, r, alpha, dropout, active=active))
                 n += 1
     return PeftWrapped(model), n
+
+
+def inert_lora_params(model):
+    """Parameters of adapters that never enter the forward (LoraLinear.active False): trainable in name, like
+    the reference's, but they receive no gradient, so the optimizer and the gradient buffer leave them out."""
+    out = []
+    for mod in model.modules():
+        if isinstance(mod, LoraLinear) and not mod.active:
+            out += list(mod.lora_A.parameters()) + list(mod.lora_B.parameters())
+    return out
 
 
 def remap_peft_keys(state_dict, model_keys):

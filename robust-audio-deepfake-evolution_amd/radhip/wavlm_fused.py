@@ -46,6 +46,10 @@ def _lora_parts(attn):
         return "unsupported"
     if not isinstance(q, LoraLinear):
         return None
+    if not q.active and not v.active:
+        return None                 # bypassed adapters (the reference's HF WavLM): the plain q/k/v GEMM
+    if q.active != v.active:
+        return "unsupported"
     r = q.r[q.adapter]
     if r != 8 or v.r[v.adapter] != 8 or q.scaling[q.adapter] != v.scaling[v.adapter]:
         return "unsupported"
@@ -69,8 +73,9 @@ def eligible(encoder, h):
             ok = False
             break
         lora_params = set()
-        if lp is not None:
-            for ad in lp:
+        from .wavlm import LoraLinear
+        for ad in (layer.attention.q_proj, layer.attention.v_proj):
+            if isinstance(ad, LoraLinear):      # active or bypassed: their gradients never come from autograd here
                 lora_params |= {id(p) for p in ad.lora_A.parameters()} | {id(p) for p in ad.lora_B.parameters()}
         if any(p.requires_grad and id(p) not in lora_params for p in layer.parameters()):
             ok = False
@@ -80,7 +85,9 @@ def eligible(encoder, h):
 
 
 def _trainable_signature(encoder):
-    return tuple(p.requires_grad for p in encoder.parameters())
+    from .wavlm import LoraLinear
+    return (tuple(p.requires_grad for p in encoder.parameters())
+            + tuple(m.active for m in encoder.modules() if isinstance(m, LoraLinear)))
 
 
 class _LayerCache:

@@ -32,6 +32,7 @@ def _run(golden, fgm, graphed, accum, n_micro, xs, ys):
     cfg = load_config("Phase6_Proposed.conf")
     cfg["training_config"]["accumulation_steps"] = accum
     cfg["training_config"]["lora_dropout"] = 0.0
+    cfg["training_config"]["lora_mode"] = "active"
     cfg["training_config"]["use_fgm"] = fgm
     torch.manual_seed(0)
     m = apply_lora_to_wavlm(_model(golden), cfg["training_config"])

@@ -70,6 +70,7 @@ def test_phase6_train_micro_step_bf16(golden):
     m, _ = _tiny_product(golden)
     cfg = load_config("Phase6_Proposed.conf")
     cfg["training_config"]["accumulation_steps"] = 1
+    cfg["training_config"]["lora_mode"] = "active"     # adapters applied, so they train
     m = apply_lora_to_wavlm(m, cfg["training_config"])
     before = {n: p.detach().clone() for n, p in m.named_parameters() if p.requires_grad}
     tr = Trainer(m, cfg, DEV, total_steps=10)

@@ -33,6 +33,7 @@ def _model(golden):
     m = m.to(DEV)
     cfg = load_config("Phase6_Proposed.conf")
     cfg["training_config"]["lora_dropout"] = 0.0
+    cfg["training_config"]["lora_mode"] = "active"     # the fused layer's folded LoRA columns take part
     cfg["training_config"]["accumulation_steps"] = 3
     cfg["freq_aug"] = "False"
     m = apply_lora_to_wavlm(m, cfg["training_config"])
