@@ -35,7 +35,7 @@ class OConv(nn.Module):
         self.band_pass = sinc_filterbank(70, 128, 16000)
 
     def forward(self, x, mask=None):
-        w = self.band_pass.clone().to(x.dtype)
+        w = self.band_pass.clone().to(device=x.device, dtype=x.dtype)
         if mask is not None:
             w[mask[0]:mask[1]] = 0
         return F.conv1d(x, w.view(70, 1, 129))

@@ -92,6 +92,11 @@ class Residual_block(nn.Module):
             self.conv_downsample = nn.Conv1d(nb_filts[0], nb_filts[1], padding=0, kernel_size=1, stride=1)
         self.mp = nn.MaxPool1d(3)
 
+    def dead_parameters(self):
+        """bn1's affine weights: the reference discards bn1's output (models/RawNet2Spoof.py:150-155), so they
+        never get a gradient or an optimizer step there (radhip.train.no_grad_params)."""
+        return [] if self.first else list(self.bn1.parameters())
+
     def forward(self, x):
         if not self.first and self.bn1.training:
             with torch.no_grad():           # the discarded bn1 branch: only its running-stat update survives

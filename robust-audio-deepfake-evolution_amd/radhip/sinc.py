@@ -109,6 +109,11 @@ class Residual_block(nn.Module):
             self.conv_downsample = nn.Conv2d(nb_filts[0], nb_filts[1], padding=(0, 1), kernel_size=(1, 3), stride=1)
         self.mp = nn.MaxPool2d((1, 3))
 
+    def dead_parameters(self):
+        """bn1's affine weights: the reference's forward discards bn1's output, so they never receive a
+        gradient there (AdamW skips them, weight decay included); radhip.train leaves them out likewise."""
+        return [] if self.first else list(self.bn1.parameters())
+
     def _fused_ok(self, x):
         return (x.is_cuda and not self.bn2.training and x.dim() == 4
                 and x.is_contiguous(memory_format=torch.channels_last) and self.conv2.out_channels % 8 == 0)

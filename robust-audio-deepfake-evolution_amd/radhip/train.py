@@ -72,6 +72,18 @@ def build_criterion(config, device):
     return nn.CrossEntropyLoss(weight=w, label_smoothing=tc.get("label_smoothing", 0.0))
 
 
+def no_grad_params(model):
+    """Trainable parameters the reference's forward never uses, so they never get a .grad there and AdamW (and
+    its weight decay) and clip_grad_norm_ skip them: bypassed LoRA adapters (radhip.wavlm.LoraLinear) and the
+    SincNet blocks' dead bn1 affine weights (Residual_block.dead_parameters)."""
+    from .wavlm import inert_lora_params
+    out = list(inert_lora_params(model))
+    for m in model.modules():
+        if hasattr(m, "dead_parameters"):
+            out += [p for p in m.dead_parameters() if p.requires_grad]
+    return out
+
+
 # --------------------------------------------------------------------------------- FGM -------
 class FGM:
     """FGM on parameters whose name contains `emb_name` (main.py:74-100), on the HIP kernel.
@@ -402,8 +414,7 @@ class Trainer:
         self.sched_on = oc.get("scheduler", "cosine") in ("cosine", "keras_decay")
         self.scaler = torch.amp.GradScaler("cuda", enabled=(amp_dtype == torch.float16))
         self.ema = EMA(model, tc.get("ema_decay", 0.999)) if tc.get("use_ema", False) else None
-        from .wavlm import inert_lora_params
-        inert = {id(p) for p in inert_lora_params(model)}      # bypassed adapters: no gradient, as in the reference
+        inert = {id(p) for p in no_grad_params(model)}     # never in the reference's graph: no .grad, no step
         self.grads = FlatGrads([p for p in model.parameters() if id(p) not in inert])
         self.params = self.grads.params
         self.micro = 0              # micro-batches since construction (resume state)

@@ -21,6 +21,7 @@ norm stages per pass and two passes, and the measured errors (printed by the tes
 sit at a few 1e-3 on the logits and 1-4 % relative L2 on the gradients. The asserted bounds are about 3x
 the measured values, tight enough that a wrong tile, mask or sign (O(1) errors) cannot pass.
 """
+import os
 import random
 
 import numpy as np
@@ -152,10 +153,13 @@ def test_bench_path_window_bf16_vs_fp64_oracle(lora_mode):
     assert tr.fgm is not None and tr.freq_aug
     names = {id(p): n for n, p in m.named_parameters()}
     trainable = [names[id(p)] for p in tr.grads.params]
-    w = WindowStep(tr, B, graphs=True)
-    w.add(0, np.zeros(B, dtype=np.int64))            # capture needs one staged window of draws (as bench.py)
-    w.capture()
-    w.reset_host()
+    # RADHIP_E2E_EAGER=1: the same window launched eagerly (a diagnostic for unfused A/B runs: the unfused
+    # module path is not capturable)
+    w = WindowStep(tr, B, graphs=os.environ.get("RADHIP_E2E_EAGER") != "1")
+    if w.graphs_on:
+        w.add(0, np.zeros(B, dtype=np.int64))        # capture needs one staged window of draws (as bench.py)
+        w.capture()
+        w.reset_host()
     got = []
 
     def opt_step():
@@ -208,10 +212,17 @@ def test_bench_path_window_bf16_vs_fp64_oracle(lora_mode):
         assert all(g is None for n, g in og.items() if "lora_" in n)
         og = {n: g for n, g in og.items() if "lora_" not in n}
     omap = from_peft_state({n: n for n in trainable})
+    omap_inv = {v: k for k, v in omap.items()}
+    dead = [n for n in trainable if og[omap_inv[n]] is None]     # no gradient in the reference's graph
+    print(f"[e2e {lora_mode}] trainable without a reference gradient: {dead}")
+    for n in dead:
+        assert float(grads[n].abs().max()) == 0.0, n
     groups = {}
     for n in trainable:
+        if n in dead:
+            continue
         g = _group(n)
-        a, b = grads[n].reshape(-1), og[[k for k, v in omap.items() if v == n][0]].reshape(-1)
+        a, b = grads[n].reshape(-1), og[omap_inv[n]].reshape(-1)
         ga, gb = groups.setdefault(g, ([], []))
         ga.append(a)
         gb.append(b)
