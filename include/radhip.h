@@ -394,6 +394,16 @@ int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
                   const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao,
                   const int64_t* seed_dev, int salt, float p_drop, void* stream);
 
+/* ---- bf16 MFMA GEMM of the WavLM encoder projections, LDS-DMA pipeline (csrc/wgemm.hip) ---------------
+ * Same contract as rdx_gemm_bf16 for the RDX_EPI_BIAS / _BIAS_GELU / _GELU_BWD epilogues, with K % 64 == 0;
+ * the projections and input gradients of HF WavLMEncoderLayerStableLayerNorm (src/models/DualStreamSEMamba.py:
+ * 292-439: q/k/v, out_proj, FFN1, FFN2 at M = B x 201 tokens). tile: 0 = 128 x 128, 1 = 64 x 128,
+ * 2 = 128 x 256, 3 = 64 x 256, 4 = 128 x 64, 5 = 64 x 64 output tiles; -1 = rdx_wgemm_pick(M, N, K). */
+int rdx_wgemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                   const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao,
+                   int tile, void* stream);
+int rdx_wgemm_pick(int M, int N, int K);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

@@ -225,6 +225,103 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_fwd_kernel(
   }
 }
 
+// Forward, time-segmented (the recurrence h_s = a_s h_{s-1} + b_s is linear, so it splits in time like the
+// backward's G): block = (12 channels x 16 states) x SF_SEG time segments, wave w = 4 channels (one per DPP
+// row) of segment w / 3; segment k owns the checkpoint chunks [cb_k, cb_k + cnt_k).
+//   pass A  each segment runs its steps from h = 0 and multiplies its decays: h_end = h0_local + P * h_in;
+//   combine the segment carries compose in LDS in step order;
+//   pass B  each segment re-runs its steps from the true carry-in, forms y = C.h + D u and writes the
+//           checkpoints at its chunk ends.
+// Staging: u, softplus(delta + bias) (12 channels) and B, C rows in LDS by all SF_SEG x 192 threads (4x the
+// loads in flight of a single-segment block), y staged in LDS and stored coalesced. Serial depth 2 L / SF_SEG.
+constexpr int SF_CHW = 3;
+
+template <typename T, int SF_SEG>
+__global__ __launch_bounds__(64 * SF_CHW * SF_SEG) void scan_fwd_seg_kernel(
+    const T* __restrict__ u, const T* __restrict__ delta, const float* __restrict__ A_log,
+    const T* __restrict__ Bm, const T* __restrict__ Cm, int64_t ldbc, const float* __restrict__ Dp,
+    const float* __restrict__ dt_bias, float* __restrict__ y, float* __restrict__ ckpt, int B, int L, int D) {
+  constexpr int NT = 64 * SF_CHW * SF_SEG;
+  extern __shared__ float smem[];
+  float* s_u = smem;                                   // [L][12]
+  float* s_dt = s_u + L * SCAN_DBLK;                   // [L][12]
+  float* s_y = s_dt + L * SCAN_DBLK;                   // [L][12]
+  float* s_B = s_y + L * SCAN_DBLK;                    // [L][16]
+  float* s_C = s_B + L * SCAN_N;                       // [L][16]
+  float* s_car = s_C + L * SCAN_N;                     // [SEG][192]
+  float* s_prod = s_car + SF_SEG * 64 * SF_CHW;        // [SEG][192]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int seg = wave / SF_CHW, cw = wave - seg * SF_CHW;
+  const int dl = cw * 4 + (lane >> 4), n = lane & 15;
+  const int dblk = blockIdx.x, b = blockIdx.y, dir = blockIdx.z;
+  const int d0 = dblk * SCAN_DBLK, d = d0 + dl;
+  const int64_t db = (int64_t)dir * B + b;
+  const int64_t ud_base = db * L * D;
+  const int64_t bc_base = db * L * ldbc;
+#pragma unroll 4
+  for (int i = tid; i < L * SCAN_DBLK; i += NT) {
+    const int t = i / SCAN_DBLK, c = i - t * SCAN_DBLK;
+    const int dd = d0 + c;
+    float uu = 0.f, dv = 0.f;
+    if (dd < D) {
+      const int64_t o = ud_base + (int64_t)t * D + dd;
+      uu = ld(u, o);
+      dv = softplusf_(ld(delta, o) + dt_bias[dd]);
+    }
+    s_u[i] = uu;
+    s_dt[i] = dv;
+  }
+#pragma unroll 4
+  for (int i = tid; i < L * SCAN_N; i += NT) {
+    const int t = i >> 4, j = i & 15;
+    s_B[i] = ld(Bm, bc_base + (int64_t)t * ldbc + j);
+    s_C[i] = ld(Cm, bc_base + (int64_t)t * ldbc + j);
+  }
+  __syncthreads();
+  const bool active = d < D;
+  const float A2 = active ? -__expf(A_log[d * SCAN_N + n]) * LOG2E : 0.f;
+  const float Dd = active ? Dp[d] : 0.f;
+  const int nck = (L + SCAN_CK - 1) / SCAN_CK;
+  const int base = nck / SF_SEG, rem = nck - base * SF_SEG;
+  const int cnt = base + (seg < rem ? 1 : 0);
+  const int cb = seg * base + min(seg, rem);
+  const int sbeg = cb * SCAN_CK, send = min(L, (cb + cnt) * SCAN_CK);
+  const int slot = cw * 64 + lane;
+  // ---- pass A: local state from zero and the decay product of the segment
+  {
+    float h = 0.f, prod = 1.f;
+    for (int s = sbeg; s < send; ++s) {
+      const int t = dir ? (L - 1 - s) : s;
+      const float dtv = s_dt[t * SCAN_DBLK + dl];
+      const float a = exp2f(dtv * A2);
+      h = fmaf(a, h, dtv * s_u[t * SCAN_DBLK + dl] * s_B[t * SCAN_N + n]);
+      prod *= a;
+    }
+    s_car[seg * 64 * SF_CHW + slot] = h;
+    s_prod[seg * 64 * SF_CHW + slot] = prod;
+  }
+  __syncthreads();
+  float h = 0.f;                                        // carry-in: the segments before this one, in step order
+  for (int k = 0; k < seg; ++k) h = fmaf(s_prod[k * 64 * SF_CHW + slot], h, s_car[k * 64 * SF_CHW + slot]);
+  // ---- pass B: y and the checkpoints from the true carry-in
+  for (int s = sbeg; s < send; ++s) {
+    const int t = dir ? (L - 1 - s) : s;
+    const float dtv = s_dt[t * SCAN_DBLK + dl];
+    const float uu = s_u[t * SCAN_DBLK + dl];
+    const float a = exp2f(dtv * A2);
+    h = fmaf(a, h, dtv * uu * s_B[t * SCAN_N + n]);
+    const float pv = row16_sum(s_C[t * SCAN_N + n] * h);
+    if (n == 0) s_y[t * SCAN_DBLK + dl] = fmaf(Dd, uu, pv);
+    if (((s + 1) % SCAN_CK) == 0 && (s + 1) < L && active)
+      ckpt[((db * (nck - 1) + (s / SCAN_CK)) * D + d) * SCAN_N + n] = h;
+  }
+  __syncthreads();
+  for (int i = tid; i < L * SCAN_DBLK; i += NT) {
+    const int t = i / SCAN_DBLK, c = i - t * SCAN_DBLK;
+    if (d0 + c < D) y[ud_base + (int64_t)t * D + d0 + c] = s_y[i];
+  }
+}
+
 // Backward. Per direction-step s (t = time index of step s):
 //   G_s = C_s dy_s + a_{s+1} G_{s+1};  ddt = sum_n G (A a h_{s-1} + B u);  du = sum_n G dt B + Dp dy
 //   dB_s = sum_d G dt u;  dC_s = sum_d dy h_s;  dA += G dt a h_{s-1};  dD += dy u
@@ -558,10 +655,35 @@ extern "C" int rdx_selective_scan_fwd(int dtype, const void* u, const void* delt
   if (N != SCAN_N || L > SCAN_LMAX) return RDX_EUNSUPPORTED;
   dim3 grid((D + SCAN_DBLK - 1) / SCAN_DBLK, B, dirs);
   size_t smem = sizeof(float) * ((size_t)L * SCAN_DBLK * 3 + (size_t)L * SCAN_N * 2);
-  DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(scan_fwd_kernel<T>, grid, dim3(SCAN_THREADS), smem,
-                                           as_stream(stream), (const T*)u, (const T*)delta, A_log,
-                                           (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, y, ckpt, B, L,
-                                           D));
+  static const int seg = [] {   // RADHIP_SCAN_FWD_SEG=1: the single-segment kernel (A/B measurement)
+    const char* e = getenv("RADHIP_SCAN_FWD_SEG");
+    return (e && atoi(e) == 1) ? 1 : 4;
+  }();
+  if (seg == 1) {
+    DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(scan_fwd_kernel<T>, grid, dim3(SCAN_THREADS), smem,
+                                             as_stream(stream), (const T*)u, (const T*)delta, A_log,
+                                             (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, y, ckpt, B, L,
+                                             D));
+  } else {
+    smem += sizeof(float) * 2 * 4 * 64 * SF_CHW;
+    if (smem > 160 * 1024) return RDX_EUNSUPPORTED;
+    if (smem > 64 * 1024) {
+      static bool attr_set = false;
+      if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_fwd_seg_kernel<float, 4>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e == hipSuccess)
+          e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_fwd_seg_kernel<__hip_bfloat16, 4>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+      }
+    }
+    DISPATCH_DTYPE(dtype, hipLaunchKernelGGL((scan_fwd_seg_kernel<T, 4>), grid, dim3(64 * SF_CHW * 4), smem,
+                                             as_stream(stream), (const T*)u, (const T*)delta, A_log,
+                                             (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, y, ckpt, B, L,
+                                             D));
+  }
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

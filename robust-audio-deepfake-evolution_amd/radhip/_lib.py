@@ -98,6 +98,9 @@ SIGNATURES = {
     "rdx_posconv_bwd": (c_int, [c_vp] * 4 + [c_int, c_int, c_vp]),
     "rdx_gemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
                               c_vp, c_i64, c_vp, c_int, c_f32, c_vp]),
+    "rdx_wgemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
+                               c_vp, c_i64, c_int, c_vp]),
+    "rdx_wgemm_pick": (c_int, [c_int, c_int, c_int]),
     "rdx_gemm_bf16_strided": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                                       c_vp, c_vp]),
     "rdx_fe_conv0": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_int, c_int, c_vp, c_vp]),

@@ -1102,6 +1102,46 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
 
 
+def wgemm_tile(M, N, K, epilogue=_lib.EPI_BIAS):
+    """Output tile of csrc/wgemm.hip for a WavLM encoder GEMM, or None where hipBLASLt measured faster
+    (tools/bench_wgemm.py, profiles/r03_wgemm_bench.jsonl, same random operands, one box): at B = 8 (M = 1608)
+    the 1024 x 1024 projections (out_proj and its input gradient: 10.5 vs 20-27 us, hipBLASLt picks a
+    16-tile-per-CU-starved configuration there) and FFN1 with its GELU fused (30.8 vs 32.6 us for hipBLASLt +
+    the GELU kernel); every other shape stays on hipBLASLt."""
+    if os.environ.get("RADHIP_WGEMM", "1") == "0" or K % 64 or N % 4:
+        return None
+    if M <= 2048 and N == 1024 and K == 1024 and epilogue == _lib.EPI_BIAS:
+        return 5
+    if M <= 2048 and epilogue == _lib.EPI_BIAS_GELU and K == 1024:
+        return 6
+    return None
+
+
+def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm"):
+    """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/wgemm.hip (LDS-DMA pipelined MFMA GEMM):
+    bf16 row views a, b (unit inner stride, 16-byte aligned, K % 64 == 0); returns C, or (C, gelu(C)) for
+    EPI_BIAS_GELU."""
+    _require_gpu(a, b)
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip wgemm: bf16 operands with unit inner stride required")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2 or K % 64:
+        raise ValueError(f"radhip wgemm: K {K} vs {K2} (K % 64 == 0 required)")
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
+        aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    with _timed(name, a, gemm_flops(M, N, K)):
+        check(lib().rdx_wgemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+                                   _p(bias) if bias is not None else None, int(epilogue),
+                                   _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                                   _p(aux_out) if aux_out is not None else None,
+                                   aux_out.stride(0) if aux_out is not None else 0, int(tile), _stream(a)),
+              "wgemm_bf16")
+    return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
+
+
 # ------------------------------------------------------------------- WavLM CNN feature encoder ----
 def fe_conv_weights(layers):
     """Per-layer device operands of the fused frozen CNN (csrc/featconv.hip) from the ConvLayer modules:

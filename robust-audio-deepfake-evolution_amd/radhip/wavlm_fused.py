@@ -21,8 +21,9 @@ import os
 import torch
 import torch.nn.functional as F
 
+from . import _lib
 from ._lib import check, lib
-from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, rel_bias_table
+from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, rel_bias_table, wgemm, wgemm_tile
 
 E_FUSED = 1024
 
@@ -120,6 +121,7 @@ class _LayerCache:
             self.b1 = ff.intermediate_dense.bias.to(torch.bfloat16)
             self.w2 = ff.output_dense.weight.to(torch.bfloat16)
             self.b2 = ff.output_dense.bias.to(torch.bfloat16)
+            self.woT = None         # [E_in][E_out] for the out_proj input gradient on csrc/wgemm.hip (lazy)
             self.wg = a.gru_rel_pos_linear.weight.detach().float().contiguous()
             self.bg = a.gru_rel_pos_linear.bias.detach().float().contiguous()
             self.gconst = a.gru_rel_pos_const.detach().float().reshape(-1).contiguous()
@@ -192,7 +194,10 @@ class WavLMLayerFn(torch.autograd.Function):
             check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(rel),
                                      _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse),
                                      _p(mask) if mask is not None else None, B, T, H, 64, st), "attn_fwd")
-        aout = F.linear(o, cache.wo, cache.bo)
+        if wgemm_tile(M, E, E) is not None:
+            aout = wgemm(o, cache.wo, cache.bo, tile=wgemm_tile(M, E, E))
+        else:
+            aout = F.linear(o, cache.wo, cache.bo)
         h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
         x2 = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
         mean2 = torch.empty_like(mean1)
@@ -200,9 +205,13 @@ class WavLMLayerFn(torch.autograd.Function):
         check(lib().rdx_wl_add_ln_fwd(_p(hf), _p(aout), sdp, salt + 1, float(p_hidden), _p(h2), _p(ln2.weight),
                                       _p(ln2.bias), float(ln2.eps), _p(x2), _p(mean2), _p(rstd2), M, E, st),
               "wl_add_ln_fwd")
-        u = F.linear(x2, cache.w1, cache.b1)
-        v = torch.empty_like(u)
-        check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
+        t_ffn1 = wgemm_tile(M, cache.w1.shape[0], E, _lib.EPI_BIAS_GELU)
+        if t_ffn1 is not None:                          # FFN1 + bias + GELU in one launch
+            u, v = wgemm(x2, cache.w1, cache.b1, epilogue=_lib.EPI_BIAS_GELU, tile=t_ffn1)
+        else:
+            u = F.linear(x2, cache.w1, cache.b1)
+            v = torch.empty_like(u)
+            check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
         fo = F.linear(v, cache.w2, cache.b2)
         out = torch.empty(M, E, device=dev, dtype=torch.float32)
         if chain is not None and index < chain.n - 1:
@@ -245,7 +254,12 @@ class WavLMLayerFn(torch.autograd.Function):
         ln1, ln2 = layer.layer_norm, layer.final_layer_norm
         check(lib().rdx_wl_ln_bwd(_p(dx2), E, _p(h2), _p(mean2), _p(rstd2), _p(ln2.weight), _p(g), _p(dh2), sdp,
                                   salt + 1, p_hidden, _p(daout), M, E, st), "wl_ln_bwd")
-        do = torch.mm(daout, cache.wo)
+        if wgemm_tile(M, E, E) is not None:
+            if cache.woT is None:
+                cache.woT = cache.wo.t().contiguous()
+            do = wgemm(daout, cache.woT, tile=wgemm_tile(M, E, E))
+        else:
+            do = torch.mm(daout, cache.wo)
         D = torch.empty(B, H, T, device=dev, dtype=torch.float32)
         dqkv = torch.empty(M, 3 * E, device=dev, dtype=torch.bfloat16)
         dgate = torch.empty(M, H, device=dev, dtype=torch.float32)

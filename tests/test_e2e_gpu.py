@@ -17,9 +17,12 @@ clean gradient, adversarial forward/backward, restore. Checked:
     as the reference does: src/main.py:958-995).
 
 Bounds (bf16): one bf16 rounding is 2^-9 = 0.2 % relative; the step chains ~100 rounded GEMM / attention /
-norm stages per pass and two passes, and the measured errors (printed by the test; DESIGN.md §2 quotes them)
-sit at a few 1e-3 on the logits and 1-4 % relative L2 on the gradients. The asserted bounds are about 3x
-the measured values, tight enough that a wrong tile, mask or sign (O(1) errors) cannot pass.
+norm stages per pass and two passes. Measured (r03, printed by the test):
+  reference LoRA: bf16 eval logits 9.4e-3 abs (|logit| <= 0.24), fp32 eval 4.5e-7; clean loss 0.18 %;
+                  gradients 0.9-2.9 % relative L2 (layer weights largest);
+  active LoRA:    logits 1.1e-2, fp32 4e-7; loss 0.08 %; gradients 2-6.4 % — the module path (hipBLASLt +
+                  SDPA, RADHIP_FUSED_WAVLM=0) measures the same 2-5.8 %, so it is bf16 rounding, not the kernels.
+The asserted bounds are ~3x those, tight enough that a wrong tile, mask or sign (O(1) errors) cannot pass.
 """
 import os
 import random
@@ -31,10 +34,12 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 B = 8
-LOGIT_ATOL_BF16 = 0.05
-LOSS_RTOL_BF16 = 0.02
-GRAD_REL_BF16 = {"lora": 0.08, "layer_weights": 0.08, "feature_projection": 0.08, "sinc": 0.08,
-                 "fusion": 0.08, "backbone": 0.08, "head": 0.08}
+LOGIT_ATOL_BF16 = 0.03
+LOSS_RTOL_BF16 = 0.01
+GRAD_REL_BF16 = {"reference": {"layer_weights": 0.09, "feature_projection": 0.05, "sinc": 0.08, "fusion": 0.05,
+                               "backbone": 0.05, "head": 0.04},
+                 "active": {"lora": 0.18, "layer_weights": 0.07, "feature_projection": 0.18, "sinc": 0.14,
+                            "fusion": 0.16, "backbone": 0.18, "head": 0.12}}
 
 
 def _cfg(lora_mode):
@@ -236,9 +241,9 @@ def test_bench_path_window_bf16_vs_fp64_oracle(lora_mode):
     assert e32 < 1e-3, e32
     assert e16 < LOGIT_ATOL_BF16, e16
     assert abs(losses[0] - o_loss) < LOSS_RTOL_BF16 * abs(o_loss), (losses[0], o_loss)
-    want = set(GRAD_REL_BF16) - ({"lora"} if lora_mode == "reference" else set())
-    assert set(errs) == want, errs
+    bounds = GRAD_REL_BF16[lora_mode]
+    assert set(errs) == set(bounds), errs
     for g, e in errs.items():
-        assert e < GRAD_REL_BF16[g], (g, e)
+        assert e < bounds[g], (g, e)
     assert np.isfinite(losses[1]) and abs(losses[1] - losses[0]) < 0.1 * abs(losses[0])
     assert torch.isfinite(got[1]).all()

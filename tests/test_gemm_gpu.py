@@ -88,3 +88,51 @@ def test_gemm_residual_dropout_epilogue(p):
     if p > 0:   # the mask itself is exact: dropped elements carry h unchanged
         dropped = mk == 0
         assert torch.equal(out[dropped], h[dropped])
+
+
+# ---- csrc/wgemm.hip: the LDS-DMA pipelined GEMM of the WavLM projections (every tile configuration) ----
+WG_TILES = [0, 1, 5, 6, 11, 12, 13, 14, 15, 16, 17, 18]
+
+
+@pytest.mark.parametrize("tile", WG_TILES)
+@pytest.mark.parametrize("M,N,K", [(1608, 1024, 1024), (333, 3072, 1024), (1608, 4096, 128), (64, 260, 4096)])
+def test_wgemm_bias_every_tile(tile, M, N, K):
+    """Row tails (M % tile != 0: the buffer range returns zeros past the last row), column tails, deep K."""
+    from radhip.ops import wgemm
+    a, b, bias = _ops(M, N, K, seed=tile)
+    got = wgemm(a, b, bias, tile=tile)
+    assert got.dtype == torch.bfloat16 and got.shape == (M, N)
+    assert _rel(got, a.float() @ b.float().t() + bias.float()) < 1e-2
+    assert _rel(wgemm(a, b, tile=tile), a.float() @ b.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [5, 6, 12])
+def test_wgemm_gelu_epilogues(tile):
+    from radhip import _lib
+    from radhip.ops import wgemm
+    a, b, bias = _ops(1608, 4096, 1024, seed=11)
+    u, v = wgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=tile)
+    assert _rel(u, a.float() @ b.float().t() + bias.float()) < 1e-2
+    ref_v = torch.nn.functional.gelu(u.float())
+    assert float((v.float() - ref_v.to(torch.bfloat16).float()).abs().max()) <= 2 ** -7 * float(ref_v.abs().max())
+    uu = torch.randn(1608, 4096, device=DEV).to(torch.bfloat16)
+    du = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile)
+    dv = (a.float() @ b.float().t()).to(torch.bfloat16).float()
+    x = uu.float()
+    grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    assert _rel(du, dv * grad) < 2e-2
+
+
+def test_wgemm_policy_shapes_match_hipblaslt():
+    """The shapes the fused WavLM layer routes to wgemm (radhip.ops.wgemm_tile) agree with hipBLASLt's bf16
+    result to bf16 rounding: out_proj / its input gradient and FFN1 + GELU at B = 8."""
+    from radhip import _lib
+    from radhip.ops import wgemm, wgemm_tile
+    for (N, K, epi) in ((1024, 1024, _lib.EPI_BIAS), (4096, 1024, _lib.EPI_BIAS_GELU)):
+        t = wgemm_tile(1608, N, K, epi)
+        assert t is not None
+        a, b, bias = _ops(1608, N, K, seed=N)
+        got = wgemm(a, b, bias, epilogue=epi, tile=t)
+        got = got[0] if isinstance(got, tuple) else got
+        ref = torch.nn.functional.linear(a, b, bias)
+        assert _rel(got, ref) < 1e-2

@@ -48,7 +48,10 @@ def _mamba_pair(d_model, seed):
     return ref.double(), hip.to(DEV)
 
 
-@pytest.mark.parametrize("dirs,d_model,L,B", [(1, 16, 23, 2), (2, 16, 19, 2), (2, 144, 201, 2), (1, 144, 201, 3)])
+# L covers fewer checkpoint chunks than time segments (19, 23: the segmented forward's empty segments), chunk-
+# aligned and ragged lengths, and the Phase-6 201
+@pytest.mark.parametrize("dirs,d_model,L,B", [(1, 16, 23, 2), (2, 16, 19, 2), (2, 144, 201, 2), (1, 144, 201, 3),
+                                              (2, 32, 64, 2), (2, 32, 65, 1), (2, 16, 7, 2)])
 def test_mamba_fwd_bwd_fp32(dirs, d_model, L, B):
     from oracle.mamba import bimamba_ref
     ref, hip = _mamba_pair(d_model, 100 + d_model)
