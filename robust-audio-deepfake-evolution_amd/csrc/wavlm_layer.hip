@@ -60,6 +60,25 @@ __device__ __forceinline__ void load16_bf(const __hip_bfloat16* p, float* v) {
     }
   }
 }
+// raw 16 bf16 (two 16-byte loads), unpacked later: keeps the unpack from pinning a wait between a row's loads
+struct Bf16x16 {
+  uint4 q[2];
+};
+__device__ __forceinline__ Bf16x16 load16_bf_raw(const __hip_bfloat16* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  return Bf16x16{{q[0], q[1]}};
+}
+__device__ __forceinline__ void unpack16_bf(const Bf16x16& t, float* v) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint32_t w[4] = {t.q[i].x, t.q[i].y, t.q[i].z, t.q[i].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[8 * i + 2 * j] = __uint_as_float(w[j] << 16);
+      v[8 * i + 2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+}
 __device__ __forceinline__ uint32_t bf16_bits(float f) {
   __hip_bfloat16 b = __float2bfloat16(f);
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&b));
@@ -127,12 +146,20 @@ struct GateW {
   const float* gconst;  // [H] gru_rel_pos_const
 };
 
-// gate pre-activations z[8] of this lane's head (4 lanes per head, 16 dims per lane)
-__device__ __forceinline__ void gate_z(const GateW& g, const float* x, int lane, float* z) {
+// gru_rel_pos_linear's [8, 64] weight staged once per workgroup (2 KB): every row-wave reads its 16 x 8 weights
+// from LDS instead of 512 B per lane from L2 (32 KB per token row), issued before the barrier so that the
+// staging overlaps the row's own HBM loads
+__device__ __forceinline__ void stage_gate_w(float* swg, const float* wg, int nthreads) {
+  for (int i = threadIdx.x; i < 8 * 64 / 4; i += nthreads)
+    reinterpret_cast<float4*>(swg)[i] = reinterpret_cast<const float4*>(wg)[i];
+}
+
+// gate pre-activations z[8] of this lane's head (4 lanes per head, 16 dims per lane); wg in LDS or global
+__device__ __forceinline__ void gate_z(const GateW& g, const float* wgp, const float* x, int lane, float* z) {
   const int part = lane & 3;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float4* w = reinterpret_cast<const float4*>(g.wg + j * 64 + part * 16);
+    const float4* w = reinterpret_cast<const float4*>(wgp + j * 64 + part * 16);
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -194,30 +221,35 @@ __device__ __forceinline__ void lds16_bf(const __hip_bfloat16* p, float* v) { lo
 template <bool kLora>
 __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
   __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[kLora ? WL_R2 * WL_E : 8];
-  if (kLora) stage_lora_a(sA, a.Aq, a.Av);
+  __shared__ __attribute__((aligned(16))) float swg[8 * 64];
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * WL_LN1_ROWS + (threadIdx.x >> 6);
-  const bool live = m < a.M;  // no early return: the LoRA part follows a barrier
+  const bool live = m < a.M;  // no early return: the gate and LoRA parts follow a barrier
   const int e0 = lane * WL_VPL;
-  float v[WL_VPL];
+  float v[WL_VPL], gm[WL_VPL], bt[WL_VPL], dl[WL_VPL];
+  Bf16x16 dlr;
+  const uint64_t sr = (a.h2 && a.dres.thr) ? attn_seed(a.dres.seed_dev, a.dres.salt) : 0;  // with the row loads
+  // every global load of the row first (one HBM round trip), the affine parameters with them
   if (live) {
-    float gm[WL_VPL], bt[WL_VPL];
+    load16(a.h2 ? a.h2 + m * WL_E + e0 : a.h + m * WL_E + e0, v);
+    if (a.h2) dlr = load16_bf_raw(a.delta + m * WL_E + e0);
+    load16(a.gamma + e0, gm);
+    load16(a.beta + e0, bt);
+  }
+  stage_gate_w(swg, a.g.wg, WL_LN1_THREADS);
+  if (kLora) stage_lora_a(sA, a.Aq, a.Av);
+  __syncthreads();
+  if (live) {
     if (a.h2) {
-      float dl[WL_VPL];
-      load16(a.h2 + m * WL_E + e0, v);
-      load16_bf(a.delta + m * WL_E + e0, dl);
-      const uint64_t sr = a.dres.thr ? attn_seed(a.dres.seed_dev, a.dres.salt) : 0;
+      unpack16_bf(dlr, dl);
+
 #pragma unroll
       for (int i = 0; i < WL_VPL; ++i)
         v[i] += dl[i] * (a.dres.thr ? drop_scale(a.dres, sr, (uint64_t)m * WL_E + e0 + i) : 1.0f);
       store16(a.hout + m * WL_E + e0, v);
-    } else {
-      load16(a.h + m * WL_E + e0, v);
     }
     float mean, rstd;
     row_stats(v, a.eps, mean, rstd);
-    load16(a.gamma + e0, gm);
-    load16(a.beta + e0, bt);
 #pragma unroll
     for (int i = 0; i < WL_VPL; ++i) v[i] = bf16_round((v[i] - mean) * rstd * gm[i] + bt[i]);
     store16_bf(a.x1 + m * a.ldx + e0, v);
@@ -226,7 +258,7 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
       a.rstd[m] = rstd;
     }
     float z[8];
-    gate_z(a.g, v, lane, z);
+    gate_z(a.g, swg, v, lane, z);
     if ((lane & 3) == 0) {
       const int head = lane >> 2;
       float ga = sigmoidf_(z[0] + z[1] + z[2] + z[3]);
@@ -235,7 +267,6 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
     }
   }
   if (kLora) {
-    __syncthreads();
     if (!live) return;
     const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
     const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
@@ -284,7 +315,10 @@ __global__ __launch_bounds__(256) void wl_add_ln_fwd_kernel(AddLnArgs a) {
   const int e0 = lane * WL_VPL;
   float v[WL_VPL], dl[WL_VPL], gm[WL_VPL], bt[WL_VPL];
   load16(a.h + m * WL_E + e0, v);
-  load16_bf(a.delta + m * WL_E + e0, dl);
+  const Bf16x16 dlr = load16_bf_raw(a.delta + m * WL_E + e0);
+  load16(a.gamma + e0, gm);   // with the row's loads: one round trip
+  load16(a.beta + e0, bt);
+  unpack16_bf(dlr, dl);
   const uint64_t seed = a.d.thr ? attn_seed(a.d.seed_dev, a.d.salt) : 0;
 #pragma unroll
   for (int i = 0; i < WL_VPL; ++i)
@@ -292,8 +326,6 @@ __global__ __launch_bounds__(256) void wl_add_ln_fwd_kernel(AddLnArgs a) {
   store16(a.h2 + m * WL_E + e0, v);
   float mean, rstd;
   row_stats(v, a.eps, mean, rstd);
-  load16(a.gamma + e0, gm);
-  load16(a.beta + e0, bt);
 #pragma unroll
   for (int i = 0; i < WL_VPL; ++i) v[i] = (v[i] - mean) * rstd * gm[i] + bt[i];
   store16_bf(a.x + m * WL_E + e0, v);
@@ -413,20 +445,20 @@ __global__ __launch_bounds__(256) void wl_ln_bwd_kernel(LnBwdArgs a) {
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= a.M) return;
   const int e0 = lane * WL_VPL;
-  float dx[WL_VPL], x[WL_VPL], gm[WL_VPL], o[WL_VPL];
-  load16_bf(a.dx + m * a.ldd + e0, dx);
+  float dx[WL_VPL], x[WL_VPL], gm[WL_VPL], o[WL_VPL], r[WL_VPL];
+  const uint64_t seed = (a.ddrop && a.d.thr) ? attn_seed(a.d.seed_dev, a.d.salt) : 0;
+  const Bf16x16 dxr = load16_bf_raw(a.dx + m * a.ldd + e0);
   load16(a.h + m * WL_E + e0, x);
   load16(a.gamma + e0, gm);
+  if (a.dres) load16(a.dres + m * WL_E + e0, r);     // every load of the row before the reductions
+  unpack16_bf(dxr, dx);
   ln_bwd_row(dx, x, a.mean[m], a.rstd[m], gm, o);
   if (a.dres) {
-    float r[WL_VPL];
-    load16(a.dres + m * WL_E + e0, r);
 #pragma unroll
     for (int i = 0; i < WL_VPL; ++i) o[i] += r[i];
   }
   store16(a.dh + m * WL_E + e0, o);
   if (a.ddrop) {
-    const uint64_t seed = a.d.thr ? attn_seed(a.d.seed_dev, a.d.salt) : 0;
 #pragma unroll
     for (int i = 0; i < WL_VPL; ++i)
       o[i] *= a.d.thr ? drop_scale(a.d, seed, (uint64_t)m * WL_E + e0 + i) : 1.0f;
@@ -465,37 +497,46 @@ struct Ln1BwdArgs {
 template <bool kLora>
 __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
   __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[kLora ? WL_R2 * WL_E : 8];
-  if (kLora) {
-    stage_lora_a(sA, a.Aq, a.Av);
-    __syncthreads();
-  }
+  __shared__ __attribute__((aligned(16))) float swg[8 * 64];
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * WL_LN1_ROWS + (threadIdx.x >> 6);
-  if (m >= a.M) return;  // after the only barrier
+  const bool live = m < a.M;
   const int e0 = lane * WL_VPL;
   const int part = lane & 3, head = lane >> 2;
-  float x[WL_VPL], x1[WL_VPL], dx[WL_VPL];
-  load16(a.h + m * WL_E + e0, x);
-  const float mean = a.mean[m], rstd = a.rstd[m];
-  {
-    float gm[WL_VPL], bt[WL_VPL];
+  // every row load first: h, dx1, the residual gradient, the layer-sum gradient, the affine parameters
+  float x[WL_VPL], x1[WL_VPL], dx[WL_VPL], r[WL_VPL], sgv[WL_VPL], gm[WL_VPL];
+  float mean = 0.f, rstd = 0.f, dg = 0.f;
+  Bf16x16 dxr;
+  const uint64_t sp = (a.ddrop && a.dprev.thr) ? attn_seed(a.dprev.seed_dev, a.dprev.salt) : 0;
+  if (live) {
+    load16(a.h + m * WL_E + e0, x);
+    dxr = load16_bf_raw(a.dx1 + m * a.ldx + e0);
+    load16(a.dres + m * WL_E + e0, r);
+    if (a.sg) load16(a.sg + m * WL_E + e0, sgv);
     load16(a.gamma + e0, gm);
-    load16(a.beta + e0, bt);
-#pragma unroll
-    for (int i = 0; i < WL_VPL; ++i) x1[i] = bf16_round((x[i] - mean) * rstd * gm[i] + bt[i]);
+    load16(a.beta + e0, x1);
+    mean = a.mean[m];
+    rstd = a.rstd[m];
+    dg = a.dgate[m * (WL_E / 64) + head];
   }
-  load16_bf(a.dx1 + m * a.ldx + e0, dx);
+  stage_gate_w(swg, a.g.wg, WL_LN1_THREADS);
+  if (kLora) stage_lora_a(sA, a.Aq, a.Av);
+  __syncthreads();
+  if (!live) return;  // after the only barrier
+  unpack16_bf(dxr, dx);
+#pragma unroll
+  for (int i = 0; i < WL_VPL; ++i) x1[i] = bf16_round((x[i] - mean) * rstd * gm[i] + x1[i]);
   // gate: gate = ga (gb c - 1) + 2
   float z[8];
-  gate_z(a.g, x1, lane, z);
+  gate_z(a.g, swg, x1, lane, z);
   const float ga = sigmoidf_(z[0] + z[1] + z[2] + z[3]), gb = sigmoidf_(z[4] + z[5] + z[6] + z[7]);
-  const float c = a.g.gconst[head], dg = a.dgate[m * (WL_E / 64) + head];
+  const float c = a.g.gconst[head];
   const float dza = dg * (gb * c - 1.0f) * ga * (1.0f - ga);
   const float dzb = dg * ga * c * gb * (1.0f - gb);
 #pragma unroll 2
   for (int j = 0; j < 8; ++j) {
     const float dz = j < 4 ? dza : dzb;
-    const float4* w = reinterpret_cast<const float4*>(a.g.wg + j * 64 + part * 16);
+    const float4* w = reinterpret_cast<const float4*>(swg + j * 64 + part * 16);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float4 t = w[i];
@@ -541,21 +582,17 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a
       for (int i = 0; i < WL_VPL; ++i) dx[i] += acc[i] * drop_scale(dd, sd, (uint64_t)m * WL_E + e0 + i);
     }
   }
-  float o[WL_VPL], r[WL_VPL], gm[WL_VPL];
-  load16(a.gamma + e0, gm);  // reloaded (L1): keeps it out of the registers live across the LoRA loop
+  float o[WL_VPL];
   ln_bwd_row(dx, x, mean, rstd, gm, o);
-  load16(a.dres + m * WL_E + e0, r);
 #pragma unroll
   for (int i = 0; i < WL_VPL; ++i) o[i] += r[i];
   if (a.sg) {
     const float pw = a.sw[0];
-    load16(a.sg + m * WL_E + e0, r);
 #pragma unroll
-    for (int i = 0; i < WL_VPL; ++i) o[i] = fmaf(pw, r[i], o[i]);
+    for (int i = 0; i < WL_VPL; ++i) o[i] = fmaf(pw, sgv[i], o[i]);
   }
   store16(a.dh + m * WL_E + e0, o);
   if (a.ddrop) {
-    const uint64_t sp = a.dprev.thr ? attn_seed(a.dprev.seed_dev, a.dprev.salt) : 0;
 #pragma unroll
     for (int i = 0; i < WL_VPL; ++i)
       o[i] *= a.dprev.thr ? drop_scale(a.dprev, sp, (uint64_t)m * WL_E + e0 + i) : 1.0f;
