@@ -103,6 +103,10 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   constexpr int NV = (SC_PW * XCH + SC_T - 1) / SC_T;
   char* ws = sc_lds;                          // [KH*3*CO][CI]
   char* xs = sc_lds + KH * 3 * CO * CI * 2;   // NSLOT x [SC_PW][CI]
+  // the epilogue's per-channel BN parameters (up to 5 x CO fp32) in LDS: read per output element, they were
+  // global loads ordered behind the previous group's stores (y may alias bn / c for the compiler)
+  float* sbn = reinterpret_cast<float*>(xs + NSLOT * SLOT);
+  const __hip_bfloat16* __restrict__ cpre_src = a.c;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n = blockIdx.y, p0 = blockIdx.x * SC_P;
   const int ho0 = blockIdx.z * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
@@ -120,6 +124,8 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
       if (i < KH * 3 * CO * XCH) *reinterpret_cast<uint4*>(ws + sc_off<CI>(i / XCH, i % XCH)) = wr[j];
     }
   }
+  if (a.bn && (kBnBwd || a.y2))
+    for (int i = tid; i < (kBnBwd ? 5 : 4) * CO; i += SC_T) sbn[i] = a.bn[i];
   uint4 pre[NV];
 #pragma unroll
   for (int kh = 0; kh < KH; ++kh) {
@@ -145,6 +151,18 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   for (int ho = ho0; ho < ho1; ++ho) {
     const bool more = ho + 1 < ho1;
     if (more) sc_load_row<CI>(pre, a.x, n, ho - a.ph + KH, a.H, a.W, p0);
+    // kBnBwd: this row's saved pre-activations, loaded with the next input row (before the MFMAs), not one
+    // round trip per channel group in the epilogue
+    uint2 cpre[kBnBwd ? NT : 1][4];
+    if constexpr (kBnBwd) {
+      if (p < a.W) {
+        const int64_t obase = (((int64_t)n * a.Ho + ho) * a.W + p) * CO;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) cpre[t][g] = *reinterpret_cast<const uint2*>(cpre_src + obase + t * 32 + 8 * g + 4 * h);
+      }
+    }
     sf32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -178,19 +196,26 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
           if constexpr (kBnBwd) {
-            const uint2 cc = *reinterpret_cast<const uint2*>(a.c + obase + co);
+            const uint2 cc = cpre[t][g];
             const float cv[4] = {__uint_as_float(cc.x << 16), __uint_as_float(cc.x & 0xffff0000u),
                                  __uint_as_float(cc.y << 16), __uint_as_float(cc.y & 0xffff0000u)};
+            const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
+            const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
+            const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
+            const float4 bb = *reinterpret_cast<const float4*>(sbn + 3 * CO + co);
+            const float4 is = *reinterpret_cast<const float4*>(sbn + 4 * CO + co);
+            const float pcb[4] = {cb.x, cb.y, cb.z, cb.w}, pmu[4] = {mu.x, mu.y, mu.z, mu.w};
+            const float psg[4] = {sg.x, sg.y, sg.z, sg.w}, pbb[4] = {bb.x, bb.y, bb.z, bb.w};
+            const float pis[4] = {is.x, is.y, is.z, is.w};
             float dz[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {  // the arithmetic of bnselu_bwd_kernel
-              const int ch = co + e;
-              const float zc = (cv[e] + a.bn[ch]) - a.bn[CO + ch];
-              const float xhat = zc * a.bn[4 * CO + ch];
-              const float u = fmaf(zc, a.bn[2 * CO + ch], a.bn[3 * CO + ch]);
+              const float zc = (cv[e] + pcb[e]) - pmu[e];
+              const float xhat = zc * pis[e];
+              const float u = fmaf(zc, psg[e], pbb[e]);
               const float sd = u > 0.f ? 1.0507009873554805f : 1.0507009873554805f * 1.6732632423543772f * __expf(u);
               const float du = sc_bf16(v[e]) * sd;
-              dz[e] = du * a.bn[2 * CO + ch];
+              dz[e] = du * psg[e];
               bsum[0][t][g][e] += dz[e];
               bsum[1][t][g][e] = fmaf(du, xhat, bsum[1][t][g][e]);
               bsum[2][t][g][e] += du;
@@ -200,12 +225,16 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
           }
           *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]));
           if (a.y2) {
+            const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
+            const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
+            const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
+            const float4 bb = *reinterpret_cast<const float4*>(sbn + 3 * CO + co);
+            const float pcb[4] = {cb.x, cb.y, cb.z, cb.w}, pmu[4] = {mu.x, mu.y, mu.z, mu.w};
+            const float psg[4] = {sg.x, sg.y, sg.z, sg.w}, pbb[4] = {bb.x, bb.y, bb.z, bb.w};
             float u[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {  // the arithmetic of bnselu_fwd_kernel on the bf16 conv output
-              const int c = co + e;
-              u[e] = sc_selu(fmaf((sc_bf16(v[e]) + a.bn[c]) - a.bn[CO + c], a.bn[2 * CO + c], a.bn[3 * CO + c]));
-            }
+            for (int e = 0; e < 4; ++e)  // the arithmetic of bnselu_fwd_kernel on the bf16 conv output
+              u[e] = sc_selu(fmaf((sc_bf16(v[e]) + pcb[e]) - pmu[e], psg[e], pbb[e]));
             *reinterpret_cast<uint2*>(a.y2 + obase + co) = make_uint2(sc_pack2(u[0], u[1]), sc_pack2(u[2], u[3]));
           }
         }
@@ -434,7 +463,7 @@ __global__ void sconv_wgrad_reduce2_kernel(const float* __restrict__ part2, int6
 
 template <int CI, int CO, int KH, bool kBnBwd = false>
 static int sconv_fwd_launch(const SConvArgs& a, hipStream_t st) {
-  const size_t smem = (size_t)(KH + 1) * SC_PW * CI * 2 + (size_t)KH * 3 * CO * CI * 2;
+  const size_t smem = (size_t)(KH + 1) * SC_PW * CI * 2 + (size_t)KH * 3 * CO * CI * 2 + 5 * CO * sizeof(float);
   const int strips = (a.W + SC_P - 1) / SC_P;
   // one round of resident workgroups (256 CUs x the workgroups the LDS image allows per CU: 4 at 32 x 32
   // channels, 1 at 64 x 64): split the rows when strips x N alone is fewer (each split restages the weights
