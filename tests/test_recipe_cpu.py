@@ -218,3 +218,17 @@ def test_swa_bn_update_combines_rank_shards():
         torch.testing.assert_close(g["mean"], ref.bn.running_mean, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(g["var"], ref.bn.running_var, rtol=1e-5, atol=1e-6)
         assert int(g["nbt"]) == int(ref.bn.num_batches_tracked) == 6
+
+
+def test_step_refuses_tunableop_tuning(monkeypatch):
+    """TunableOp tuning inside the step faults the GPU on a rocBLAS candidate for the head's n=1 batched GEMM
+    (gpurun_out/tune3): WindowStep.capture refuses it up front."""
+    import pytest
+    from radhip.window import refuse_step_tuning
+    monkeypatch.delenv("PYTORCH_TUNABLEOP_ENABLED", raising=False)
+    refuse_step_tuning()
+    monkeypatch.setenv("PYTORCH_TUNABLEOP_ENABLED", "1")
+    with pytest.raises(RuntimeError, match="tune offline"):
+        refuse_step_tuning()
+    monkeypatch.setenv("PYTORCH_TUNABLEOP_TUNING", "0")
+    refuse_step_tuning()
