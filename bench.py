@@ -42,7 +42,7 @@ KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "selective_scan_fwd": (
                 "sincnet_b0_bwd": ("hbm", None), "sincnet_b0_fwd": ("hbm", None), "sconv_fwd": ("hbm", None), "sconv_wgrad": ("hbm", None),
                 "sconv_dgrad_bnselu": ("hbm", None),
                 "fe_conv0": ("hbm", None), "fe_ln_gelu": ("hbm", None), "fe_conv_gemm": ("mfma", "bf16"),
-                "gemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}
+                "gemm": ("mfma", "bf16"), "wgemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}
 TRAIN_FLOP_PER_UTT = 0.72e12                # SURVEY.md §8d (algorithmic, FGM step)
 
 

@@ -1,6 +1,7 @@
 """libradhip.so loads, exports every symbol include/radhip.h declares, and its host-only entry
 points behave (no GPU needed: argument checks return before any HIP call)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -48,3 +49,17 @@ def test_resample_kernel_matches_oracle(orig, new):
     kr, wr, ogr, ngr = sinc_kernel(orig, new)
     assert (width, og, ng) == (wr, ogr, ngr)
     np.testing.assert_allclose(k.numpy(), kr, rtol=1e-6, atol=1e-7)
+
+
+def test_bench_knows_the_bound_of_every_timed_kernel():
+    """bench.py's roofline prices the dominant kernel by KERNEL_BOUND; a kernel timed in radhip/ops.py but absent
+    there would be priced as HBM-bound bytes (round 3 found wgemm's FLOPs read as bytes)."""
+    import ast
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "robust-audio-deepfake-evolution_amd", "radhip", "ops.py")).read()
+    names = set(re.findall(r'_timed\("([a-z0-9_]+)"', src)) | set(re.findall(r'name="([a-z0-9_]*gemm)"', src))
+    tree = ast.parse(open(os.path.join(root, "bench.py")).read())
+    bound = next(ast.literal_eval(n.value) for n in tree.body
+                 if isinstance(n, ast.Assign) and getattr(n.targets[0], "id", "") == "KERNEL_BOUND")
+    assert names and names <= set(bound), sorted(names - set(bound))
