@@ -397,12 +397,26 @@ int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
 /* ---- bf16 MFMA GEMM of the WavLM encoder projections, LDS-DMA pipeline (csrc/wgemm.hip) ---------------
  * Same contract as rdx_gemm_bf16 for the RDX_EPI_BIAS / _BIAS_GELU / _GELU_BWD epilogues, with K % 64 == 0;
  * the projections and input gradients of HF WavLMEncoderLayerStableLayerNorm (src/models/DualStreamSEMamba.py:
- * 292-439: q/k/v, out_proj, FFN1, FFN2 at M = B x 201 tokens). tile: 0 = 128 x 128, 1 = 64 x 128,
- * 2 = 128 x 256, 3 = 64 x 256, 4 = 128 x 64, 5 = 64 x 64 output tiles; -1 = rdx_wgemm_pick(M, N, K). */
+ * 292-439: q/k/v, out_proj, FFN1, FFN2 at M = B x 201 tokens). tile codes (csrc/wgemm.hip wg_geometry):
+ * 0 / 6 / 14 = 128 x 128, 1 / 11 / 17 = 64 x 128, 5 = 64 x 64, 12 / 16 = 128 x 256, 13 = 256 x 128,
+ * 15 = 64 x 256, 18 = 256 x 256, 20 / 21 = 128 x 192 output tiles (4- or 8-wave, 2-4 deep LDS rings);
+ * -1 = rdx_wgemm_pick(M, N, K). The epilogue stages the tile through LDS and stores whole rows. */
 int rdx_wgemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                    const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao,
                    int tile, void* stream);
 int rdx_wgemm_pick(int M, int N, int K);
+/* Split-K form: `splits` (1 ..= K / 64) workgroups share each output tile, split s taking k-steps
+ * [s*nk/splits, (s+1)*nk/splits); each publishes an fp32 partial to `ws` and the last arriver (an agent-scope
+ * ticket in `counters`, one int per tile, zero before the first launch and left zero after each) sums the
+ * partials in split order (deterministic) and runs the epilogue. ws_bytes >= rdx_wgemm_ws_bytes(M, N, tile,
+ * splits), n_counters >= rdx_wgemm_counters(M, N, tile). One workspace per stream: two launches in flight at
+ * once must not share it. Rows of C / aux / aux_out 16-byte aligned (ld % 8 == 0) take 16-byte accesses. */
+int rdx_wgemm_bf16_ex(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
+                      int K, const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out,
+                      int64_t ldao, int tile, int splits, void* ws, int64_t ws_bytes, int* counters,
+                      int64_t n_counters, void* stream);
+int64_t rdx_wgemm_ws_bytes(int M, int N, int tile, int splits);
+int64_t rdx_wgemm_counters(int M, int N, int tile);
 
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.

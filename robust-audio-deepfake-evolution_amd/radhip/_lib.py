@@ -101,6 +101,10 @@ SIGNATURES = {
     "rdx_wgemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
                                c_vp, c_i64, c_int, c_vp]),
     "rdx_wgemm_pick": (c_int, [c_int, c_int, c_int]),
+    "rdx_wgemm_bf16_ex": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp,
+                                  c_i64, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "rdx_wgemm_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
+    "rdx_wgemm_counters": (c_i64, [c_int, c_int, c_int]),
     "rdx_gemm_bf16_strided": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                                       c_vp, c_vp]),
     "rdx_fe_conv0": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_int, c_int, c_vp, c_vp]),

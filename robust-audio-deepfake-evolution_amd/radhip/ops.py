@@ -1102,25 +1102,61 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
 
 
-def wgemm_tile(M, N, K, epilogue=_lib.EPI_BIAS):
-    """Output tile of csrc/wgemm.hip for a WavLM encoder GEMM, or None where hipBLASLt measured faster
-    (tools/bench_wgemm.py, profiles/r03_wgemm_bench.jsonl, same random operands, one box): at B = 8 (M = 1608)
-    the 1024 x 1024 projections (out_proj and its input gradient: 10.5 vs 20-27 us, hipBLASLt picks a
-    16-tile-per-CU-starved configuration there) and FFN1 with its GELU fused (30.8 vs 32.6 us for hipBLASLt +
-    the GELU kernel); every other shape stays on hipBLASLt."""
-    if os.environ.get("RADHIP_WGEMM", "1") == "0" or K % 64 or N % 4:
+# (tile, splits) of csrc/wgemm.hip per WavLM layer GEMM and token-count class; a missing entry runs on hipBLASLt.
+# Chosen in the step (rocprofv3 traces of bench.py, profiles/r03_wgemm_in_step.txt), not from standalone timings:
+# standalone (tools/bench_wgemm.py, profiles/r03_wgemm_sweep.jsonl) the B = 8 q/k/v GEMM took 17.3 us on the
+# 128 x 192 tile vs hipBLASLt's 22.7, in the step 21.3 vs 22.1 (cold weights from HBM); FFN2's input gradient
+# with the GELU backward fused took 30.9 us in the step vs 18.0 + 9.3 for hipBLASLt's 128 x 192 kernel + the
+# GELU backward, so it stays unfused. out_proj / its input gradient (64 x 64 tiles, 10.3 us vs 20-27) and FFN1 +
+# GELU (28.3 vs 32.7) run here; every B = 32 shape and the N = 1024, K = 3072 / 4096 ones stay on hipBLASLt.
+WGEMM_POLICY = {
+    "b8": {"qkv": (21, 1), "out": (5, 1), "d_out": (5, 1), "ffn1": (6, 1)},
+    "b32": {},
+}
+
+
+def wgemm_policy(name, M, N, K):
+    """(tile, splits) for the fused WavLM layer's GEMM `name` (qkv, out, ffn1, ffn2 and the input gradients
+    d_qkv, d_out, d_ffn1 (FFN1's), d_ffn2 (FFN2's, with the GELU backward fused)) at M token rows, or None for
+    hipBLASLt. RADHIP_WGEMM=0 routes everything to hipBLASLt; RADHIP_WGEMM_POLICY (JSON, same layout as
+    WGEMM_POLICY) overrides the table for A/B runs."""
+    if os.environ.get("RADHIP_WGEMM", "1") == "0" or K % 64 or N % 8:
         return None
-    if M <= 2048 and N == 1024 and K == 1024 and epilogue == _lib.EPI_BIAS:
-        return 5
-    if M <= 2048 and epilogue == _lib.EPI_BIAS_GELU and K == 1024:
-        return 6
-    return None
+    table = WGEMM_POLICY
+    env = os.environ.get("RADHIP_WGEMM_POLICY")
+    if env:
+        import json
+        table = json.loads(env)
+    ent = table.get("b8" if M <= 2048 else "b32", {}).get(name)
+    return (int(ent[0]), int(ent[1])) if ent is not None else None
 
 
-def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm"):
+_WG_WS = {}
+
+
+def _wgemm_workspace(dev, ws_bytes, n_counters):
+    """Split-K workspace of csrc/wgemm.hip: fp32 partial slabs and per-tile arrival tickets (zeroed once here;
+    the last arriver re-zeroes its ticket). One per device: every split-K launch of the product is on the
+    encoder's compute stream, one after another (graph replays included), and two launches in flight at once
+    must not share a workspace. Grown outside graph capture only: the first launch of every shape happens in
+    the eager warm-up."""
+    key = dev.index
+    cur = _WG_WS.get(key)
+    if cur is None or cur[0].numel() < ws_bytes or cur[1].numel() < n_counters:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("radhip wgemm: split-K workspace must be allocated before graph capture")
+        nb = max(ws_bytes, cur[0].numel() if cur else 0)
+        nc = max(n_counters, cur[1].numel() if cur else 0)
+        cur = (torch.empty(nb, dtype=torch.uint8, device=dev), torch.zeros(nc, dtype=torch.int32, device=dev))
+        _WG_WS[key] = cur
+    return cur
+
+
+def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm",
+          splits=1):
     """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/wgemm.hip (LDS-DMA pipelined MFMA GEMM):
     bf16 row views a, b (unit inner stride, 16-byte aligned, K % 64 == 0); returns C, or (C, gelu(C)) for
-    EPI_BIAS_GELU."""
+    EPI_BIAS_GELU. splits > 1: split-K over that many workgroups per output tile (last-arriver reduction)."""
     _require_gpu(a, b)
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
         raise ValueError("radhip wgemm: bf16 operands with unit inner stride required")
@@ -1132,12 +1168,26 @@ def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
         out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
     if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
         aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    st = _stream(a)
+    ws = cnt = None
+    ws_bytes = n_cnt = 0
+    if splits > 1:
+        if tile < 0:
+            raise ValueError("radhip wgemm: split-K needs an explicit tile")
+        ws_bytes = int(lib().rdx_wgemm_ws_bytes(M, N, int(tile), int(splits)))
+        n_cnt = int(lib().rdx_wgemm_counters(M, N, int(tile)))
+        if ws_bytes <= 0 or n_cnt <= 0:
+            raise ValueError(f"radhip wgemm: no split-K geometry for tile {tile}")
+        ws, cnt = _wgemm_workspace(a.device, ws_bytes, n_cnt)
+        ws_bytes, n_cnt = ws.numel(), cnt.numel()
     with _timed(name, a, gemm_flops(M, N, K)):
-        check(lib().rdx_wgemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
-                                   _p(bias) if bias is not None else None, int(epilogue),
-                                   _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
-                                   _p(aux_out) if aux_out is not None else None,
-                                   aux_out.stride(0) if aux_out is not None else 0, int(tile), _stream(a)),
+        check(lib().rdx_wgemm_bf16_ex(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+                                      _p(bias) if bias is not None else None, int(epilogue),
+                                      _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                                      _p(aux_out) if aux_out is not None else None,
+                                      aux_out.stride(0) if aux_out is not None else 0, int(tile), int(splits),
+                                      _p(ws) if ws is not None else None, ws_bytes,
+                                      _p(cnt) if cnt is not None else None, n_cnt, st),
               "wgemm_bf16")
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
 

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, lib
-from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, rel_bias_table, wgemm, wgemm_tile
+from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, rel_bias_table, wgemm, wgemm_policy
 
 E_FUSED = 1024
 
@@ -121,11 +121,27 @@ class _LayerCache:
             self.b1 = ff.intermediate_dense.bias.to(torch.bfloat16)
             self.w2 = ff.output_dense.weight.to(torch.bfloat16)
             self.b2 = ff.output_dense.bias.to(torch.bfloat16)
-            self.woT = None         # [E_in][E_out] for the out_proj input gradient on csrc/wgemm.hip (lazy)
+            # transposed copies for the input-gradient GEMMs on csrc/wgemm.hip (B operand [N][K]; built lazily)
+            self.woT = self.w1T = self.w2T = self.wqkvT = None
             self.wg = a.gru_rel_pos_linear.weight.detach().float().contiguous()
             self.bg = a.gru_rel_pos_linear.bias.detach().float().contiguous()
             self.gconst = a.gru_rel_pos_const.detach().float().reshape(-1).contiguous()
         self.key = key
+
+    def t(self, name):
+        """The transposed frozen weight `name` ('wo', 'w1', 'w2', 'wqkv' = the q/k/v rows without LoRA columns)."""
+        cur = getattr(self, name + "T")
+        if cur is None:
+            src = self.wext[:, :E_FUSED] if name == "wqkv" else getattr(self, name)
+            cur = src.t().contiguous()
+            setattr(self, name + "T", cur)
+        return cur
+
+
+def _gemm(name, M, N, K):
+    """(tile, splits) of csrc/wgemm.hip for the layer GEMM `name` at M tokens, or None for hipBLASLt
+    (radhip.ops.wgemm_policy)."""
+    return wgemm_policy(name, M, N, K)
 
 
 class EncoderChain:
@@ -185,7 +201,11 @@ class WavLMLayerFn(torch.autograd.Function):
                                        _p(cache.bg), _p(cache.gconst), _p(aq) if lora else None,
                                        _p(av) if lora else None, 8, sdp, salt + 3, salt + 4, float(p_lora), _p(x1),
                                        ldx, _p(gate), _p(mean1), _p(rstd1), M, E, st), "wl_ln1_fwd")
-        qkv = F.linear(x1, cache.wext, cache.bqkv)                          # [M, 3E] (LoRA folded in)
+        pol = _gemm("qkv", M, 3 * E, ldx)
+        if pol is not None:
+            qkv = wgemm(x1, cache.wext, cache.bqkv, tile=pol[0], splits=pol[1])
+        else:
+            qkv = F.linear(x1, cache.wext, cache.bqkv)                      # [M, 3E] (LoRA folded in)
         o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(B, H, T, device=dev, dtype=torch.float32)
         zseed = sd if sd is not None else torch.zeros(1, dtype=torch.int64, device=dev)
@@ -194,8 +214,9 @@ class WavLMLayerFn(torch.autograd.Function):
             check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(rel),
                                      _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse),
                                      _p(mask) if mask is not None else None, B, T, H, 64, st), "attn_fwd")
-        if wgemm_tile(M, E, E) is not None:
-            aout = wgemm(o, cache.wo, cache.bo, tile=wgemm_tile(M, E, E))
+        pol = _gemm("out", M, E, E)
+        if pol is not None:
+            aout = wgemm(o, cache.wo, cache.bo, tile=pol[0], splits=pol[1])
         else:
             aout = F.linear(o, cache.wo, cache.bo)
         h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -205,14 +226,19 @@ class WavLMLayerFn(torch.autograd.Function):
         check(lib().rdx_wl_add_ln_fwd(_p(hf), _p(aout), sdp, salt + 1, float(p_hidden), _p(h2), _p(ln2.weight),
                                       _p(ln2.bias), float(ln2.eps), _p(x2), _p(mean2), _p(rstd2), M, E, st),
               "wl_add_ln_fwd")
-        t_ffn1 = wgemm_tile(M, cache.w1.shape[0], E, _lib.EPI_BIAS_GELU)
-        if t_ffn1 is not None:                          # FFN1 + bias + GELU in one launch
-            u, v = wgemm(x2, cache.w1, cache.b1, epilogue=_lib.EPI_BIAS_GELU, tile=t_ffn1)
+        F4 = cache.w1.shape[0]
+        pol = _gemm("ffn1", M, F4, E)
+        if pol is not None:                             # FFN1 + bias + GELU in one launch
+            u, v = wgemm(x2, cache.w1, cache.b1, epilogue=_lib.EPI_BIAS_GELU, tile=pol[0], splits=pol[1])
         else:
             u = F.linear(x2, cache.w1, cache.b1)
             v = torch.empty_like(u)
             check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
-        fo = F.linear(v, cache.w2, cache.b2)
+        pol = _gemm("ffn2", M, E, F4)
+        if pol is not None:
+            fo = wgemm(v, cache.w2, cache.b2, tile=pol[0], splits=pol[1])
+        else:
+            fo = F.linear(v, cache.w2, cache.b2)
         out = torch.empty(M, E, device=dev, dtype=torch.float32)
         if chain is not None and index < chain.n - 1:
             chain.pending_res = (out.data_ptr(), h2, fo, salt + 2, float(p_hidden))   # -> the next LN1 forward
@@ -245,19 +271,27 @@ class WavLMLayerFn(torch.autograd.Function):
         else:
             dfo = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
             check(lib().rdx_wl_dropout_bwd(_p(g), sdp, salt + 2, p_hidden, _p(dfo), M * E, st), "wl_dropout_bwd")
-        dv = torch.mm(dfo, cache.w2)
-        du = torch.empty_like(u)
-        check(lib().rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
-        dx2 = torch.mm(du, cache.w1)
+        F4 = u.shape[1]
+        pol = _gemm("d_ffn2", M, F4, E)
+        if pol is not None:                             # FFN2's input gradient with the GELU backward fused
+            du = wgemm(dfo, cache.t("w2"), epilogue=_lib.EPI_GELU_BWD, aux=u, tile=pol[0], splits=pol[1])
+        else:
+            dv = torch.mm(dfo, cache.w2)
+            du = torch.empty_like(u)
+            check(lib().rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
+        pol = _gemm("d_ffn1", M, E, F4)
+        if pol is not None:
+            dx2 = wgemm(du, cache.t("w1"), tile=pol[0], splits=pol[1])
+        else:
+            dx2 = torch.mm(du, cache.w1)
         dh2 = torch.empty(M, E, device=dev, dtype=torch.float32)
         daout = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
         ln1, ln2 = layer.layer_norm, layer.final_layer_norm
         check(lib().rdx_wl_ln_bwd(_p(dx2), E, _p(h2), _p(mean2), _p(rstd2), _p(ln2.weight), _p(g), _p(dh2), sdp,
                                   salt + 1, p_hidden, _p(daout), M, E, st), "wl_ln_bwd")
-        if wgemm_tile(M, E, E) is not None:
-            if cache.woT is None:
-                cache.woT = cache.wo.t().contiguous()
-            do = wgemm(daout, cache.woT, tile=wgemm_tile(M, E, E))
+        pol = _gemm("d_out", M, E, E)
+        if pol is not None:
+            do = wgemm(daout, cache.t("wo"), tile=pol[0], splits=pol[1])
         else:
             do = torch.mm(daout, cache.wo)
         D = torch.empty(B, H, T, device=dev, dtype=torch.float32)
@@ -267,7 +301,11 @@ class WavLMLayerFn(torch.autograd.Function):
             attn_bwd_launch(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, gate, rel, ctx.mask,
                             _p(zseed), int(index), p_attn, _p(o), E, lse, _p(do), E, D, _p(dqkv), _off(dqkv, E),
                             _off(dqkv, 2 * E), 3 * E, dgate, B, T, H, st)
-        dx1 = torch.mm(dqkv, cache.wext)                                     # [M, E + 2r]
+        pol = _gemm("d_qkv", M, ldx, 3 * E) if not lora else None   # (active LoRA: wext changes every step)
+        if pol is not None:
+            dx1 = wgemm(dqkv, cache.t("wqkv"), tile=pol[0], splits=pol[1])
+        else:
+            dx1 = torch.mm(dqkv, cache.wext)                                 # [M, E + 2r]
         dh = torch.empty(M, E, device=dev, dtype=torch.float32)
         sgp = swp = ddp = None
         if chain is not None and chain.g is not None and index in chain.indices:

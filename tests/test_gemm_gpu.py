@@ -106,6 +106,23 @@ def test_wgemm_bias_every_tile(tile, M, N, K):
     assert _rel(wgemm(a, b, tile=tile), a.float() @ b.float().t()) < 1e-2
 
 
+@pytest.mark.parametrize("staged,unstaged", [(5, 45), (6, 46), (12, 52), (16, 56)])
+def test_wgemm_staged_epilogue_bit_exact(staged, unstaged):
+    """The LDS-staged row epilogue stores exactly what the per-lane fragment epilogue stored (same fp32
+    accumulation, same roundings), for all three epilogues and a column tail (N = 4100)."""
+    from radhip import _lib
+    from radhip.ops import wgemm
+    for N in (4096, 4100):
+        a, b, bias = _ops(1608, N, 1024, seed=N + staged)
+        assert torch.equal(wgemm(a, b, bias, tile=staged), wgemm(a, b, bias, tile=unstaged))
+        u1, v1 = wgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=staged)
+        u2, v2 = wgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=unstaged)
+        assert torch.equal(u1, u2) and torch.equal(v1, v2)
+        uu = torch.randn(1608, N, device=DEV).to(torch.bfloat16)
+        assert torch.equal(wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=staged),
+                           wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=unstaged))
+
+
 @pytest.mark.parametrize("tile", [5, 6, 12])
 def test_wgemm_gelu_epilogues(tile):
     from radhip import _lib
@@ -124,15 +141,56 @@ def test_wgemm_gelu_epilogues(tile):
 
 
 def test_wgemm_policy_shapes_match_hipblaslt():
-    """The shapes the fused WavLM layer routes to wgemm (radhip.ops.wgemm_tile) agree with hipBLASLt's bf16
-    result to bf16 rounding: out_proj / its input gradient and FFN1 + GELU at B = 8."""
+    """Every (GEMM, token count) the fused WavLM layer routes to wgemm (radhip.ops.wgemm_policy) agrees with
+    hipBLASLt's bf16 result to bf16 rounding, with its epilogue."""
     from radhip import _lib
-    from radhip.ops import wgemm, wgemm_tile
-    for (N, K, epi) in ((1024, 1024, _lib.EPI_BIAS), (4096, 1024, _lib.EPI_BIAS_GELU)):
-        t = wgemm_tile(1608, N, K, epi)
-        assert t is not None
-        a, b, bias = _ops(1608, N, K, seed=N)
-        got = wgemm(a, b, bias, epilogue=epi, tile=t)
-        got = got[0] if isinstance(got, tuple) else got
-        ref = torch.nn.functional.linear(a, b, bias)
-        assert _rel(got, ref) < 1e-2
+    from radhip.ops import wgemm, wgemm_policy
+    shapes = {"qkv": (3072, 1024), "out": (1024, 1024), "ffn1": (4096, 1024), "ffn2": (1024, 4096),
+              "d_ffn2": (4096, 1024), "d_ffn1": (1024, 4096), "d_out": (1024, 1024), "d_qkv": (1024, 3072)}
+    n = 0
+    for M in (1608, 6432):
+        for name, (N, K) in shapes.items():
+            pol = wgemm_policy(name, M, N, K)
+            if pol is None:
+                continue
+            n += 1
+            a, b, bias = _ops(M, N, K, seed=N + K)
+            if name == "d_ffn2":
+                uu = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+                got = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=pol[0], splits=pol[1])
+                x = uu.float()
+                grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+                ref = torch.mm(a, b.t()).float() * grad
+                assert _rel(got, ref) < 2e-2, name
+                continue
+            epi = _lib.EPI_BIAS_GELU if name == "ffn1" else _lib.EPI_BIAS
+            got = wgemm(a, b, bias, epilogue=epi, tile=pol[0], splits=pol[1])
+            got = got[0] if isinstance(got, tuple) else got
+            ref = torch.nn.functional.linear(a, b, bias)
+            assert _rel(got, ref) < 1e-2, name
+    assert n > 0
+
+
+@pytest.mark.parametrize("tile,splits", [(12, 4), (20, 2), (5, 3), (16, 7)])
+@pytest.mark.parametrize("M,N,K", [(1608, 1024, 4096), (333, 260, 3072)])
+def test_wgemm_split_k(tile, splits, M, N, K):
+    """Split-K with the last-arriver reduction: equal to the unsplit launch up to fp32 summation order, bit-for-bit
+    repeatable (fixed split order whoever arrives last; the tickets re-zero themselves between launches), every
+    epilogue, row and column tails."""
+    from radhip import _lib
+    from radhip.ops import wgemm
+    a, b, bias = _ops(M, N, K, seed=splits)
+    ref = a.float() @ b.float().t() + bias.float()
+    outs = [wgemm(a, b, bias, tile=tile, splits=splits) for _ in range(3)]
+    assert _rel(outs[0], ref) < 1e-2
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    one = wgemm(a, b, bias, tile=tile)
+    assert float((outs[0].float() - one.float()).abs().max()) <= 2 ** -7 * float(one.float().abs().max())
+    u, v = wgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=tile, splits=splits)
+    assert torch.equal(u, outs[0])
+    assert torch.equal(v, torch.nn.functional.gelu(u.float()).to(torch.bfloat16)) or \
+        float((v.float() - torch.nn.functional.gelu(u.float())).abs().max()) <= 2 ** -7 * float(v.float().abs().max())
+    uu = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    du = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile, splits=splits)
+    du1 = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile)
+    assert _rel(du, du1) < 1e-2

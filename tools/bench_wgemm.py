@@ -3,7 +3,7 @@ configuration, its epilogue fused) against hipBLASLt (torch F.linear / mm + the 
 fp32 accumulate, random operands rotated over 6 copies (weights do not stay L2-resident between calls, as in
 the 24-layer pass). Checks each result against an fp32 torch reference and prints us and TFLOP/s per shape.
 
-  python tools/bench_wgemm.py [--tiles 0,1,2] [--B 8,32] [--reps 30]
+  python tools/bench_wgemm.py [--tiles 0,1,12x4] [--B 8,32] [--reps 30]   (TxS: tile T split-K S)
 """
 import argparse
 import ctypes
@@ -59,7 +59,7 @@ def main():
     args = ap.parse_args()
     L = _lib.lib()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    tiles = [int(t) for t in args.tiles.split(",")]
+    tiles = [t for t in args.tiles.split(",")]
     torch.manual_seed(0)
     for B in [int(b) for b in args.B.split(",")]:
         M = B * 201
@@ -96,14 +96,23 @@ def main():
                    "hipblaslt_us": round(t_blas, 2), "hipblaslt_tflops": round(fl / t_blas / 1e6, 1)}
             outs = [torch.empty(M, N, device="cuda", dtype=torch.bfloat16) for _ in sets]
             vs = [torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi == "gelu" else None for _ in sets]
-            for tile in tiles:
-                def ours(i, tile=tile):
+            for tname in tiles:
+                tile, splits = (int(v) for v in tname.split("x")) if "x" in tname else (int(tname), 1)
+                if splits > K // 64:
+                    continue
+                nws = max(int(L.rdx_wgemm_ws_bytes(M, N, tile, splits)), 16)
+                ncn = max(int(L.rdx_wgemm_counters(M, N, tile)), 1)
+                ws = torch.empty(nws, dtype=torch.uint8, device="cuda")
+                cnt = torch.zeros(ncn, dtype=torch.int32, device="cuda")
+
+                def ours(i, tile=tile, splits=splits, ws=ws, cnt=cnt, nws=nws, ncn=ncn):
                     a_, w_, b_, x_ = sets[i]
-                    return lambda: L.rdx_wgemm_bf16(p(a_), K, p(w_), K, p(outs[i]), N, M, N, K, p(b_), EPI[epi], p(x_),
-                                                    N, p(vs[i]), N, tile, st)
+                    return lambda: L.rdx_wgemm_bf16_ex(p(a_), K, p(w_), K, p(outs[i]), N, M, N, K, p(b_), EPI[epi],
+                                                       p(x_), N, p(vs[i]), N, tile, splits, p(ws), nws, p(cnt), ncn,
+                                                       st)
                 rc = ours(0)()
                 if rc != 0:
-                    row[f"t{tile}"] = f"rc {rc}"
+                    row[f"t{tname}"] = f"rc {rc}"
                     continue
                 torch.cuda.synchronize()
                 got = outs[0].float()
@@ -112,9 +121,9 @@ def main():
                 if epi == "gelu":
                     err = max(err, float((vs[0].float() - ref_v.float()).abs().max() / ref_v.float().abs().max()))
                 t = timed([ours(i) for i in range(len(sets))], args.reps)
-                row[f"t{tile}_us"] = round(t, 2)
-                row[f"t{tile}_tflops"] = round(fl / t / 1e6, 1)
-                row[f"t{tile}_err"] = float(f"{err:.2e}")
+                row[f"t{tname}_us"] = round(t, 2)
+                row[f"t{tname}_tflops"] = round(fl / t / 1e6, 1)
+                row[f"t{tname}_err"] = float(f"{err:.2e}")
             print(json.dumps(row), flush=True)
 
 
