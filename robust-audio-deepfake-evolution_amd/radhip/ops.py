@@ -902,6 +902,77 @@ class Block0Front(torch.autograd.Function):
                 sums[2], dw2.to(w2dt))
 
 
+class Block0Fused(torch.autograd.Function):
+    """SincNet block 0 whole (Residual_block.forward, src/models/DualStreamSEMamba.py:182-200, one input channel,
+    frozen BN): y = MaxPool2d((1, 3))(conv2(selu(bn2(conv1(x) + cb))) + conv_downsample(x) + b2 + bd) in ONE HIP
+    pass (rdx_b0x_fwd: only x is read, only y and the window argmax are written; bit-identical to Block0Front +
+    ResTail). Backward in one pass too (rdx_b0x_bwd: c and out1 recomputed from x, per-workgroup partial rows of
+    every parameter gradient); RADHIP_B0X_BWD=0 runs the unfused backward kernels on recomputed intermediates
+    instead (c / out1 by rdx_sincnet_b0_fwd, the pool gradient scattered by the argmax, Block0Front's kernels)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd, conv_bias, mean, invstd, gamma, beta, w2, b2, bd):
+        _require_gpu(x)
+        xb = x.to(torch.bfloat16).contiguous()                       # one channel: [N, H, W] in memory
+        N, _, H, W = xb.shape
+        C = w1.shape[0]
+        w1b = w1.detach().to(torch.bfloat16).float().reshape(C, 6).contiguous()   # autocast's bf16 weights
+        wdb = wd.detach().to(torch.bfloat16).float().reshape(C, 3).contiguous()
+        f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
+        wf2, wd2 = _sconv_w(w2)
+        bias = (b2.detach().float() + bd.detach().float()).contiguous()
+        y = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        arg = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.uint8, memory_format=torch.channels_last)
+        # MFMA work: conv2 (32 -> 32, 2 x 3) over N x H x W positions; HBM: x in, y + argmax out
+        with _timed("b0x_fwd", x, 2.0 * N * H * W * 32 * 192):
+            check(lib().rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg), N, H, W,
+                                    _stream(x)), "b0x_fwd")
+        ctx.save_for_backward(xb, w1b, wdb, wd2, bn5, arg, *f32)
+        ctx.meta = (tuple(w1.shape), tuple(wd.shape), x.dtype, tuple(w2.shape), w2.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, w1b, wdb, wd2, bn5, arg, *f32 = ctx.saved_tensors
+        w1_shape, wd_shape, x_dtype, s2, w2dt = ctx.meta
+        N, H, W = xb.shape[0], xb.shape[2], xb.shape[3]
+        C = w1_shape[0]
+        if os.environ.get("RADHIP_B0X_BWD", "1") != "0":
+            dy = _nhwc(dy.to(torch.bfloat16))
+            dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
+            part = torch.empty(lib().rdx_b0x_bwd_nblk(N, W), 6560, device=xb.device, dtype=torch.float32)
+            # MFMA work: conv2's input gradient and weight gradient (2 x the forward's conv2)
+            with _timed("b0x_bwd", dy, 4.0 * N * H * W * 32 * 192):
+                check(lib().rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2), _p(dx), _p(part),
+                                        N, H, W, _stream(dy)), "b0x_bwd")
+            tot = part.sum(0)
+            dw2 = tot[:6144].view(2, 3, C, C).permute(2, 3, 0, 1)
+            dw1 = tot[6144:6336].reshape(w1_shape)
+            dwd = tot[6336:6432].reshape(wd_shape)
+            dbias = tot[6432:6464]
+            sums = tot[6464:6560].view(3, C)
+            return (dx.to(x_dtype), dw1, dwd, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt), dbias, dbias)
+        c = torch.empty(N, C, H + 1, W, device=xb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        out1 = torch.empty_like(c)
+        idn = torch.empty(N, C, H, W, device=xb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        check(lib().rdx_sincnet_b0_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(c), _p(out1), _p(idn), N, H, W, C,
+                                       _stream(xb)), "sincnet_b0_fwd")
+        dy = _nhwc(dy.to(torch.bfloat16))
+        ds = torch.empty(N, C, H, W, device=xb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        dbias = torch.zeros(C, device=xb.device, dtype=torch.float32)
+        check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(ds), _p(dbias), N * H, W, C, _stream(dy)),
+              "res_tail_bwd")
+        dc, sums, dw2 = _conv2_grad_to_c(ds, out1, c, wd2, s2, bn5, f32)
+        dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
+        part = torch.empty(lib().rdx_sincnet_b0_nblk(N * H * W), C * 9, device=xb.device, dtype=torch.float32)
+        with _timed("sincnet_b0_bwd", dc, 2 * (dc.numel() + ds.numel()) + 4 * dx.numel() + 2 * xb.numel()):
+            check(lib().rdx_sincnet_b0_bwd(_p(xb), _p(dc), _p(ds), _p(w1b), _p(wdb), _p(dx), _p(part), N, H, W, C,
+                                           _stream(dc)), "sincnet_b0_bwd")
+        dw = part.sum(0).view(C, 9)
+        return (dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape), sums[0], None, None, sums[1],
+                sums[2], dw2.to(w2dt), dbias, dbias)
+
+
 # ------------------------------------------------------------ WavLM positional convolution ----
 def posconv_weights(weight):
     """Conv weight [1024, 64, 128] (weight_norm applied) -> the two bf16 operand layouts of csrc/posconv.hip:

@@ -12,7 +12,7 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import (Block0Convs, Block0Front, BnSelu, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
+from .ops import (Block0Convs, Block0Front, Block0Fused, BnSelu, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
                   sconv_weight_ok, sincconv_absmaxpool)
 
 
@@ -135,6 +135,11 @@ class Residual_block(nn.Module):
             # pre-activation in one pass for the 32-channel blocks)
             pair = bf and sconv_weight_ok(w2) and os.environ.get("RADHIP_SCONV_PAIR", "1") != "0"
             idn, a = None, None
+            if (self.first and self.downsample and x.shape[1] == 1 and bf and pair and x.shape[3] >= 3
+                    and self.conv1.out_channels == 32 and os.environ.get("RADHIP_B0X", "1") != "0"):
+                # the whole block in one HIP pass each way (radhip.ops.Block0Fused): no full-size intermediates
+                return Block0Fused.apply(x, self.conv1.weight, self.conv_downsample.weight, *bnp, w2, self.conv2.bias,
+                                         self.conv_downsample.bias)
             if (self.first and self.downsample and x.shape[1] == 1 and bf
                     and os.environ.get("RADHIP_FUSED_B0", "1") != "0"):
                 # one input channel: both convolutions (and conv1's BN + SELU) in one HIP pass each way
