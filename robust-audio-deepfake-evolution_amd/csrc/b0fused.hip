@@ -35,7 +35,7 @@ constexpr int BX_IR = 136;      // out1 image rows: positions q0 - 1 .. q0 + 128
 constexpr int BX_XW = 132;      // staged x positions q0 - 2 .. q0 + 129
 constexpr int BX_SP = 36;       // fp32 pitch of the pre-pool row (32 channels + 4: spreads the row stores)
 constexpr int BX_IMG = BX_IR * 64;
-constexpr int BX_LDS = 192 * 64 + 3 * BX_IMG + 4 * BX_XW * 4 + 128 * BX_SP * 4 + 128 * 4;
+constexpr int BX_LDS = 192 * 64 + 3 * BX_IMG + 4 * BX_XW * 4 + 128 * BX_SP * 4 + 32 * 16;
 
 __device__ __forceinline__ float bx_selu(float u) {
   return BX_SELU_SCALE * (u > 0.f ? u : BX_SELU_ALPHA * (__expf(u) - 1.0f));
@@ -68,8 +68,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   char* os = ws + 192 * 64;                                 // out1 ring: 3 slots
   float* xr = reinterpret_cast<float*>(os + 3 * BX_IMG);    // x ring: 4 rows of BX_XW
   float* ss = xr + 4 * BX_XW;                               // s = a + idn + bias of the current row
-  float* pwd = ss + 128 * BX_SP;                            // conv_downsample weights [32][3]
-  float* pbias = pwd + 96;                                  // [32]
+  float4* prec = reinterpret_cast<float4*>(ss + 128 * BX_SP);   // [32] {wd[co][0..2], bias[co]}
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int strip = blockIdx.x, n = blockIdx.y;
   const int q0 = strip * BX_P;
@@ -80,8 +79,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
     const int row = i >> 2, ch = i & 3;
     *reinterpret_cast<uint4*>(ws + bx_img(row, ch)) = *reinterpret_cast<const uint4*>(a.w2 + row * BX_C + ch * 8);
   }
-  if (tid < 96) pwd[tid] = a.wd[tid];
-  if (tid < 32) pbias[tid] = a.bias[tid];
+  if (tid < 32) prec[tid] = make_float4(a.wd[tid * 3], a.wd[tid * 3 + 1], a.wd[tid * 3 + 2], a.bias[tid]);
   // this thread's out1 channels: 8 * g8 .. + 7 (its items it = tid + 256 k all have it & 3 == tid & 3)
   const int g8 = tid & 3;
   float t1[8][6], cb[8], mu[8], sg[8], sh[8];
@@ -174,8 +172,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
         for (int e = 0; e < 4; ++e) {
           const int co = 8 * g + 4 * hh + e;
           const float av = bx_bf16(acc[4 * g + e]);
-          const float iv = bx_bf16(fmaf(x0, pwd[co * 3], fmaf(x1, pwd[co * 3 + 1], x2 * pwd[co * 3 + 2])));
-          o[e] = av + iv + pbias[co];
+          const float4 pr = prec[co];
+          const float iv = bx_bf16(fmaf(x0, pr.x, fmaf(x1, pr.y, x2 * pr.z)));
+          o[e] = av + iv + pr.w;
         }
         *reinterpret_cast<float4*>(ss + pw * BX_SP + 8 * g + 4 * hh) = make_float4(o[0], o[1], o[2], o[3]);
       }
@@ -259,15 +258,16 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
 // the unfused ones up to the order of their fp32 sums.
 //
 // A workgroup walks units (utterance, strip of 126 positions) in a grid-stride loop and, per unit, the H + 1
-// rows h' of dout1 top-down: ds row h' (LDS ring of 2), out1 row h' + 1 (ring of 2), dout1 row h' on the MFMA
-// with its BN + SELU backward epilogue into the dc ring (2 rows), the d w2 MFMAs of ds row h', then one VALU
-// pass for dx row h' - 1, d w1, d wd and the bias sums. Every sum counts the strip's own positions
+// rows h' of dout1 top-down in four phases: (A) ds row h' into an LDS ring of 2 (its pooled gradient and argmax
+// fetched a row ahead), out1 row h' + 1 (ring of 2); (B) dout1 row h' on the MFMA into the dc ring (2 rows) and
+// the d w2 MFMAs of ds row h'; (C) the BN + SELU backward of dout1 in place, with a thread owning 8 channels
+// (c recomputed from x); (D) dx row h' - 1, d w1, d wd and the bias sums, a thread owning 4 channels. Every sum counts the strip's own positions
 // [126 s, 126 s + 126) (the d w2 MFMA runs K over 128 positions and zeroes the last two); with Wo / 42 + 1
 // strips they partition every position that carries a gradient. Per-workgroup sums go to one fp32 partial row (the caller sums the rows: no atomics).
 constexpr int BXB_DCR = 128;                         // dc image rows: positions q0 - 1 .. q0 + 126
 constexpr int BXB_XW = 136;                          // staged x positions q0 - 4 .. q0 + 131
 constexpr int BXB_NPART = 6 * 32 * 32 + 32 * 6 + 32 * 3 + 32 + 3 * 32;
-constexpr int BXB_LDS = 192 * 64 + 2 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + (192 + 96 + 160) * 4;
+constexpr int BXB_LDS = 192 * 64 + 2 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + 32 * 64;
 constexpr int BXB_BLOCKS = 512;
 
 typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 bxbf16x4v;
@@ -281,6 +281,26 @@ __device__ __forceinline__ bxbf16x8 bx_read_tr(const char* img, int r0, int s, i
   const int sub = 2 * (col & 7);
   const bxbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + bx_img(row, col >> 3) + sub));
   const bxbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + bx_img(row + 8, col >> 3) + sub));
+  bxbf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = lo[j];
+    r[4 + j] = hi[j];
+  }
+  return r;
+}
+// the same read from precomputed per-lane byte offsets (lo, hi) of K step 0: step s adds 1024 bytes (16 image
+// rows = two 512-byte subtiles, the swizzle repeats), so the loop keeps 2 offsets live instead of 16 addresses
+__device__ __forceinline__ int2 bx_tr_off(int r0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = r0 + 4 * (g >> 1) + (i >> 2);
+  const int col = 16 * (g & 1) + 4 * (i & 3);
+  const int sub = 2 * (col & 7);
+  return make_int2(bx_img(row, col >> 3) + sub, bx_img(row + 8, col >> 3) + sub);
+}
+__device__ __forceinline__ bxbf16x8 bx_read_tr_at(const char* img, int2 off, int s) {
+  const bxbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + off.x + 1024 * s));
+  const bxbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + off.y + 1024 * s));
   bxbf16x8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -311,28 +331,34 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
   char* wsf = lds;                                           // flipped conv2 weights: rows tap * 32 + ci
   char* dsr = wsf + 192 * 64;                                // ds ring (2): row i <-> position q0 - 2 + i
   char* o1r = dsr + 2 * BX_IMG;                              // out1 ring (2): row i <-> q0 - 3 + i
-  char* dcr = o1r + 2 * BX_IMG;                              // dc ring (2): row i <-> q0 - 1 + i
+  char* dcr = o1r + 2 * BX_IMG;                              // dO, then dc, ring (2): row i <-> q0 - 1 + i
   float* xr = reinterpret_cast<float*>(dcr + 2 * BXB_DCR * 64);   // x ring (4): index i <-> q0 - 4 + i
-  float* pw1 = xr + 4 * BXB_XW;                              // [32][6]
-  float* pwd = pw1 + 192;                                    // [32][3]
-  float* pbn = pwd + 96;                                     // [5][32]
+  // per-channel record (four 16-byte reads): w1[0..5], wd[0..2], conv1 bias, mean, invstd * gamma, beta, invstd;
+  // part j of channel co at float4 j * 32 + co (the channels one instruction reads spread over the bank slots)
+  float4* prec = reinterpret_cast<float4*>(xr + 4 * BXB_XW);   // [4][32]
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int H = a.H, W = a.W, Wo = a.Wo, W3 = 3 * a.Wo;
   for (int i = tid; i < 192 * 4; i += BX_T) {
     const int row = i >> 2, ch = i & 3;
     *reinterpret_cast<uint4*>(wsf + bx_img(row, ch)) = *reinterpret_cast<const uint4*>(a.w2f + row * BX_C + ch * 8);
   }
-  if (tid < 192) pw1[tid] = a.w1[tid];
-  if (tid < 96) pwd[tid] = a.wd[tid];
-  if (tid < 160) pbn[tid] = a.bn[tid];
-  // per-thread sums: BN sums of the dout1 epilogue (lane channels 8 gg + 4 hh + e), the VALU pass's
-  // (channel group g = tid & 7: channels 4 g .. 4 g + 3) d w1 / d wd / d bias, and the d w2 MFMA tiles
-  float bsum[3][4][4];
+  if (tid < 32) {
+    const float* w1 = a.w1 + tid * 6;
+    const float* wd = a.wd + tid * 3;
+    prec[tid] = make_float4(w1[0], w1[1], w1[2], w1[3]);
+    prec[32 + tid] = make_float4(w1[4], w1[5], wd[0], wd[1]);
+    prec[64 + tid] = make_float4(wd[2], a.bn[tid], a.bn[BX_C + tid], a.bn[2 * BX_C + tid]);
+    prec[96 + tid] = make_float4(a.bn[3 * BX_C + tid], a.bn[4 * BX_C + tid], 0.f, 0.f);
+  }
+  // persistent per-thread sums. Phase C (dc) owns channels 8 c8 .. 8 c8 + 7 (c8 = tid & 3): BN sums;
+  // phase D (dx) owns channels 4 g .. 4 g + 3 (g = tid & 7): d w1, d wd, d bias; the d w2 MFMA tiles
+  const int c8 = tid & 3, g = tid & 7;
+  float bsum[3][8];
   float aw1[4][6], awd[4][3], abias[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int k = 0; k < 8; ++k) bsum[0][k] = bsum[1][k] = bsum[2][k] = 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bsum[0][i][e] = bsum[1][i][e] = bsum[2][i][e] = 0.f;
+  for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) aw1[i][j] = 0.f;
 #pragma unroll
@@ -344,9 +370,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc2[t][i] = 0.f;
-  const int g = tid & 7;
-  const int pw = wv * 32 + r;    // dout1 position q0 - 1 + pw of this lane
+  const int pw = wv * 32 + r;    // dout1 position q0 - 1 + pw of this lane in phase B
   __syncthreads();
+  constexpr int DSN = (BX_IR * 4 + BX_T - 1) / BX_T;   // ds items per thread (3)
 
   for (int64_t u = blockIdx.x; u < (int64_t)a.strips * a.N; u += gridDim.x) {
     const int strip = (int)(u % a.strips), n = (int)(u / a.strips);
@@ -358,12 +384,22 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
                                                                         : 0.f;
     };
     auto xslot = [&](int row) -> float* { return xr + (row & 3) * BXB_XW; };
+    // conv1 pre-activation c (bf16-rounded, the unfused kernel's FMA order) at x columns v0 / v1, from a record
+    auto conv1c = [&](const float (&v0)[3], const float (&v1)[3], const float4& r0, const float4& r1) -> float {
+      float acc = v0[0] * r0.x;
+      acc = fmaf(v0[1], r0.y, acc);
+      acc = fmaf(v0[2], r0.z, acc);
+      acc = fmaf(v1[0], r0.w, acc);
+      acc = fmaf(v1[1], r1.x, acc);
+      acc = fmaf(v1[2], r1.y, acc);
+      return bx_bf16(acc);
+    };
     auto make_out1 = [&](int ro) {   // out1 row ro at positions q0 - 3 + i, i < 132 (zero outside [0, W))
       const float* xa = xslot(ro - 1);
       const float* xb = xslot(ro);
       char* sl = o1r + (ro & 1) * BX_IMG;
       for (int it = tid; it < 132 * 4; it += BX_T) {
-        const int i = it >> 2, c8 = it & 3;
+        const int i = it >> 2;
         const int q = q0 - 3 + i;
         const float v0[3] = {xa[i], xa[i + 1], xa[i + 2]}, v1[3] = {xb[i], xb[i + 1], xb[i + 2]};
         uint32_t o[4];
@@ -373,44 +409,53 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int co = 8 * c8 + k + e;
-            const float* t = pw1 + co * 6;
-            float acc = v0[0] * t[0];
-            acc = fmaf(v0[1], t[1], acc);
-            acc = fmaf(v0[2], t[2], acc);
-            acc = fmaf(v1[0], t[3], acc);
-            acc = fmaf(v1[1], t[4], acc);
-            acc = fmaf(v1[2], t[5], acc);
-            const float cv = bx_bf16(acc);
-            yv[e] = bx_selu(fmaf((cv + pbn[co]) - pbn[BX_C + co], pbn[2 * BX_C + co], pbn[3 * BX_C + co]));
+            const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co], r3 = prec[96 + co];
+            const float cv = conv1c(v0, v1, r0, r1);
+            yv[e] = bx_selu(fmaf((cv + r2.y) - r2.z, r2.w, r3.x));
           }
           o[k >> 1] = (q >= 0 && q < W) ? bx_pack2(yv[0], yv[1]) : 0u;
         }
         *reinterpret_cast<uint4*>(sl + bx_img(i, c8)) = make_uint4(o[0], o[1], o[2], o[3]);
       }
     };
-    auto make_ds = [&](int hrow) {   // ds row hrow at positions q0 - 2 + i, i < 136 (zero rows outside [0, H))
-      char* sl = dsr + (hrow & 1) * BX_IMG;
-      for (int it = tid; it < BX_IR * 4; it += BX_T) {
-        const int i = it >> 2, c8 = it & 3;
+    // ds row hrow: the pooled gradient where the window argmax hits, fetched a row ahead into registers
+    uint4 pd[DSN];
+    uint2 pa[DSN];
+    auto fetch_ds = [&](int hrow) {
+#pragma unroll
+      for (int j = 0; j < DSN; ++j) {
+        const int it = tid + BX_T * j;
+        const int i = it >> 2;
         const int w = q0 - 2 + i;
-        uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (hrow >= 0 && hrow < H && i < 130 && w >= 0 && w < W3) {
-          const int j = w / 3, t = w - 3 * j;
-          const int64_t off = (((int64_t)n * H + hrow) * Wo + j) * BX_C + 8 * c8;
-          const uint4 d = *reinterpret_cast<const uint4*>(a.dp + off);
-          const uint2 ag = *reinterpret_cast<const uint2*>(a.arg + off);
-          const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+        pd[j] = make_uint4(0u, 0u, 0u, 0u);
+        pa[j] = make_uint2(0xffffffffu, 0xffffffffu);
+        if (it < BX_IR * 4 && hrow >= 0 && hrow < H && i < 130 && w >= 0 && w < W3) {
+          const int jj = w / 3;
+          const int64_t off = (((int64_t)n * H + hrow) * Wo + jj) * BX_C + 8 * c8;
+          pd[j] = *reinterpret_cast<const uint4*>(a.dp + off);
+          pa[j] = *reinterpret_cast<const uint2*>(a.arg + off);
+        }
+      }
+    };
+    auto store_ds = [&](int hrow) {
+      char* sl = dsr + (hrow & 1) * BX_IMG;
+#pragma unroll
+      for (int j = 0; j < DSN; ++j) {
+        const int it = tid + BX_T * j;
+        if (it < BX_IR * 4) {
+          const int i = it >> 2;
+          const uint32_t t = (uint32_t)((q0 - 2 + i + 3) % 3);   // window slot of position q0 - 2 + i
+          const uint32_t dw[4] = {pd[j].x, pd[j].y, pd[j].z, pd[j].w};
           uint32_t ow[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const uint32_t bits = e < 2 ? ag.x >> (16 * e) : ag.y >> (16 * (e - 2));
-            const uint32_t m0 = ((bits & 0xff) == (uint32_t)t) ? 0x0000ffffu : 0u;
-            const uint32_t m1 = (((bits >> 8) & 0xff) == (uint32_t)t) ? 0xffff0000u : 0u;
+            const uint32_t bits = e < 2 ? pa[j].x >> (16 * e) : pa[j].y >> (16 * (e - 2));
+            const uint32_t m0 = ((bits & 0xff) == t) ? 0x0000ffffu : 0u;
+            const uint32_t m1 = (((bits >> 8) & 0xff) == t) ? 0xffff0000u : 0u;
             ow[e] = dw[e] & (m0 | m1);
           }
-          o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          *reinterpret_cast<uint4*>(sl + bx_img(i, c8)) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
-        *reinterpret_cast<uint4*>(sl + bx_img(i, c8)) = o;
       }
     };
     __syncthreads();   // the previous unit's readers are done
@@ -422,19 +467,29 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
       for (int i = 0; i < 3; ++i)
         if (tid < BXB_XW) xslot(i - 1)[tid] = v[i];
     }
-    make_ds(-1);
+    fetch_ds(-1);
+    store_ds(-1);       // zeros
+    fetch_ds(0);
     __syncthreads();
     make_out1(0);
     for (int hp = 0; hp <= H; ++hp) {
+      // ---- phase A: ds row hp (registers -> LDS), next row's fetch, out1 row hp + 1
       const float xnext = load_x(hp + 2);
-      make_ds(hp);
+      store_ds(hp);
+      fetch_ds(hp + 1);
       if (hp + 1 <= H) make_out1(hp + 1);
-      __syncthreads();   // (1) ds row hp, out1 row hp + 1
-      // dout1 row hp = conv(ds rows hp - 1, hp) with the flipped weights, then the BN + SELU backward
+      __syncthreads();
+      // ---- phase B: dout1 row hp = conv(ds rows hp - 1, hp) with the flipped weights -> bf16 into the dc slot;
+      // d w2 += ds row hp x out1 rows hp, hp + 1 over K = ds image rows 2 .. 129 (positions q0 .. q0 + 127); rows
+      // 128 and 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed (in the last K
+      // step, element j of lane l holds row 2 + 112 + 8 (j >> 2) + 4 (l >> 5) + (j & 3): elements 6, 7 of lanes
+      // 32-63)
       {
         bxf32x16 acc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        // weight rows tap * 32 + r: 2048 bytes per tap; input rows pw + kw
+        const int wo0 = bx_img(r, hh), wo1 = bx_img(r, 2 + hh);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
           const char* dk = dsr + ((hp - 1 + kh) & 1) * BX_IMG;
@@ -443,53 +498,17 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
               const bxbf16x8 xf = *reinterpret_cast<const bxbf16x8*>(dk + bx_img(pw + kw, 2 * s + hh));
-              const bxbf16x8 wf = *reinterpret_cast<const bxbf16x8*>(wsf + bx_img((kh * 3 + kw) * BX_C + r, 2 * s + hh));
+              const bxbf16x8 wf = *reinterpret_cast<const bxbf16x8*>(wsf + (kh * 3 + kw) * 2048 + (s ? wo1 : wo0));
               acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf, acc, 0, 0, 0);
             }
         }
-        const int q = q0 - 1 + pw;
-        const bool inside = q >= 0 && q < W;
-        const bool own = inside && pw >= 1 && pw <= BX_P;
-        const float* xa = xslot(hp - 1);
-        const float* xb = xslot(hp);
-        const float v0[3] = {xa[pw + 2], xa[pw + 3], xa[pw + 4]}, v1[3] = {xb[pw + 2], xb[pw + 3], xb[pw + 4]};
         char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
 #pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-          float dz[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int co = 8 * gg + 4 * hh + e;
-            const float* t = pw1 + co * 6;
-            float cacc = v0[0] * t[0];
-            cacc = fmaf(v0[1], t[1], cacc);
-            cacc = fmaf(v0[2], t[2], cacc);
-            cacc = fmaf(v1[0], t[3], cacc);
-            cacc = fmaf(v1[1], t[4], cacc);
-            cacc = fmaf(v1[2], t[5], cacc);
-            const float cv = bx_bf16(cacc);
-            // the arithmetic of rdx_sconv_dgrad_bnselu's epilogue
-            const float zc = (cv + pbn[co]) - pbn[BX_C + co];
-            const float xhat = zc * pbn[4 * BX_C + co];
-            const float uu = fmaf(zc, pbn[2 * BX_C + co], pbn[3 * BX_C + co]);
-            const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * __expf(uu);
-            const float du = bx_bf16(acc[4 * gg + e]) * sd;
-            dz[e] = inside ? du * pbn[2 * BX_C + co] : 0.f;
-            if (own) {
-              bsum[0][gg][e] += dz[e];
-              bsum[1][gg][e] = fmaf(du, xhat, bsum[1][gg][e]);
-              bsum[2][gg][e] += du;
-            }
-          }
+        for (int gg = 0; gg < 4; ++gg)
           *reinterpret_cast<uint2*>(dcs + bx_img(pw, gg) + 8 * hh) =
-              make_uint2(bx_pack2(dz[0], dz[1]), bx_pack2(dz[2], dz[3]));
-        }
+              make_uint2(bx_pack2(acc[4 * gg], acc[4 * gg + 1]), bx_pack2(acc[4 * gg + 2], acc[4 * gg + 3]));
       }
       if (hp < H) {
-        // d w2 += ds row hp x out1 rows hp, hp + 1 over K = ds image rows 2 .. 129 (positions q0 .. q0 + 127);
-        // rows 128 and 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed (in the
-        // last K step, element j of lane l holds row 2 + 112 + 8 (j >> 2) + 4 (l >> 5) + (j & 3): elements 6, 7
-        // of lanes 32-63)
         const char* dsi = dsr + (hp & 1) * BX_IMG;
         const bool tail_lane = (lane >> 5) == 1;
 #pragma unroll
@@ -498,27 +517,72 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           if (tap < 6) {
             const int kh = tap / 3, kw = tap - 3 * kh;
             const char* oi = o1r + ((hp + kh) & 1) * BX_IMG;
+            const int2 offa = bx_tr_off(2, lane), offb = bx_tr_off(2 + kw, lane);
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-              bxbf16x8 av = bx_read_tr(dsi, 2, s, lane);
+              bxbf16x8 av = bx_read_tr_at(dsi, offa, s);
               if (s == 7 && tail_lane) {
                 av[6] = (__bf16)0.0f;
                 av[7] = (__bf16)0.0f;
               }
-              acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr(oi, 2 + kw, s, lane), acc2[t], 0, 0, 0);
+              acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr_at(oi, offb, s), acc2[t], 0, 0, 0);
             }
           }
         }
       }
-      __syncthreads();   // (2) dc row hp
-      {  // VALU pass over the strip's own positions: dx row hp - 1, d w1 (dc row hp), d wd / d bias (ds row hp)
+      __syncthreads();
+      // ---- phase C: dc row hp = bf16(dO selu'(u) s) in place (rdx_sconv_dgrad_bnselu's arithmetic on c
+      // recomputed from x), BN sums over the strip's own positions
+      {
+        char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
+        const float* xa = xslot(hp - 1);
+        const float* xb = xslot(hp);
+        for (int it = tid; it < BXB_DCR * 4; it += BX_T) {
+          const int i = it >> 2;
+          const int q = q0 - 1 + i;
+          const bool inside = q >= 0 && q < W;
+          const bool own = inside && i >= 1 && i <= BX_P;
+          uint4* slot = reinterpret_cast<uint4*>(dcs + bx_img(i, c8));
+          const uint4 dov = *slot;
+          const uint32_t dw[4] = {dov.x, dov.y, dov.z, dov.w};
+          const float v0[3] = {xa[i + 2], xa[i + 3], xa[i + 4]}, v1[3] = {xb[i + 2], xb[i + 3], xb[i + 4]};
+          uint32_t ow[4];
+#pragma unroll
+          for (int k = 0; k < 8; k += 2) {
+            float dz[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int co = 8 * c8 + k + e;
+              const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co], r3 = prec[96 + co];
+              const float cv = conv1c(v0, v1, r0, r1);
+              const float zc = (cv + r2.y) - r2.z;
+              const float xhat = zc * r3.y;
+              const float uu = fmaf(zc, r2.w, r3.x);
+              const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * __expf(uu);
+              const float dov_e = e == 0 ? bx_lo(dw[k >> 1]) : bx_hi(dw[k >> 1]);
+              const float du = dov_e * sd;
+              dz[e] = inside ? du * r2.w : 0.f;
+              if (own) {
+                bsum[0][k + e] += dz[e];
+                bsum[1][k + e] = fmaf(du, xhat, bsum[1][k + e]);
+                bsum[2][k + e] += du;
+              }
+            }
+            ow[k >> 1] = bx_pack2(dz[0], dz[1]);
+          }
+          *slot = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+      }
+      __syncthreads();
+      // ---- phase D: dx row hp - 1, d w1 (dc row hp), d wd / d bias (ds row hp) over the strip's own positions
+      {
         const char* dcA = dcr + (hp & 1) * (BXB_DCR * 64);         // dc row hp
         const char* dcB = dcr + ((hp - 1) & 1) * (BXB_DCR * 64);   // dc row hp - 1
         const char* dsP = dsr + ((hp - 1) & 1) * BX_IMG;           // ds row hp - 1
         const char* dsC = dsr + (hp & 1) * BX_IMG;                 // ds row hp
         const float* xa = xslot(hp - 1);
         const float* xb = xslot(hp);
-        const int c8 = g >> 1, sub = 8 * (g & 1);
+        const int gc = g >> 1, sub = 8 * (g & 1);
         for (int it = tid; it < BX_P * 8; it += BX_T) {
           const int k = it >> 3;
           const int q = q0 + k;
@@ -527,18 +591,20 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           if (hp >= 1 && valid) {
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
-              const uint2 A = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 2 - kw, c8) + sub);
-              const uint2 Bv = *reinterpret_cast<const uint2*>(dcB + bx_img(k + 2 - kw, c8) + sub);
-              const uint2 D = *reinterpret_cast<const uint2*>(dsP + bx_img(k + 3 - kw, c8) + sub);
+              const uint2 A = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 2 - kw, gc) + sub);
+              const uint2 Bv = *reinterpret_cast<const uint2*>(dcB + bx_img(k + 2 - kw, gc) + sub);
+              const uint2 D = *reinterpret_cast<const uint2*>(dsP + bx_img(k + 3 - kw, gc) + sub);
               const float av[4] = {bx_lo(A.x), bx_hi(A.x), bx_lo(A.y), bx_hi(A.y)};
               const float bv[4] = {bx_lo(Bv.x), bx_hi(Bv.x), bx_lo(Bv.y), bx_hi(Bv.y)};
               const float dv[4] = {bx_lo(D.x), bx_hi(D.x), bx_lo(D.y), bx_hi(D.y)};
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const int co = 4 * g + e;
-                pdx = fmaf(av[e], pw1[co * 6 + kw], pdx);
-                pdx = fmaf(bv[e], pw1[co * 6 + 3 + kw], pdx);
-                pdx = fmaf(dv[e], pwd[co * 3 + kw], pdx);
+                const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co];
+                const float w1a[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, wda[3] = {r1.z, r1.w, r2.x};
+                pdx = fmaf(av[e], w1a[kw], pdx);
+                pdx = fmaf(bv[e], w1a[3 + kw], pdx);
+                pdx = fmaf(dv[e], wda[kw], pdx);
               }
             }
           }
@@ -547,7 +613,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           pdx += __shfl_xor(pdx, 4, 64);
           if (hp >= 1 && valid && g == 0) a.dx[((int64_t)n * H + hp - 1) * W + q] = pdx;
           if (valid) {
-            const uint2 C = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 1, c8) + sub);
+            const uint2 C = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 1, gc) + sub);
             const float cv[4] = {bx_lo(C.x), bx_hi(C.x), bx_lo(C.y), bx_hi(C.y)};
             const float xv0[3] = {xa[k + 3], xa[k + 4], xa[k + 5]}, xv1[3] = {xb[k + 3], xb[k + 4], xb[k + 5]};
 #pragma unroll
@@ -558,7 +624,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
                 aw1[e][3 + kw] = fmaf(cv[e], xv1[kw], aw1[e][3 + kw]);
               }
             if (hp < H) {
-              const uint2 S = *reinterpret_cast<const uint2*>(dsC + bx_img(k + 2, c8) + sub);
+              const uint2 S = *reinterpret_cast<const uint2*>(dsC + bx_img(k + 2, gc) + sub);
               const float sv[4] = {bx_lo(S.x), bx_hi(S.x), bx_lo(S.y), bx_hi(S.y)};
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
@@ -571,7 +637,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         }
       }
       if (tid < BXB_XW) xslot(hp + 2)[tid] = xnext;   // the slot of x row hp - 2 (no reader in this row)
-      __syncthreads();   // (3) rings reusable
+      __syncthreads();
     }
   }
 
@@ -587,7 +653,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         out[(tap * BX_C + co) * BX_C + r] = acc2[t][i];
       }
   }
-  float* red = reinterpret_cast<float*>(lds);   // the rings are free: [256][40] thread sums, then [8][48] BN
+  float* red = reinterpret_cast<float*>(lds);   // the rings are free: [256][40] + [256][24] thread sums
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -597,26 +663,11 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     for (int j = 0; j < 3; ++j) red[tid * 40 + 24 + e * 3 + j] = awd[e][j];
     red[tid * 40 + 36 + e] = abias[e];
   }
-  // BN sums: the 32 lanes of a half-wave share their 16 channels
+  float* bred = red + 256 * 40;
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = bsum[q][gg][e];
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
-        bsum[q][gg][e] = v;
-      }
-  float* bred = red + 256 * 40;
-  if (r == 0)
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bred[(wv * 2 + hh) * 48 + q * 16 + gg * 4 + e] = bsum[q][gg][e];
+    for (int k = 0; k < 8; ++k) bred[tid * 24 + q * 8 + k] = bsum[q][k];
   __syncthreads();
   // d w1 [32][6], d wd [32][3], d bias [32]: channel co = 4 g + e sums the 32 threads with tid & 7 == g
   for (int i = tid; i < 32 * 10; i += BX_T) {
@@ -627,10 +678,10 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     const int dst = j < 6 ? 6144 + co * 6 + j : (j < 9 ? 6144 + 192 + co * 3 + (j - 6) : 6144 + 192 + 96 + co);
     out[dst] = s;
   }
-  if (tid < 96) {   // BN sums [3][32]: channel co = 8 gg + 4 hh + e
-    const int q = tid / 32, co = tid % 32, gg = co >> 3, hq = (co >> 2) & 1, e = co & 3;
+  if (tid < 96) {   // BN sums [3][32]: channel co = 8 c8 + k sums the 64 threads with tid & 3 == c8
+    const int q = tid / 32, co = tid % 32, cq = co >> 3, k = co & 7;
     float s = 0.f;
-    for (int w = 0; w < 4; ++w) s += bred[(w * 2 + hq) * 48 + q * 16 + gg * 4 + e];
+    for (int t = 0; t < 64; ++t) s += bred[(t * 4 + cq) * 24 + q * 8 + k];
     out[6144 + 192 + 96 + 32 + q * 32 + co] = s;
   }
 }
