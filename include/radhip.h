@@ -436,6 +436,17 @@ int rdx_wgemm_bf16_ex(const void* A, int64_t lda, const void* B, int64_t ldb, vo
 int64_t rdx_wgemm_ws_bytes(int M, int N, int tile, int splits);
 int64_t rdx_wgemm_counters(int M, int N, int tile);
 
+/* ---- Weight / bias gradients of the head's linears, accumulated in fp32 (csrc/wgrad.hip) ----------------
+ * dW[n][k] += sum_m dY[m][n] X[m][k], db[n] += sum_m dY[m][n] (db may be NULL): bf16 dY [M, ldy] and X [M, ldx],
+ * fp32 dW [N, ldw] (the flat gradient buffer's views), the token rows split over the chip in chunks of
+ * rdx_wgrad_chunk(M, N, K) rows and the chunk partials (ws, >= rdx_wgrad_ws_floats fp32) added in a fixed order:
+ * deterministic. Replaces the addmm(out_dtype = fp32) + sum + add of SideLinear's backward
+ * (radhip/linear.py; the linears of src/models/DualStreamSEMamba.py:445-531, 537-637, 700-770). */
+int rdx_wgrad_chunk(int M, int N, int K);
+int64_t rdx_wgrad_ws_floats(int M, int N, int K);
+int rdx_wgrad_acc(const void* dy, int64_t ldy, const void* x, int64_t ldx, int M, int N, int K, float* dw, int64_t ldw,
+                  float* db, float* ws, int64_t ws_floats, void* stream);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

@@ -107,6 +107,9 @@ SIGNATURES = {
     "rdx_wgemm_bf16_ex": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp,
                                   c_i64, c_vp, c_i64, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "rdx_wgemm_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
+    "rdx_wgrad_chunk": (c_int, [c_int, c_int, c_int]),
+    "rdx_wgrad_ws_floats": (c_i64, [c_int, c_int, c_int]),
+    "rdx_wgrad_acc": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rdx_wgemm_counters": (c_i64, [c_int, c_int, c_int]),
     "rdx_gemm_bf16_strided": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                                       c_vp, c_vp]),

@@ -94,12 +94,18 @@ class SideLinearFn(torch.autograd.Function):
         if side is not cur:
             side.wait_stream(cur)
         with torch.cuda.stream(side):
-            if dy2.dtype == torch.float32:
+            if (_WGRAD and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.stride(-1) == 1
+                    and x2.stride(-1) == 1 and weight.grad.is_contiguous()):
+                # one split-over-tokens MFMA pass + a fixed-order reduce into .grad (csrc/wgrad.hip): hipBLASLt
+                # ran these long-K, tiny-output GEMMs on 5-27 workgroups
+                ops.wgrad_acc(dy2, x2, weight.grad, bias.grad if need_b else None)
+            elif dy2.dtype == torch.float32:
                 weight.grad.addmm_(dy2.t(), x2)
             else:
                 torch.ops.aten.addmm.dtype_out(weight.grad, dy2.t(), x2, torch.float32, beta=1, alpha=1,
                                                out=weight.grad)
-            if need_b:
+            if need_b and not (_WGRAD and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+                               and dy2.stride(-1) == 1 and x2.stride(-1) == 1 and weight.grad.is_contiguous()):
                 bias.grad.add_(dy2.sum(0, dtype=torch.float32))
         if side is cur:
             return dx, None, None, None
@@ -111,6 +117,7 @@ class SideLinearFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+_WGRAD = os.environ.get("RADHIP_WGRAD", "1") != "0"     # csrc/wgrad.hip for the bf16 weight gradients
 _MODE = os.environ.get("RADHIP_SIDE_LINEAR", "2")   # "2": main stream; "1": side stream; "0": F.linear
 _ON = _MODE != "0"
 

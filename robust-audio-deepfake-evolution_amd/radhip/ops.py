@@ -1202,6 +1202,24 @@ def wgemm_policy(name, M, N, K):
     return (int(ent[0]), int(ent[1])) if ent is not None else None
 
 
+def wgrad_acc(dy, x, dw, db=None):
+    """dw += dy^T x and db += dy.sum(0) in fp32 on csrc/wgrad.hip: dy [M, N], x [M, K] bf16 row views (unit inner
+    stride), dw fp32 [N, K] (row stride >= K, unit inner stride), db fp32 [N] or None."""
+    _require_gpu(dy, x)
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or dy.stride(-1) != 1 or x.stride(-1) != 1:
+        raise ValueError("radhip wgrad_acc: bf16 operands with unit inner stride required")
+    M, N = dy.shape
+    M2, K = x.shape
+    if M != M2 or dw.shape != (N, K) or dw.dtype != torch.float32 or dw.stride(-1) != 1:
+        raise ValueError(f"radhip wgrad_acc: shapes dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)}")
+    if db is not None and (db.shape != (N,) or db.dtype != torch.float32 or not db.is_contiguous()):
+        raise ValueError("radhip wgrad_acc: db must be fp32 [N]")
+    ws = torch.empty(int(lib().rdx_wgrad_ws_floats(M, N, K)), device=dy.device, dtype=torch.float32)
+    with _timed("wgrad_acc", dy, gemm_flops(N, K, M)):
+        check(lib().rdx_wgrad_acc(_p(dy), dy.stride(0), _p(x), x.stride(0), M, N, K, _p(dw), dw.stride(0),
+                                  _p(db) if db is not None else None, _p(ws), ws.numel(), _stream(dy)), "wgrad_acc")
+
+
 _WG_WS = {}
 
 
