@@ -269,18 +269,20 @@ int rdx_sincnet_b0_nblk(int64_t npix);
  * equal bit for bit to rdx_sincnet_b0_fwd + rdx_sconv_fwd + rdx_res_tail_fwd without their four full-size
  * intermediates. x [N, H, W] bf16 (one channel); w1 [32][6] / wd [32][3] fp32 (bf16 values); bn [4][32]
  * (conv1 bias, mean, invstd * gamma, beta); w2 [6][32 co][32 ci] bf16 tap-major; bias [32] = conv2.bias +
- * conv_downsample.bias. */
+ * conv_downsample.bias; o1 (optional, else NULL): out1 = selu(bn2(conv1(x) + cb)) NHWC bf16 [N, H + 1, W, 32]
+ * for the backward. */
 int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, const float* bn, const void* w2, const float* bias,
-                void* y, uint8_t* arg, int N, int H, int W, void* stream);
+                void* y, uint8_t* arg, void* o1, int N, int H, int W, void* stream);
 /* Its backward in one pass (recomputing c and out1 from x): dx fp32 [N, H, W] and one partial row per
  * workgroup, part [rdx_b0x_bwd_nblk(N, W)][6560] fp32 = d conv2.weight [6 taps][32 co][32 ci] | d conv1.weight
  * [32][6] | d conv_downsample.weight [32][3] | d bias [32] (both conv biases) | BN sums [3][32] (d conv1.bias,
  * d gamma, d beta); the caller sums the rows. dp = the pooled output gradient (NHWC bf16), arg = the forward's
  * argmax, bn [5][32] (conv1 bias, mean, invstd * gamma, beta, invstd), w2f = [6][32 ci][32 co] conv2 weights
- * flipped in both axes (the input-gradient layout of rdx_sconv_fwd). */
+ * flipped in both axes (the input-gradient layout of rdx_sconv_fwd); o1 = the forward's out1, or NULL to
+ * recompute it from x. */
 int rdx_b0x_bwd_nblk(int N, int W);
 int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, const float* w1, const float* wd, const float* bn,
-                const void* w2f, float* dx, float* part, int N, int H, int W, void* stream);
+                const void* w2f, const void* o1, float* dx, float* part, int N, int H, int W, void* stream);
 int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di, const float* w1, const float* wd, float* dx,
                        float* part, int N, int H, int W, int C, void* stream);
 

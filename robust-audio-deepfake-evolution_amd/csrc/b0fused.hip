@@ -59,6 +59,7 @@ struct BxFwdArgs {
   const float* bias;         // [32] conv2.bias + conv_downsample.bias
   __hip_bfloat16* y;         // [N, H, Wo, 32] pooled output (NHWC)
   uint8_t* arg;              // [N, H, Wo, 32] window argmax (0..2)
+  __hip_bfloat16* o1;        // optional: out1 [N, H + 1, W, 32] (NHWC) for the backward, or null
   int N, H, W, Wo, rows_per;
 };
 
@@ -128,6 +129,11 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
         o[k >> 1] = (q >= 0 && q < W) ? bx_pack2(yv[0], yv[1]) : 0u;
       }
       *reinterpret_cast<uint4*>(sl + bx_img(pp, g8)) = make_uint4(o[0], o[1], o[2], o[3]);
+      // out1 for the backward: the strip's own positions, each row once (a chunk's last row is the next
+      // chunk's first)
+      if (a.o1 && pp >= 1 && pp <= BX_P && q < W && (ro < h1 || ro == H))
+        *reinterpret_cast<uint4*>(a.o1 + (((int64_t)n * (H + 1) + ro) * W + q) * BX_C + 8 * g8) =
+            make_uint4(o[0], o[1], o[2], o[3]);
     }
   };
   const int pw = wv * 32 + r;   // this lane's output position q0 + pw (B operand row of the MFMA)
@@ -215,7 +221,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
 using namespace rdx;
 
 extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, const float* bn, const void* w2,
-                           const float* bias, void* y, uint8_t* arg, int N, int H, int W, void* stream) {
+                           const float* bias, void* y, uint8_t* arg, void* o1, int N, int H, int W, void* stream) {
   RDX_REQUIRE(x && w1 && wd && bn && w2 && bias && y && arg && N > 0 && H > 0 && W >= 3);
   RDX_REQUIRE(((uintptr_t)y & 15) == 0 && ((uintptr_t)arg & 7) == 0 && ((uintptr_t)w2 & 15) == 0);
   RDX_REQUIRE(N < 65536);
@@ -233,8 +239,9 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
+  RDX_REQUIRE(((uintptr_t)o1 & 15) == 0);
   BxFwdArgs a{(const __hip_bfloat16*)x, w1, wd, bn, (const __hip_bfloat16*)w2, bias, (__hip_bfloat16*)y, arg,
-              N, H, W, Wo, rows_per};
+              (__hip_bfloat16*)o1, N, H, W, Wo, rows_per};
   hipLaunchKernelGGL(b0x_fwd_kernel, dim3((unsigned)strips, (unsigned)N, (unsigned)nz), dim3(BX_T), BX_LDS,
                      as_stream(stream), a);
   RDX_LAUNCH_CHECK();
@@ -320,6 +327,7 @@ struct BxBwdArgs {
   const float* wd;            // [32][3]
   const float* bn;            // [5][32]: conv1 bias, mean, invstd * gamma, beta, invstd
   const __hip_bfloat16* w2f;  // [6][32 ci][32 co] conv2 weights flipped in both axes, transposed (input gradient)
+  const __hip_bfloat16* o1;   // the forward's out1 [N, H + 1, W, 32], or null (recomputed from x)
   float* dx;                  // [N, H, W]
   float* part;                // [gridDim.x][BXB_NPART]: d w2 [6][32 co][32 ci], d w1 [32][6], d wd [32][3],
                               //   d bias [32], BN sums [3][32]
@@ -418,6 +426,30 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         *reinterpret_cast<uint4*>(sl + bx_img(i, c8)) = make_uint4(o[0], o[1], o[2], o[3]);
       }
     };
+    // out1 rows from the forward's saved tensor (a.o1): fetched a row ahead, 16-byte chunks of positions
+    // q0 - 3 + i, i < 132 (zero outside [0, W))
+    constexpr int ON = (132 * 4 + BX_T - 1) / BX_T;
+    uint4 po[ON];
+    auto fetch_o1 = [&](int ro) {
+#pragma unroll
+      for (int j = 0; j < ON; ++j) {
+        const int it = tid + BX_T * j;
+        const int i = it >> 2;
+        const int q = q0 - 3 + i;
+        po[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (it < 132 * 4 && ro <= H && q >= 0 && q < W)
+          po[j] = *reinterpret_cast<const uint4*>(a.o1 + (((int64_t)n * (H + 1) + ro) * W + q) * BX_C + 8 * c8);
+      }
+    };
+    auto store_o1 = [&](int ro) {
+      char* sl = o1r + (ro & 1) * BX_IMG;
+#pragma unroll
+      for (int j = 0; j < ON; ++j) {
+        const int it = tid + BX_T * j;
+        if (it < 132 * 4) *reinterpret_cast<uint4*>(sl + bx_img(it >> 2, c8)) = po[j];
+      }
+    };
+    const bool saved = a.o1 != nullptr;
     // ds row hrow: the pooled gradient where the window argmax hits, fetched a row ahead into registers
     uint4 pd[DSN];
     uint2 pa[DSN];
@@ -470,14 +502,24 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     fetch_ds(-1);
     store_ds(-1);       // zeros
     fetch_ds(0);
+    if (saved) {
+      fetch_o1(0);
+      store_o1(0);
+      fetch_o1(1);
+    }
     __syncthreads();
-    make_out1(0);
+    if (!saved) make_out1(0);
     for (int hp = 0; hp <= H; ++hp) {
       // ---- phase A: ds row hp (registers -> LDS), next row's fetch, out1 row hp + 1
       const float xnext = load_x(hp + 2);
       store_ds(hp);
       fetch_ds(hp + 1);
-      if (hp + 1 <= H) make_out1(hp + 1);
+      if (saved) {
+        if (hp + 1 <= H) store_o1(hp + 1);
+        fetch_o1(hp + 2);
+      } else if (hp + 1 <= H) {
+        make_out1(hp + 1);
+      }
       __syncthreads();
       // ---- phase B: dout1 row hp = conv(ds rows hp - 1, hp) with the flipped weights -> bf16 into the dc slot;
       // d w2 += ds row hp x out1 rows hp, hp + 1 over K = ds image rows 2 .. 129 (positions q0 .. q0 + 127); rows
@@ -692,8 +734,8 @@ extern "C" int rdx_b0x_bwd_nblk(int N, int W) {
 }
 
 extern "C" int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, const float* w1, const float* wd,
-                           const float* bn, const void* w2f, float* dx, float* part, int N, int H, int W,
-                           void* stream) {
+                           const float* bn, const void* w2f, const void* o1, float* dx, float* part, int N, int H,
+                           int W, void* stream) {
   RDX_REQUIRE(x && dp && arg && w1 && wd && bn && w2f && dx && part && N > 0 && H > 0 && W >= 3);
   RDX_REQUIRE(((uintptr_t)dp & 15) == 0 && ((uintptr_t)arg & 7) == 0 && ((uintptr_t)w2f & 15) == 0);
   static bool attr = false;
@@ -703,8 +745,9 @@ extern "C" int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, co
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  BxBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)dp, arg, w1, wd, bn, (const __hip_bfloat16*)w2f, dx,
-              part, N, H, W, W / 3, W / 3 / BX_J + 1};
+  RDX_REQUIRE(((uintptr_t)o1 & 15) == 0);
+  BxBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)dp, arg, w1, wd, bn, (const __hip_bfloat16*)w2f,
+              (const __hip_bfloat16*)o1, dx, part, N, H, W, W / 3, W / 3 / BX_J + 1};
   hipLaunchKernelGGL(b0x_bwd_kernel, dim3((unsigned)rdx_b0x_bwd_nblk(N, W)), dim3(BX_T), BXB_LDS, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return RDX_OK;

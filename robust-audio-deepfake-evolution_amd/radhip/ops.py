@@ -923,10 +923,15 @@ class Block0Fused(torch.autograd.Function):
         bias = (b2.detach().float() + bd.detach().float()).contiguous()
         y = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
         arg = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.uint8, memory_format=torch.channels_last)
-        # MFMA work: conv2 (32 -> 32, 2 x 3) over N x H x W positions; HBM: x in, y + argmax out
+        # out1 for the one-pass backward (it reads it instead of recomputing conv1 + BN + SELU: VALU-bound there)
+        save_o1 = torch.is_grad_enabled() and os.environ.get("RADHIP_B0X_BWD", "1") != "0" and \
+            os.environ.get("RADHIP_B0X_SAVE", "1") != "0"
+        o1 = torch.empty(N, H + 1, W, C, device=x.device, dtype=torch.bfloat16) if save_o1 else None
+        # MFMA work: conv2 (32 -> 32, 2 x 3) over N x H x W positions; HBM: x in, y + argmax (+ out1) out
         with _timed("b0x_fwd", x, 2.0 * N * H * W * 32 * 192):
-            check(lib().rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg), N, H, W,
-                                    _stream(x)), "b0x_fwd")
+            check(lib().rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg),
+                                    _p(o1) if o1 is not None else None, N, H, W, _stream(x)), "b0x_fwd")
+        ctx.o1 = o1
         ctx.save_for_backward(xb, w1b, wdb, wd2, bn5, arg, *f32)
         ctx.meta = (tuple(w1.shape), tuple(wd.shape), x.dtype, tuple(w2.shape), w2.dtype)
         return y
@@ -942,9 +947,12 @@ class Block0Fused(torch.autograd.Function):
             dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
             part = torch.empty(lib().rdx_b0x_bwd_nblk(N, W), 6560, device=xb.device, dtype=torch.float32)
             # MFMA work: conv2's input gradient and weight gradient (2 x the forward's conv2)
+            o1 = ctx.o1
             with _timed("b0x_bwd", dy, 4.0 * N * H * W * 32 * 192):
-                check(lib().rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2), _p(dx), _p(part),
-                                        N, H, W, _stream(dy)), "b0x_bwd")
+                check(lib().rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2),
+                                        _p(o1) if o1 is not None else None, _p(dx), _p(part), N, H, W, _stream(dy)),
+                      "b0x_bwd")
+            ctx.o1 = None
             tot = part.sum(0)
             dw2 = tot[:6144].view(2, 3, C, C).permute(2, 3, 0, 1)
             dw1 = tot[6144:6336].reshape(w1_shape)

@@ -585,6 +585,13 @@ def swa_bn_update(model, feeder, augmenter, device):
     return n
 
 
+def layerdrop_draws(n):
+    """HF WavLM's LayerDrop draws, torch.rand([]) once per layer on the CPU generator, as ONE torch.rand(n): the
+    same values and the same generator state afterwards (tests/test_recipe_cpu.py checks it), at 1/20 of the
+    host time (24 scalar draws took ~80 us per forward)."""
+    return torch.rand(n).numpy().astype(np.float64)
+
+
 class _PinnedRing:
     """Small ring of pinned host slots for H2D copies of per-replay inputs (non_blocking, stream-ordered;
     a slot is reused only after the copy that read it has executed)."""
@@ -687,7 +694,7 @@ class GraphedMicroStep:
               if self.spec_on else np.zeros((self.B, self.T), dtype=bool))
         p = c.layerdrop
         keep = np.ones(self.nl, dtype=bool)
-        r = np.array([float(torch.rand([])) for _ in range(self.nl)])   # one CPU draw per layer, as HF
+        r = layerdrop_draws(self.nl)   # one CPU draw per layer, as HF
         if p > 0:
             keep[1:] = ~(r[1:] < p)
         lo, hi = self.conv.draw_mask() if self.tr.freq_aug else (0, 0)

@@ -25,7 +25,7 @@ import torch
 
 from . import ops
 from .linear import direct_grad
-from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay
+from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay, layerdrop_draws
 from .wavlm import compute_time_mask
 
 
@@ -147,7 +147,7 @@ class WindowStep:
               if self.spec_on else np.zeros((self.B, self.T), dtype=bool))
         p = c.layerdrop
         keep = np.ones(self.nl, dtype=bool)
-        r = np.array([float(torch.rand([])) for _ in range(self.nl)])
+        r = layerdrop_draws(self.nl)
         if p > 0:
             keep[1:] = ~(r[1:] < p)
         lo, hi = self.conv.draw_mask() if self.tr.freq_aug else (0, 0)

@@ -232,3 +232,18 @@ def test_step_refuses_tunableop_tuning(monkeypatch):
         refuse_step_tuning()
     monkeypatch.setenv("PYTORCH_TUNABLEOP_TUNING", "0")
     refuse_step_tuning()
+
+
+def test_layerdrop_draws_match_scalar_draws():
+    """One torch.rand(n) gives the values and the generator state of n torch.rand([]) calls (HF WavLM's LayerDrop
+    draw, one per layer), so batching them keeps the reference's CPU RNG stream."""
+    import torch
+    from radhip.train import layerdrop_draws
+    for n in (1, 5, 16, 24, 25, 48):
+        torch.manual_seed(123 + n)
+        a = [float(torch.rand([])) for _ in range(n)]
+        sa = torch.get_rng_state()
+        torch.manual_seed(123 + n)
+        b = layerdrop_draws(n)
+        sb = torch.get_rng_state()
+        assert a == list(b) and torch.equal(sa, sb)
