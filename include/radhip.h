@@ -269,20 +269,18 @@ int rdx_sincnet_b0_nblk(int64_t npix);
  * equal bit for bit to rdx_sincnet_b0_fwd + rdx_sconv_fwd + rdx_res_tail_fwd without their four full-size
  * intermediates. x [N, H, W] bf16 (one channel); w1 [32][6] / wd [32][3] fp32 (bf16 values); bn [4][32]
  * (conv1 bias, mean, invstd * gamma, beta); w2 [6][32 co][32 ci] bf16 tap-major; bias [32] = conv2.bias +
- * conv_downsample.bias; o1 (optional, else NULL): out1 = selu(bn2(conv1(x) + cb)) NHWC bf16 [N, H + 1, W, 32]
- * for the backward. */
+ * conv_downsample.bias. */
 int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, const float* bn, const void* w2, const float* bias,
-                void* y, uint8_t* arg, void* o1, int N, int H, int W, void* stream);
-/* Its backward in one pass (recomputing c and out1 from x): dx fp32 [N, H, W] and one partial row per
+                void* y, uint8_t* arg, int N, int H, int W, void* stream);
+/* Its backward in one pass (recomputing c and out1 from x, one exp for both out1 and the SELU derivative): dx fp32 [N, H, W] and one partial row per
  * workgroup, part [rdx_b0x_bwd_nblk(N, W)][6560] fp32 = d conv2.weight [6 taps][32 co][32 ci] | d conv1.weight
  * [32][6] | d conv_downsample.weight [32][3] | d bias [32] (both conv biases) | BN sums [3][32] (d conv1.bias,
  * d gamma, d beta); the caller sums the rows. dp = the pooled output gradient (NHWC bf16), arg = the forward's
  * argmax, bn [5][32] (conv1 bias, mean, invstd * gamma, beta, invstd), w2f = [6][32 ci][32 co] conv2 weights
- * flipped in both axes (the input-gradient layout of rdx_sconv_fwd); o1 = the forward's out1, or NULL to
- * recompute it from x. */
+ * flipped in both axes (the input-gradient layout of rdx_sconv_fwd). */
 int rdx_b0x_bwd_nblk(int N, int W);
 int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, const float* w1, const float* wd, const float* bn,
-                const void* w2f, const void* o1, float* dx, float* part, int N, int H, int W, void* stream);
+                const void* w2f, float* dx, float* part, int N, int H, int W, void* stream);
 int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di, const float* w1, const float* wd, float* dx,
                        float* part, int N, int H, int W, int C, void* stream);
 
@@ -328,6 +326,17 @@ int rdx_attn_bwd_fused(const void* q, int64_t ldq, const void* k, int64_t ldk, c
                        const void* o, int64_t ldo, const float* lse, const void* dout, int64_t lddo, float* D,
                        void* dq, void* dk, void* dv, int64_t ldg, float* dgate, int B, int T, int H, int head_dim,
                        void* stream);
+/* The same for grids of fewer (b, h) than CUs: two workgroups per (b, h) split the key tiles; each writes its
+ * fp32 partial dQ / d gate to ws (>= rdx_attn_bwd_split_ws(B, H) floats) and the second to finish adds them in
+ * part order (an agent-scope ticket per (b, h) in counters, zero before the first launch, left zero). B * H % 8
+ * == 0. One workspace per stream. */
+int64_t rdx_attn_bwd_split_ws(int B, int H);
+int rdx_attn_bwd_fused_split(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                             const float* gate, const float* rel_bias, const uint32_t* keep_mask, float p_drop,
+                             float scale, const void* o, int64_t ldo, const float* lse, const void* dout,
+                             int64_t lddo, float* D, void* dq, void* dk, void* dv, int64_t ldg, float* dgate,
+                             float* ws, int64_t ws_floats, int* counters, int64_t n_counters, int B, int T, int H,
+                             int head_dim, void* stream);
 int rdx_attn_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* keep, int64_t n, int T,
                           void* stream);
 /* the element-wise dropout of the fused WavLM layer kernels below (element t kept iff

@@ -581,20 +581,30 @@ __device__ __forceinline__ bf16x8 lds_tr(const char* lo, const char* hi) {
   return r;
 }
 
-template <bool kDrop>
+// kSplit (grids of fewer (b, h) than CUs, B = 8): TWO workgroups per (b, h), part p taking the key tiles
+// [kbeg, kend) (the first ceil(nt / 2), the rest) in phase 1 and in phase 2's sum over keys; each writes its
+// partial dQ / d gate (fp32) to ws, and the second to arrive (agent-scope release / acquire, a self-resetting
+// ticket) adds the two in part order and stores dQ and d gate. Per CU: half the phase-1 MFMAs, 4 / 7 of phase 2.
+constexpr int FB_WSP = AT_FUSED_MAXNT * AT_TILE * (AT_DH + 1);   // fp32 per (b, h, part): dQ [tp][64], d gate [tp]
+
+template <bool kDrop, bool kSplit = false>
 __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     AttnArgs a, AttnBwdArgs g, const uint32_t* __restrict__ mask,
     const __hip_bfloat16* __restrict__ O, int64_t ldo,
     __hip_bfloat16* __restrict__ dq, __hip_bfloat16* __restrict__ dk, __hip_bfloat16* __restrict__ dv, int64_t ldg,
-    float* __restrict__ dgate) {
+    float* __restrict__ dgate, float* __restrict__ ws, int* __restrict__ counters) {
   extern __shared__ __attribute__((aligned(16))) char at_lds[];
   char* const L = at_lds;
   const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE, tp = nt * AT_TILE;
   // blocks of one head on one XCD (blocks b and b + 8 share an XCD): the head's bias row stays in that XCD's L2.
   // A speed choice only; any placement is correct.
-  int head, b;
+  int head, b, part = 0;
   {
-    const int bid = blockIdx.x;
+    int bid = blockIdx.x;
+    if (kSplit) {   // the two parts of a (b, h) are blocks bid and bid + 8 (one XCD)
+      part = (bid >> 3) & 1;
+      bid = (bid & 7) | ((bid >> 4) << 3);
+    }
     if ((H & 7) == 0) {
       const int xcd = bid & 7, j = bid >> 3, hpx = H >> 3;
       head = xcd + 8 * (j % hpx);
@@ -617,9 +627,11 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
   // ---- phase 0: every global load of the phase in flight at once (Q and dO images, the O row and
   // scalars of this thread's query row, this wave's K / V fragments), then the LDS writes; D =
   // rowsum(dO o O) after a barrier, from the dO image (dO is read from HBM once)
-  const int kb = __builtin_amdgcn_readfirstlane(w);
+  const int kbeg = kSplit && part ? (nt + 1) / 2 : 0, kend = kSplit && !part ? (nt + 1) / 2 : nt;
+  const int kb = __builtin_amdgcn_readfirstlane(w) + kbeg;
+  const bool kact = kb < kend;       // this wave has a key tile in phase 1
   const int key = kb * AT_TILE + r;
-  const bool kvalid = key < T;
+  const bool kvalid = kact && key < T;
   bf16x8 kf[4], vf[4];
   {
     bf16x8 qv[4], ov[4], xo[8];
@@ -664,7 +676,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) dd = fmaf((float)xd[j], (float)xo[c][j], dd);
       }
-      if (trow) g.D[bh * T + t] = dd;
+      if (trow && part == 0) g.D[bh * T + t] = dd;
       s_D[t] = dd;
     }
   }
@@ -672,8 +684,8 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
   const int tr0 = fb_tr_off(lane, 0), tr1 = fb_tr_off(lane, 1);
   __syncthreads();
   RDX_PROBE(1);
-  // ---- phase 1: wave w owns key tile kb = w
-  {
+  // ---- phase 1: wave w owns key tile kb = kbeg + w
+  if (kact) {
     // this lane's key in a mask word of the forward: bit i + 16 h with crow(i, h) = r
     const int bitpos = (r & 3) + 4 * (r >> 3) + 16 * ((r >> 2) & 1);
     const float scale2 = a.scale * kLog2e;
@@ -777,8 +789,10 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
   // kb*32 + r, columns 16 s + 8 hh .. + 7 = chunk 2 s + hh (zero rows past T)
   RDX_PROBE(7);
   __syncthreads();  // every dS panel is complete; the Q image is free
+  if (kact) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(L + FB_Q + img_off(kb * AT_TILE + r, 2 * s + hh)) = kf[s];
+    for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(L + FB_Q + img_off(kb * AT_TILE + r, 2 * s + hh)) = kf[s];
+  }
   __syncthreads();
   RDX_PROBE(3);
   // ---- phase 2: wave w owns query tile qb = w
@@ -790,7 +804,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     const char* P1 = L + FB_DS + qb * tp * 64 + fb_pan_off(lane, 1);
     f32x16 dqacc[2] = {zero16(), zero16()};
     float dg = 0.f;
-    for (int kb2 = 0; kb2 < nt; ++kb2) {
+    for (int kb2 = kbeg; kb2 < kend; ++kb2) {
       float pbv[16];
       rel16_q(tab, qi, T, tp, kb2, hh, pbv);
       // dS of a key past T is finite but meaningless (phase 1 does not mask keys): its bias weight is 0
@@ -815,16 +829,64 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     }
     RDX_PROBE(4);
     dg += __shfl_xor(dg, 32, 64);
-    if (qvalid && hh == 0) dgate[(row0 + qi) * H + head] = dg;
-    // C[q][d]: col = d (lane), row = q (registers)
+    if (kSplit) {   // partials of this part: dQ [tp][64] then d gate [tp]
+      float* wp = ws + (bh * 2 + part) * FB_WSP;
+      if (qvalid && hh == 0) wp[AT_FUSED_MAXNT * AT_TILE * AT_DH + qi] = dg;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qq = qb * AT_TILE + crow(i, hh);
-      if (qq < T) {
+      for (int i = 0; i < 16; ++i) {
+        const int qq = qb * AT_TILE + crow(i, hh);
+        if (qq < T) {
 #pragma unroll
-        for (int db = 0; db < 2; ++db)
-          dq[(row0 + qq) * ldg + col0 + db * 32 + r] = __float2bfloat16(dqacc[db][i] * a.scale);
+          for (int db = 0; db < 2; ++db) wp[qq * AT_DH + db * 32 + r] = dqacc[db][i];
+        }
       }
+    } else {
+      if (qvalid && hh == 0) dgate[(row0 + qi) * H + head] = dg;
+      // C[q][d]: col = d (lane), row = q (registers)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qq = qb * AT_TILE + crow(i, hh);
+        if (qq < T) {
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+            dq[(row0 + qq) * ldg + col0 + db * 32 + r] = __float2bfloat16(dqacc[db][i] * a.scale);
+        }
+      }
+    }
+  }
+  if (kSplit) {
+    // publish (every wave's stores retired, then one agent-scope release and the ticket); the second arriver
+    // acquires and combines (cdna_hip_programming.md Guideline 16); the ticket is left at zero
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(L + FB_SC);   // the row-scalar area is free in phase 2
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = t;
+      if (t == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        counters[bh] = 0;
+      }
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(flag[0]) == 1) {
+      const float* w0 = ws + (bh * 2) * FB_WSP;
+      const float* w1 = w0 + FB_WSP;
+      for (int i = threadIdx.x; i < T * (AT_DH / 4); i += nthr) {
+        const int qq = i / (AT_DH / 4), c4 = (i - qq * (AT_DH / 4)) * 4;
+        const float4 x0 = *reinterpret_cast<const float4*>(w0 + qq * AT_DH + c4);
+        const float4 x1 = *reinterpret_cast<const float4*>(w1 + qq * AT_DH + c4);
+        __hip_bfloat16* dst = dq + (row0 + qq) * ldg + col0 + c4;
+        dst[0] = __float2bfloat16((x0.x + x1.x) * a.scale);
+        dst[1] = __float2bfloat16((x0.y + x1.y) * a.scale);
+        dst[2] = __float2bfloat16((x0.z + x1.z) * a.scale);
+        dst[3] = __float2bfloat16((x0.w + x1.w) * a.scale);
+      }
+      for (int t = threadIdx.x; t < T; t += nthr)
+        dgate[(row0 + t) * H + head] = w0[AT_FUSED_MAXNT * AT_TILE * AT_DH + t] + w1[AT_FUSED_MAXNT * AT_TILE * AT_DH + t];
     }
   }
   RDX_PROBE(5);
@@ -979,15 +1041,16 @@ extern "C" int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
                                    (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg, dgate);
 }
 
-template <bool kDrop>
+template <bool kDrop, bool kSplit>
 static int launch_bwd_fused(dim3 grid, dim3 block, size_t lds, hipStream_t st, const AttnArgs& a,
                             const AttnBwdArgs& g, const uint32_t* mask, const void* o, int64_t ldo,
-                            void* dq, void* dk, void* dv, int64_t ldg, float* dgate) {
+                            void* dq, void* dk, void* dv, int64_t ldg, float* dgate, float* ws, int* counters) {
   static bool done = false;
-  const int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_bwd_fused_kernel<kDrop>), done);
+  const int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_bwd_fused_kernel<kDrop, kSplit>), done);
   if (rc != RDX_OK) return rc;
-  hipLaunchKernelGGL((attn_bwd_fused_kernel<kDrop>), grid, block, lds, st, a, g, mask, (const __hip_bfloat16*)o,
-                     ldo, (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg, dgate);
+  hipLaunchKernelGGL((attn_bwd_fused_kernel<kDrop, kSplit>), grid, block, lds, st, a, g, mask,
+                     (const __hip_bfloat16*)o, ldo, (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg,
+                     dgate, ws, counters);
   return RDX_OK;
 }
 
@@ -1010,10 +1073,41 @@ extern "C" int rdx_attn_bwd_fused(const void* q, int64_t ldq, const void* k, int
   const dim3 grid((unsigned)(B * H)), block(nt * 64);
   (void)tp;
   hipStream_t st = as_stream(stream);
-  const int rc = a.thr ? launch_bwd_fused<true>(grid, block, lds, st, a, g, keep_mask, o, ldo, dq, dk, dv,
-                                                ldg, dgate)
-                       : launch_bwd_fused<false>(grid, block, lds, st, a, g, keep_mask, o, ldo, dq, dk,
-                                                 dv, ldg, dgate);
+  const int rc = a.thr ? launch_bwd_fused<true, false>(grid, block, lds, st, a, g, keep_mask, o, ldo, dq, dk, dv,
+                                                       ldg, dgate, nullptr, nullptr)
+                       : launch_bwd_fused<false, false>(grid, block, lds, st, a, g, keep_mask, o, ldo, dq, dk,
+                                                        dv, ldg, dgate, nullptr, nullptr);
+  if (rc != RDX_OK) return rc;
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+extern "C" int64_t rdx_attn_bwd_split_ws(int B, int H) { return (int64_t)B * H * 2 * FB_WSP; }
+
+extern "C" int rdx_attn_bwd_fused_split(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                        int64_t ldv, const float* gate, const float* rel_bias,
+                                        const uint32_t* keep_mask, float p_drop, float scale, const void* o,
+                                        int64_t ldo, const float* lse, const void* dout, int64_t lddo, float* D,
+                                        void* dq, void* dk, void* dv, int64_t ldg, float* dgate, float* ws,
+                                        int64_t ws_floats, int* counters, int64_t n_counters, int B, int T, int H,
+                                        int head_dim, void* stream) {
+  RDX_REQUIRE(attn_ok(q, ldq, k, ldk, v, ldv, B, T, H) && gate && rel_bias && o && lse && dout && D);
+  RDX_REQUIRE(dq && dk && dv && dgate && ldg >= (int64_t)H * AT_DH && ldg % 8 == 0 && lddo % 8 == 0 && ldo % 8 == 0);
+  RDX_REQUIRE(((uintptr_t)o & 15) == 0 && ((uintptr_t)dout & 15) == 0);
+  RDX_REQUIRE(p_drop >= 0.f && p_drop < 1.f && (p_drop == 0.f || keep_mask));
+  RDX_REQUIRE(ws && counters && ((uintptr_t)ws & 15) == 0 && ws_floats >= rdx_attn_bwd_split_ws(B, H) &&
+              n_counters >= (int64_t)B * H);
+  RDX_REQUIRE(((int64_t)B * H) % 8 == 0 && (int64_t)B * H * 2 <= 0x7fffffff);   // the block -> part map
+  if (head_dim != AT_DH || T > AT_FUSED_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
+  const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, rel_bias, nullptr, 0, p_drop, scale, B, T, H);
+  const AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
+  const int nt = (T + AT_TILE - 1) / AT_TILE;
+  const dim3 grid((unsigned)(2 * B * H)), block(nt * 64);
+  hipStream_t st = as_stream(stream);
+  const int rc = a.thr ? launch_bwd_fused<true, true>(grid, block, FB_LDS, st, a, g, keep_mask, o, ldo, dq, dk, dv,
+                                                      ldg, dgate, ws, counters)
+                       : launch_bwd_fused<false, true>(grid, block, FB_LDS, st, a, g, keep_mask, o, ldo, dq, dk, dv,
+                                                       ldg, dgate, ws, counters);
   if (rc != RDX_OK) return rc;
   RDX_LAUNCH_CHECK();
   return RDX_OK;

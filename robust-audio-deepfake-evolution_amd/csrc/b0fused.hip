@@ -59,7 +59,6 @@ struct BxFwdArgs {
   const float* bias;         // [32] conv2.bias + conv_downsample.bias
   __hip_bfloat16* y;         // [N, H, Wo, 32] pooled output (NHWC)
   uint8_t* arg;              // [N, H, Wo, 32] window argmax (0..2)
-  __hip_bfloat16* o1;        // optional: out1 [N, H + 1, W, 32] (NHWC) for the backward, or null
   int N, H, W, Wo, rows_per;
 };
 
@@ -129,11 +128,6 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
         o[k >> 1] = (q >= 0 && q < W) ? bx_pack2(yv[0], yv[1]) : 0u;
       }
       *reinterpret_cast<uint4*>(sl + bx_img(pp, g8)) = make_uint4(o[0], o[1], o[2], o[3]);
-      // out1 for the backward: the strip's own positions, each row once (a chunk's last row is the next
-      // chunk's first)
-      if (a.o1 && pp >= 1 && pp <= BX_P && q < W && (ro < h1 || ro == H))
-        *reinterpret_cast<uint4*>(a.o1 + (((int64_t)n * (H + 1) + ro) * W + q) * BX_C + 8 * g8) =
-            make_uint4(o[0], o[1], o[2], o[3]);
     }
   };
   const int pw = wv * 32 + r;   // this lane's output position q0 + pw (B operand row of the MFMA)
@@ -221,7 +215,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
 using namespace rdx;
 
 extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, const float* bn, const void* w2,
-                           const float* bias, void* y, uint8_t* arg, void* o1, int N, int H, int W, void* stream) {
+                           const float* bias, void* y, uint8_t* arg, int N, int H, int W, void* stream) {
   RDX_REQUIRE(x && w1 && wd && bn && w2 && bias && y && arg && N > 0 && H > 0 && W >= 3);
   RDX_REQUIRE(((uintptr_t)y & 15) == 0 && ((uintptr_t)arg & 7) == 0 && ((uintptr_t)w2 & 15) == 0);
   RDX_REQUIRE(N < 65536);
@@ -239,9 +233,8 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  RDX_REQUIRE(((uintptr_t)o1 & 15) == 0);
   BxFwdArgs a{(const __hip_bfloat16*)x, w1, wd, bn, (const __hip_bfloat16*)w2, bias, (__hip_bfloat16*)y, arg,
-              (__hip_bfloat16*)o1, N, H, W, Wo, rows_per};
+              N, H, W, Wo, rows_per};
   hipLaunchKernelGGL(b0x_fwd_kernel, dim3((unsigned)strips, (unsigned)N, (unsigned)nz), dim3(BX_T), BX_LDS,
                      as_stream(stream), a);
   RDX_LAUNCH_CHECK();
@@ -274,7 +267,7 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
 constexpr int BXB_DCR = 128;                         // dc image rows: positions q0 - 1 .. q0 + 126
 constexpr int BXB_XW = 136;                          // staged x positions q0 - 4 .. q0 + 131
 constexpr int BXB_NPART = 6 * 32 * 32 + 32 * 6 + 32 * 3 + 32 + 3 * 32;
-constexpr int BXB_LDS = 192 * 64 + 2 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + 32 * 64;
+constexpr int BXB_LDS = 192 * 64 + 3 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + 32 * 64;
 constexpr int BXB_BLOCKS = 512;
 
 typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 bxbf16x4v;
@@ -327,18 +320,36 @@ struct BxBwdArgs {
   const float* wd;            // [32][3]
   const float* bn;            // [5][32]: conv1 bias, mean, invstd * gamma, beta, invstd
   const __hip_bfloat16* w2f;  // [6][32 ci][32 co] conv2 weights flipped in both axes, transposed (input gradient)
-  const __hip_bfloat16* o1;   // the forward's out1 [N, H + 1, W, 32], or null (recomputed from x)
   float* dx;                  // [N, H, W]
   float* part;                // [gridDim.x][BXB_NPART]: d w2 [6][32 co][32 ci], d w1 [32][6], d wd [32][3],
                               //   d bias [32], BN sums [3][32]
   int N, H, W, Wo, strips;
 };
 
+#ifdef BX_PROF
+// tools/prof_b0x.hip: per-workgroup shader-cycle sums of the backward's phases (A, B, C, D, unit prologue)
+__device__ unsigned long long bx_prof[BXB_BLOCKS][5];
+#define BX_STAMP(k)                     \
+  do {                                  \
+    const long long t_ = clock64();     \
+    prof_acc[k] += t_ - prof_t;         \
+    prof_t = t_;                        \
+  } while (0)
+#else
+#define BX_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
+#ifdef BX_PROF
+  long long prof_acc[5] = {0, 0, 0, 0, 0};
+  long long prof_t = clock64();
+#endif
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* wsf = lds;                                           // flipped conv2 weights: rows tap * 32 + ci
-  char* dsr = wsf + 192 * 64;                                // ds ring (2): row i <-> position q0 - 2 + i
-  char* o1r = dsr + 2 * BX_IMG;                              // out1 ring (2): row i <-> q0 - 3 + i
+  char* dsr = wsf + 192 * 64;                                // ds ring (3): row i <-> position q0 - 2 + i
+  char* o1r = dsr + 3 * BX_IMG;                              // out1 ring (2): row i <-> q0 - 3 + i
   char* dcr = o1r + 2 * BX_IMG;                              // dO, then dc, ring (2): row i <-> q0 - 1 + i
   float* xr = reinterpret_cast<float*>(dcr + 2 * BXB_DCR * 64);   // x ring (4): index i <-> q0 - 4 + i
   // per-channel record (four 16-byte reads): w1[0..5], wd[0..2], conv1 bias, mean, invstd * gamma, beta, invstd;
@@ -358,6 +369,11 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     prec[64 + tid] = make_float4(wd[2], a.bn[tid], a.bn[BX_C + tid], a.bn[2 * BX_C + tid]);
     prec[96 + tid] = make_float4(a.bn[3 * BX_C + tid], a.bn[4 * BX_C + tid], 0.f, 0.f);
   }
+  // out1 image rows 130, 131 (positions q0 + 127, q0 + 128) meet only the zeroed ds elements of the d w2 MFMA
+  // (below): zeros, never stale LDS; phase C writes rows 2 .. 129
+  if (tid < 16)
+    *reinterpret_cast<uint4*>(o1r + (tid >> 3) * BX_IMG + bx_img(130 + ((tid >> 2) & 1), tid & 3)) =
+        make_uint4(0u, 0u, 0u, 0u);
   // persistent per-thread sums. Phase C (dc) owns channels 8 c8 .. 8 c8 + 7 (c8 = tid & 3): BN sums;
   // phase D (dx) owns channels 4 g .. 4 g + 3 (g = tid & 7): d w1, d wd, d bias; the d w2 MFMA tiles
   const int c8 = tid & 3, g = tid & 7;
@@ -381,15 +397,23 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
   const int pw = wv * 32 + r;    // dout1 position q0 - 1 + pw of this lane in phase B
   __syncthreads();
   constexpr int DSN = (BX_IR * 4 + BX_T - 1) / BX_T;   // ds items per thread (3)
+  auto ds_slot = [&](int h) -> char* { return dsr + ((h + 3) % 3) * BX_IMG; };   // h >= -3
 
   for (int64_t u = blockIdx.x; u < (int64_t)a.strips * a.N; u += gridDim.x) {
     const int strip = (int)(u % a.strips), n = (int)(u / a.strips);
     const int q0 = strip * BX_P;
     const __hip_bfloat16* xn = a.x + (int64_t)n * H * W;
-    auto load_x = [&](int row) -> float {
+    // x row `row` at position q0 - 4 + tid: raw bf16 bits from a clamped (always valid) address, so the load
+    // carries no branch and its wait falls where the row is stored (x_val), a phase or more later
+    auto x_raw = [&](int row) -> uint32_t {
       const int q = q0 - 4 + tid;
-      return (tid < BXB_XW && row >= 0 && row < H && q >= 0 && q < W) ? __bfloat162float(xn[(int64_t)row * W + q])
-                                                                        : 0.f;
+      const int rc = row < 0 ? 0 : (row >= H ? H - 1 : row);
+      const int qc = q < 0 ? 0 : (q >= W ? W - 1 : q);
+      return reinterpret_cast<const uint16_t*>(xn)[(int64_t)rc * W + qc];
+    };
+    auto x_val = [&](int row, uint32_t raw) -> float {   // zero outside the image
+      const int q = q0 - 4 + tid;
+      return (row >= 0 && row < H && q >= 0 && q < W) ? __uint_as_float(raw << 16) : 0.f;
     };
     auto xslot = [&](int row) -> float* { return xr + (row & 3) * BXB_XW; };
     // conv1 pre-activation c (bf16-rounded, the unfused kernel's FMA order) at x columns v0 / v1, from a record
@@ -402,54 +426,6 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
       acc = fmaf(v1[2], r1.y, acc);
       return bx_bf16(acc);
     };
-    auto make_out1 = [&](int ro) {   // out1 row ro at positions q0 - 3 + i, i < 132 (zero outside [0, W))
-      const float* xa = xslot(ro - 1);
-      const float* xb = xslot(ro);
-      char* sl = o1r + (ro & 1) * BX_IMG;
-      for (int it = tid; it < 132 * 4; it += BX_T) {
-        const int i = it >> 2;
-        const int q = q0 - 3 + i;
-        const float v0[3] = {xa[i], xa[i + 1], xa[i + 2]}, v1[3] = {xb[i], xb[i + 1], xb[i + 2]};
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-          float yv[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int co = 8 * c8 + k + e;
-            const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co], r3 = prec[96 + co];
-            const float cv = conv1c(v0, v1, r0, r1);
-            yv[e] = bx_selu(fmaf((cv + r2.y) - r2.z, r2.w, r3.x));
-          }
-          o[k >> 1] = (q >= 0 && q < W) ? bx_pack2(yv[0], yv[1]) : 0u;
-        }
-        *reinterpret_cast<uint4*>(sl + bx_img(i, c8)) = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-    };
-    // out1 rows from the forward's saved tensor (a.o1): fetched a row ahead, 16-byte chunks of positions
-    // q0 - 3 + i, i < 132 (zero outside [0, W))
-    constexpr int ON = (132 * 4 + BX_T - 1) / BX_T;
-    uint4 po[ON];
-    auto fetch_o1 = [&](int ro) {
-#pragma unroll
-      for (int j = 0; j < ON; ++j) {
-        const int it = tid + BX_T * j;
-        const int i = it >> 2;
-        const int q = q0 - 3 + i;
-        po[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (it < 132 * 4 && ro <= H && q >= 0 && q < W)
-          po[j] = *reinterpret_cast<const uint4*>(a.o1 + (((int64_t)n * (H + 1) + ro) * W + q) * BX_C + 8 * c8);
-      }
-    };
-    auto store_o1 = [&](int ro) {
-      char* sl = o1r + (ro & 1) * BX_IMG;
-#pragma unroll
-      for (int j = 0; j < ON; ++j) {
-        const int it = tid + BX_T * j;
-        if (it < 132 * 4) *reinterpret_cast<uint4*>(sl + bx_img(it >> 2, c8)) = po[j];
-      }
-    };
-    const bool saved = a.o1 != nullptr;
     // ds row hrow: the pooled gradient where the window argmax hits, fetched a row ahead into registers
     uint4 pd[DSN];
     uint2 pa[DSN];
@@ -470,7 +446,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
       }
     };
     auto store_ds = [&](int hrow) {
-      char* sl = dsr + (hrow & 1) * BX_IMG;
+      char* sl = ds_slot(hrow);
 #pragma unroll
       for (int j = 0; j < DSN; ++j) {
         const int it = tid + BX_T * j;
@@ -492,41 +468,33 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     };
     __syncthreads();   // the previous unit's readers are done
     {
-      float v[3];
+      uint32_t v[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) v[i] = load_x(i - 1);
+      for (int i = 0; i < 3; ++i) v[i] = x_raw(i - 1);
 #pragma unroll
       for (int i = 0; i < 3; ++i)
-        if (tid < BXB_XW) xslot(i - 1)[tid] = v[i];
+        if (tid < BXB_XW) xslot(i - 1)[tid] = x_val(i - 1, v[i]);
     }
     fetch_ds(-1);
     store_ds(-1);       // zeros
     fetch_ds(0);
-    if (saved) {
-      fetch_o1(0);
-      store_o1(0);
-      fetch_o1(1);
-    }
-    __syncthreads();
-    if (!saved) make_out1(0);
-    for (int hp = 0; hp <= H; ++hp) {
-      // ---- phase A: ds row hp (registers -> LDS), next row's fetch, out1 row hp + 1
-      const float xnext = load_x(hp + 2);
+    BX_STAMP(4);
+    // iteration hp: dout1 / dc row hp (hp <= H), out1 row hp (phase C, used by the d w2 MFMAs of ds row hp - 1 and
+    // hp - 2 in the next two iterations), dx row hp - 1, d w2 of ds row hp - 2 (hp >= 2: out1 rows hp - 2, hp - 1)
+    for (int hp = 0; hp <= H + 1; ++hp) {
+      const bool rowc = hp <= H;
+      // ---- phase A: ds row hp (registers -> LDS), the next row's fetch, x row hp + 2 in flight
+      const uint32_t xnext = x_raw(hp + 2);
       store_ds(hp);
       fetch_ds(hp + 1);
-      if (saved) {
-        if (hp + 1 <= H) store_o1(hp + 1);
-        fetch_o1(hp + 2);
-      } else if (hp + 1 <= H) {
-        make_out1(hp + 1);
-      }
       __syncthreads();
+      BX_STAMP(0);
       // ---- phase B: dout1 row hp = conv(ds rows hp - 1, hp) with the flipped weights -> bf16 into the dc slot;
-      // d w2 += ds row hp x out1 rows hp, hp + 1 over K = ds image rows 2 .. 129 (positions q0 .. q0 + 127); rows
-      // 128 and 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed (in the last K
-      // step, element j of lane l holds row 2 + 112 + 8 (j >> 2) + 4 (l >> 5) + (j & 3): elements 6, 7 of lanes
+      // d w2 += ds row hp - 2 x out1 rows hp - 2, hp - 1 over K = ds image rows 2 .. 129 (positions q0 .. q0 + 127);
+      // rows 128 and 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed (in the last
+      // K step, element j of lane l holds row 2 + 112 + 8 (j >> 2) + 4 (l >> 5) + (j & 3): elements 6, 7 of lanes
       // 32-63)
-      {
+      if (rowc) {
         bxf32x16 acc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -534,7 +502,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         const int wo0 = bx_img(r, hh), wo1 = bx_img(r, 2 + hh);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
-          const char* dk = dsr + ((hp - 1 + kh) & 1) * BX_IMG;
+          const char* dk = ds_slot(hp - 1 + kh);
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
@@ -550,15 +518,15 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           *reinterpret_cast<uint2*>(dcs + bx_img(pw, gg) + 8 * hh) =
               make_uint2(bx_pack2(acc[4 * gg], acc[4 * gg + 1]), bx_pack2(acc[4 * gg + 2], acc[4 * gg + 3]));
       }
-      if (hp < H) {
-        const char* dsi = dsr + (hp & 1) * BX_IMG;
+      if (hp >= 2) {
+        const char* dsi = ds_slot(hp - 2);
         const bool tail_lane = (lane >> 5) == 1;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int tap = wv + 4 * t;
           if (tap < 6) {
             const int kh = tap / 3, kw = tap - 3 * kh;
-            const char* oi = o1r + ((hp + kh) & 1) * BX_IMG;
+            const char* oi = o1r + ((hp + kh) & 1) * BX_IMG;   // out1 row hp - 2 + kh
             const int2 offa = bx_tr_off(2, lane), offb = bx_tr_off(2 + kw, lane);
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
@@ -573,116 +541,134 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         }
       }
       __syncthreads();
-      // ---- phase C: dc row hp = bf16(dO selu'(u) s) in place (rdx_sconv_dgrad_bnselu's arithmetic on c
-      // recomputed from x), BN sums over the strip's own positions
-      {
-        char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
-        const float* xa = xslot(hp - 1);
-        const float* xb = xslot(hp);
-        for (int it = tid; it < BXB_DCR * 4; it += BX_T) {
-          const int i = it >> 2;
-          const int q = q0 - 1 + i;
-          const bool inside = q >= 0 && q < W;
-          const bool own = inside && i >= 1 && i <= BX_P;
-          uint4* slot = reinterpret_cast<uint4*>(dcs + bx_img(i, c8));
-          const uint4 dov = *slot;
-          const uint32_t dw[4] = {dov.x, dov.y, dov.z, dov.w};
-          const float v0[3] = {xa[i + 2], xa[i + 3], xa[i + 4]}, v1[3] = {xb[i + 2], xb[i + 3], xb[i + 4]};
-          uint32_t ow[4];
+      BX_STAMP(1);
+      if (rowc) {
+        // ---- phase C: dc row hp = bf16(dO selu'(u) s) in place (rdx_sconv_dgrad_bnselu's arithmetic on c
+        // recomputed from x), BN sums over the strip's own positions; out1 row hp = selu(u) (rdx_sincnet_b0_fwd's
+        // value, one exp for both) into the out1 slot of row hp - 2 (read for the last time in phase B above)
+        {
+          char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
+          char* o1s = o1r + (hp & 1) * BX_IMG;
+          const float* xa = xslot(hp - 1);
+          const float* xb = xslot(hp);
 #pragma unroll
-          for (int k = 0; k < 8; k += 2) {
-            float dz[2];
+          for (int jt = 0; jt < 2; ++jt) {
+            const int it = tid + BX_T * jt;
+            const int i = it >> 2;
+            const int q = q0 - 1 + i;
+            const bool inside = q >= 0 && q < W;
+            const bool own = inside && i >= 1 && i <= BX_P;
+            uint4* slot = reinterpret_cast<uint4*>(dcs + bx_img(i, c8));
+            const uint4 dov = *slot;
+            const uint32_t dw[4] = {dov.x, dov.y, dov.z, dov.w};
+            const float v0[3] = {xa[i + 2], xa[i + 3], xa[i + 4]}, v1[3] = {xb[i + 2], xb[i + 3], xb[i + 4]};
+            uint32_t ow[4], oo[4];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int co = 8 * c8 + k + e;
-              const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co], r3 = prec[96 + co];
-              const float cv = conv1c(v0, v1, r0, r1);
-              const float zc = (cv + r2.y) - r2.z;
-              const float xhat = zc * r3.y;
-              const float uu = fmaf(zc, r2.w, r3.x);
-              const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * __expf(uu);
-              const float dov_e = e == 0 ? bx_lo(dw[k >> 1]) : bx_hi(dw[k >> 1]);
-              const float du = dov_e * sd;
-              dz[e] = inside ? du * r2.w : 0.f;
-              if (own) {
-                bsum[0][k + e] += dz[e];
-                bsum[1][k + e] = fmaf(du, xhat, bsum[1][k + e]);
-                bsum[2][k + e] += du;
+            for (int k = 0; k < 8; k += 2) {
+              float dz[2], yo[2];
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const int co = 8 * c8 + k + e;
+                const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co], r3 = prec[96 + co];
+                const float cv = conv1c(v0, v1, r0, r1);
+                const float zc = (cv + r2.y) - r2.z;
+                const float xhat = zc * r3.y;
+                const float uu = fmaf(zc, r2.w, r3.x);
+                const float ex = __expf(uu);
+                const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * ex;
+                yo[e] = BX_SELU_SCALE * (uu > 0.f ? uu : BX_SELU_ALPHA * (ex - 1.0f));   // bx_selu(uu)
+                const float dov_e = e == 0 ? bx_lo(dw[k >> 1]) : bx_hi(dw[k >> 1]);
+                const float du = dov_e * sd;
+                dz[e] = inside ? du * r2.w : 0.f;
+                if (own) {
+                  bsum[0][k + e] += dz[e];
+                  bsum[1][k + e] = fmaf(du, xhat, bsum[1][k + e]);
+                  bsum[2][k + e] += du;
+                }
               }
+              ow[k >> 1] = bx_pack2(dz[0], dz[1]);
+              oo[k >> 1] = inside ? bx_pack2(yo[0], yo[1]) : 0u;
             }
-            ow[k >> 1] = bx_pack2(dz[0], dz[1]);
+            *slot = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+            *reinterpret_cast<uint4*>(o1s + bx_img(i + 2, c8)) = make_uint4(oo[0], oo[1], oo[2], oo[3]);
           }
-          *slot = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
-      }
-      __syncthreads();
-      // ---- phase D: dx row hp - 1, d w1 (dc row hp), d wd / d bias (ds row hp) over the strip's own positions
-      {
-        const char* dcA = dcr + (hp & 1) * (BXB_DCR * 64);         // dc row hp
-        const char* dcB = dcr + ((hp - 1) & 1) * (BXB_DCR * 64);   // dc row hp - 1
-        const char* dsP = dsr + ((hp - 1) & 1) * BX_IMG;           // ds row hp - 1
-        const char* dsC = dsr + (hp & 1) * BX_IMG;                 // ds row hp
-        const float* xa = xslot(hp - 1);
-        const float* xb = xslot(hp);
-        const int gc = g >> 1, sub = 8 * (g & 1);
-        for (int it = tid; it < BX_P * 8; it += BX_T) {
-          const int k = it >> 3;
-          const int q = q0 + k;
-          const bool valid = q < W;
-          float pdx = 0.f;
-          if (hp >= 1 && valid) {
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-              const uint2 A = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 2 - kw, gc) + sub);
-              const uint2 Bv = *reinterpret_cast<const uint2*>(dcB + bx_img(k + 2 - kw, gc) + sub);
-              const uint2 D = *reinterpret_cast<const uint2*>(dsP + bx_img(k + 3 - kw, gc) + sub);
-              const float av[4] = {bx_lo(A.x), bx_hi(A.x), bx_lo(A.y), bx_hi(A.y)};
-              const float bv[4] = {bx_lo(Bv.x), bx_hi(Bv.x), bx_lo(Bv.y), bx_hi(Bv.y)};
-              const float dv[4] = {bx_lo(D.x), bx_hi(D.x), bx_lo(D.y), bx_hi(D.y)};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int co = 4 * g + e;
-                const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co];
-                const float w1a[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, wda[3] = {r1.z, r1.w, r2.x};
-                pdx = fmaf(av[e], w1a[kw], pdx);
-                pdx = fmaf(bv[e], w1a[3 + kw], pdx);
-                pdx = fmaf(dv[e], wda[kw], pdx);
-              }
-            }
-          }
-          pdx += __shfl_xor(pdx, 1, 64);
-          pdx += __shfl_xor(pdx, 2, 64);
-          pdx += __shfl_xor(pdx, 4, 64);
-          if (hp >= 1 && valid && g == 0) a.dx[((int64_t)n * H + hp - 1) * W + q] = pdx;
-          if (valid) {
-            const uint2 C = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 1, gc) + sub);
-            const float cv[4] = {bx_lo(C.x), bx_hi(C.x), bx_lo(C.y), bx_hi(C.y)};
-            const float xv0[3] = {xa[k + 3], xa[k + 4], xa[k + 5]}, xv1[3] = {xb[k + 3], xb[k + 4], xb[k + 5]};
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
+        __syncthreads();
+        BX_STAMP(2);
+        // ---- phase D: dx row hp - 1, d w1 (dc row hp), d wd / d bias (ds row hp) over the strip's own positions
+        {
+          const char* dcA = dcr + (hp & 1) * (BXB_DCR * 64);         // dc row hp
+          const char* dcB = dcr + ((hp - 1) & 1) * (BXB_DCR * 64);   // dc row hp - 1
+          const char* dsP = ds_slot(hp - 1);                         // ds row hp - 1
+          const char* dsC = ds_slot(hp);                             // ds row hp
+          const float* xa = xslot(hp - 1);
+          const float* xb = xslot(hp);
+          const int gc = g >> 1, sub = 8 * (g & 1);
+          for (int it = tid; it < BX_P * 8; it += BX_T) {
+            const int k = it >> 3;
+            const int q = q0 + k;
+            const bool valid = q < W;
+            float pdx = 0.f;
+            if (hp >= 1 && valid) {
 #pragma unroll
               for (int kw = 0; kw < 3; ++kw) {
-                aw1[e][kw] = fmaf(cv[e], xv0[kw], aw1[e][kw]);
-                aw1[e][3 + kw] = fmaf(cv[e], xv1[kw], aw1[e][3 + kw]);
+                const uint2 A = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 2 - kw, gc) + sub);
+                const uint2 Bv = *reinterpret_cast<const uint2*>(dcB + bx_img(k + 2 - kw, gc) + sub);
+                const uint2 D = *reinterpret_cast<const uint2*>(dsP + bx_img(k + 3 - kw, gc) + sub);
+                const float av[4] = {bx_lo(A.x), bx_hi(A.x), bx_lo(A.y), bx_hi(A.y)};
+                const float bv[4] = {bx_lo(Bv.x), bx_hi(Bv.x), bx_lo(Bv.y), bx_hi(Bv.y)};
+                const float dv[4] = {bx_lo(D.x), bx_hi(D.x), bx_lo(D.y), bx_hi(D.y)};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const int co = 4 * g + e;
+                  const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co];
+                  const float w1a[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, wda[3] = {r1.z, r1.w, r2.x};
+                  pdx = fmaf(av[e], w1a[kw], pdx);
+                  pdx = fmaf(bv[e], w1a[3 + kw], pdx);
+                  pdx = fmaf(dv[e], wda[kw], pdx);
+                }
               }
-            if (hp < H) {
-              const uint2 S = *reinterpret_cast<const uint2*>(dsC + bx_img(k + 2, gc) + sub);
-              const float sv[4] = {bx_lo(S.x), bx_hi(S.x), bx_lo(S.y), bx_hi(S.y)};
+            }
+            pdx += __shfl_xor(pdx, 1, 64);
+            pdx += __shfl_xor(pdx, 2, 64);
+            pdx += __shfl_xor(pdx, 4, 64);
+            if (hp >= 1 && valid && g == 0) a.dx[((int64_t)n * H + hp - 1) * W + q] = pdx;
+            if (valid) {
+              const uint2 C = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 1, gc) + sub);
+              const float cv[4] = {bx_lo(C.x), bx_hi(C.x), bx_lo(C.y), bx_hi(C.y)};
+              const float xv0[3] = {xa[k + 3], xa[k + 4], xa[k + 5]}, xv1[3] = {xb[k + 3], xb[k + 4], xb[k + 5]};
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                abias[e] += sv[e];
+              for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int kw = 0; kw < 3; ++kw) awd[e][kw] = fmaf(sv[e], xv1[kw], awd[e][kw]);
+                for (int kw = 0; kw < 3; ++kw) {
+                  aw1[e][kw] = fmaf(cv[e], xv0[kw], aw1[e][kw]);
+                  aw1[e][3 + kw] = fmaf(cv[e], xv1[kw], aw1[e][3 + kw]);
+                }
+              if (hp < H) {
+                const uint2 S = *reinterpret_cast<const uint2*>(dsC + bx_img(k + 2, gc) + sub);
+                const float sv[4] = {bx_lo(S.x), bx_hi(S.x), bx_lo(S.y), bx_hi(S.y)};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  abias[e] += sv[e];
+#pragma unroll
+                  for (int kw = 0; kw < 3; ++kw) awd[e][kw] = fmaf(sv[e], xv1[kw], awd[e][kw]);
+                }
               }
             }
           }
         }
       }
-      if (tid < BXB_XW) xslot(hp + 2)[tid] = xnext;   // the slot of x row hp - 2 (no reader in this row)
+      // x row hp + 2 into the slot of row hp - 2 (no reader in this row)
+      if (tid < BXB_XW) xslot(hp + 2)[tid] = x_val(hp + 2, xnext);
       __syncthreads();
+      BX_STAMP(3);
     }
   }
-
+#ifdef BX_PROF
+  if (tid == 0)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) bx_prof[blockIdx.x][k] = (unsigned long long)prof_acc[k];
+#endif
   // ---- per-workgroup partial row (fixed-order sums: bitwise repeatable) ----
   float* out = a.part + (int64_t)blockIdx.x * BXB_NPART;
 #pragma unroll
@@ -734,8 +720,8 @@ extern "C" int rdx_b0x_bwd_nblk(int N, int W) {
 }
 
 extern "C" int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, const float* w1, const float* wd,
-                           const float* bn, const void* w2f, const void* o1, float* dx, float* part, int N, int H,
-                           int W, void* stream) {
+                           const float* bn, const void* w2f, float* dx, float* part, int N, int H, int W,
+                           void* stream) {
   RDX_REQUIRE(x && dp && arg && w1 && wd && bn && w2f && dx && part && N > 0 && H > 0 && W >= 3);
   RDX_REQUIRE(((uintptr_t)dp & 15) == 0 && ((uintptr_t)arg & 7) == 0 && ((uintptr_t)w2f & 15) == 0);
   static bool attr = false;
@@ -745,10 +731,10 @@ extern "C" int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, co
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  RDX_REQUIRE(((uintptr_t)o1 & 15) == 0);
   BxBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)dp, arg, w1, wd, bn, (const __hip_bfloat16*)w2f,
-              (const __hip_bfloat16*)o1, dx, part, N, H, W, W / 3, W / 3 / BX_J + 1};
-  hipLaunchKernelGGL(b0x_bwd_kernel, dim3((unsigned)rdx_b0x_bwd_nblk(N, W)), dim3(BX_T), BXB_LDS, as_stream(stream), a);
+              dx, part, N, H, W, W / 3, W / 3 / BX_J + 1};
+  hipLaunchKernelGGL(b0x_bwd_kernel, dim3((unsigned)rdx_b0x_bwd_nblk(N, W)), dim3(BX_T), BXB_LDS, as_stream(stream),
+                     a);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

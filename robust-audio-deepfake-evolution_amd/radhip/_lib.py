@@ -94,9 +94,9 @@ SIGNATURES = {
     "rdx_sincnet_b0_fwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),
     "rdx_sincnet_b0_nblk": (c_int, [c_i64]),
     "rdx_sincnet_b0_bwd": (c_int, [c_vp] * 7 + [c_int, c_int, c_int, c_int, c_vp]),
-    "rdx_b0x_fwd": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_vp]),
+    "rdx_b0x_fwd": (c_int, [c_vp] * 8 + [c_int, c_int, c_int, c_vp]),
     "rdx_b0x_bwd_nblk": (c_int, [c_int, c_int]),
-    "rdx_b0x_bwd": (c_int, [c_vp] * 10 + [c_int, c_int, c_int, c_vp]),
+    "rdx_b0x_bwd": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_vp]),
     "rdx_posconv_fwd": (c_int, [c_vp] * 5 + [c_int, c_int, c_vp]),
     "rdx_posconv_bwd": (c_int, [c_vp] * 4 + [c_int, c_int, c_vp]),
     "rdx_gemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
@@ -128,6 +128,10 @@ SIGNATURES = {
     "rdx_attn_bwd_fused": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_i64,
                                    c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                                    c_vp]),
+    "rdx_attn_bwd_split_ws": (c_i64, [c_int, c_int]),
+    "rdx_attn_bwd_fused_split": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp,
+                                         c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                         c_vp, c_i64, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_attn_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_int, c_vp]),
     "rdx_dropout_mask": (c_int, [c_vp, c_int, c_f32, c_vp, c_i64, c_vp]),
     "rdx_wl_ln1_fwd": (c_int, [c_vp] * 3 + [c_f32] + [c_vp] * 5 + [c_int, c_vp,

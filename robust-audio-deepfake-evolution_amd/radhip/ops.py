@@ -923,15 +923,10 @@ class Block0Fused(torch.autograd.Function):
         bias = (b2.detach().float() + bd.detach().float()).contiguous()
         y = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
         arg = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.uint8, memory_format=torch.channels_last)
-        # out1 for the one-pass backward (it reads it instead of recomputing conv1 + BN + SELU: VALU-bound there)
-        save_o1 = torch.is_grad_enabled() and os.environ.get("RADHIP_B0X_BWD", "1") != "0" and \
-            os.environ.get("RADHIP_B0X_SAVE", "1") != "0"
-        o1 = torch.empty(N, H + 1, W, C, device=x.device, dtype=torch.bfloat16) if save_o1 else None
-        # MFMA work: conv2 (32 -> 32, 2 x 3) over N x H x W positions; HBM: x in, y + argmax (+ out1) out
+        # MFMA work: conv2 (32 -> 32, 2 x 3) over N x H x W positions; HBM: x in, y + argmax out
         with _timed("b0x_fwd", x, 2.0 * N * H * W * 32 * 192):
-            check(lib().rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg),
-                                    _p(o1) if o1 is not None else None, N, H, W, _stream(x)), "b0x_fwd")
-        ctx.o1 = o1
+            check(lib().rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg), N, H, W,
+                                    _stream(x)), "b0x_fwd")
         ctx.save_for_backward(xb, w1b, wdb, wd2, bn5, arg, *f32)
         ctx.meta = (tuple(w1.shape), tuple(wd.shape), x.dtype, tuple(w2.shape), w2.dtype)
         return y
@@ -947,12 +942,9 @@ class Block0Fused(torch.autograd.Function):
             dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
             part = torch.empty(lib().rdx_b0x_bwd_nblk(N, W), 6560, device=xb.device, dtype=torch.float32)
             # MFMA work: conv2's input gradient and weight gradient (2 x the forward's conv2)
-            o1 = ctx.o1
             with _timed("b0x_bwd", dy, 4.0 * N * H * W * 32 * 192):
-                check(lib().rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2),
-                                        _p(o1) if o1 is not None else None, _p(dx), _p(part), N, H, W, _stream(dy)),
-                      "b0x_bwd")
-            ctx.o1 = None
+                check(lib().rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2), _p(dx), _p(part),
+                                        N, H, W, _stream(dy)), "b0x_bwd")
             tot = part.sum(0)
             dw2 = tot[:6144].view(2, 3, C, C).permute(2, 3, 0, 1)
             dw1 = tot[6144:6336].reshape(w1_shape)
@@ -1065,6 +1057,23 @@ def attn_keep_mask(B, T, H, p_drop, device):
     return torch.empty(lib().rdx_attn_keep_mask_words(B, T, H), device=device, dtype=torch.int32)
 
 
+_ATTN_WS = {}
+
+
+def _attn_split_workspace(dev, n_floats, n_counters):
+    """fp32 partial dQ / d gate and the per-(b, h) tickets of the split attention backward, one per device (every
+    attention backward of the product runs on the encoder's compute stream, one after another); the tickets are
+    zeroed here once and left at zero by each launch. Grown outside graph capture only."""
+    cur = _ATTN_WS.get(dev.index)
+    if cur is None or cur[0].numel() < n_floats or cur[1].numel() < n_counters:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("radhip attention: split-backward workspace must be allocated before graph capture")
+        cur = (torch.empty(max(n_floats, cur[0].numel() if cur else 0), dtype=torch.float32, device=dev),
+               torch.zeros(max(n_counters, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
+        _ATTN_WS[dev.index] = cur
+    return cur
+
+
 def attn_bwd_launch(q, ldq, k, ldk, v, ldv, gate, rel, mask, seed, salt, p_drop, o, ldo, lse, do, lddo, D, dq, dk, dv,
                     ldg, dgate, B, T, H, stream):
     """One gated-attention backward: the fused one-workgroup-per-(b, h) kernel when T <= 224 (dropout from
@@ -1073,6 +1082,16 @@ def attn_bwd_launch(q, ldq, k, ldk, v, ldv, gate, rel, mask, seed, salt, p_drop,
     if fused_bwd_enabled(T):
         if p_drop > 0 and mask is None:
             raise RuntimeError("fused attention backward with dropout needs the forward's keep mask")
+        if B * H < 256 and (B * H) % 8 == 0 and os.environ.get("RADHIP_ATTN_SPLIT", "0") == "1":
+            # opt-in: two workgroups per (b, h) over the key tiles, the second to finish combines dQ / d gate
+            # (fills the chip at B = 8, but measured 4.6 vs 4.2 ms of attention backward per step in the
+            # bench: the combine's extra dQ traffic and the halved per-workgroup key reuse cost more)
+            ws, cnt = _attn_split_workspace(gate.device, int(lib().rdx_attn_bwd_split_ws(B, H)), B * H)
+            return check(lib().rdx_attn_bwd_fused_split(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
+                                                        _p(mask) if mask is not None else None, p_drop, 0.125, o,
+                                                        ldo, _p(lse), do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate),
+                                                        _p(ws), ws.numel(), _p(cnt), cnt.numel(), B, T, H, 64,
+                                                        stream), "attn_bwd_fused_split")
         return check(lib().rdx_attn_bwd_fused(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
                                               _p(mask) if mask is not None else None, p_drop, 0.125, o, ldo, _p(lse),
                                               do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate), B, T, H, 64, stream),

@@ -328,16 +328,18 @@ def _toeplitz_bias(H, T, seed=0):
     return tab[:, i[None, :] - i[:, None] + T - 1]
 
 
-@pytest.mark.parametrize("bwd", ["fused", "split"])
+@pytest.mark.parametrize("bwd", ["fused", "fused_keysplit", "split"])
 @pytest.mark.parametrize("p_drop,H", [(0.0, 4), (0.1, 4), (0.1, 16)])
 def test_gated_attention_matches_torch(p_drop, H, bwd, monkeypatch):
     """Fused MFMA WavLM attention (gated rel-pos bias formed in registers, hashed dropout) vs an fp32
     torch reference fed the same bf16 inputs and the kernel's own dropout mask; forward and the q/k/v/
-    gate gradients, through both backward paths (the one-launch fused kernel and the dQ + dK/dV pair).
+    gate gradients, through every backward path (the one-launch fused kernel, its two-workgroups-per-(b, h)
+    key-split form with the last-arriver dQ / d gate combine, and the dQ + dK/dV pair).
     k is a strided column view of a fused q|k|v tensor (as in the model). H = 16 takes the fused
     kernel's head-per-XCD block mapping."""
     from radhip.ops import GatedAttention, attention_dropout_mask
-    monkeypatch.setenv("RADHIP_ATTN_BWD", bwd)
+    monkeypatch.setenv("RADHIP_ATTN_BWD", "split" if bwd == "split" else "fused")
+    monkeypatch.setenv("RADHIP_ATTN_SPLIT", "1" if bwd == "fused_keysplit" else "0")
     torch.manual_seed(0)
     B, T, D = 2, 201, 64
     E = H * D
@@ -384,7 +386,8 @@ def test_gated_attention_matches_torch(p_drop, H, bwd, monkeypatch):
 def test_gated_attention_ragged_lengths(B, T, H):
     """Sequence lengths with a one-row last tile, an exact tile multiple, the fused backward's 224-row
     maximum, the first length past it (dQ + dK/dV pair), the 256-row maximum and two frames: forward
-    and gradients against the fp32 torch reference (no dropout)."""
+    and gradients against the fp32 torch reference (no dropout). B * H = 16 and 48 take the key-split fused
+    backward (the T = 2 case gives its second workgroup no key tile)."""
     from radhip.ops import GatedAttention
     torch.manual_seed(T)
     E = H * 64
