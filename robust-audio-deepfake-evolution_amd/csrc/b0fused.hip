@@ -257,18 +257,31 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
 // dc and ds carry the unfused path's bf16 roundings and dout1 its MFMA order, so dc and every gradient equal
 // the unfused ones up to the order of their fp32 sums.
 //
-// A workgroup walks units (utterance, strip of 126 positions) in a grid-stride loop and, per unit, the H + 1
-// rows h' of dout1 top-down in four phases: (A) ds row h' into an LDS ring of 2 (its pooled gradient and argmax
-// fetched a row ahead), out1 row h' + 1 (ring of 2); (B) dout1 row h' on the MFMA into the dc ring (2 rows) and
-// the d w2 MFMAs of ds row h'; (C) the BN + SELU backward of dout1 in place, with a thread owning 8 channels
-// (c recomputed from x); (D) dx row h' - 1, d w1, d wd and the bias sums, a thread owning 4 channels. Every sum counts the strip's own positions
-// [126 s, 126 s + 126) (the d w2 MFMA runs K over 128 positions and zeroes the last two); with Wo / 42 + 1
-// strips they partition every position that carries a gradient. Per-workgroup sums go to one fp32 partial row (the caller sums the rows: no atomics).
+// A workgroup walks units (utterance, strip of 126 positions) in a grid-stride loop and, per unit, the rows
+// top-down; iteration hp has four phases:
+//   (A) ds row hp into an LDS ring of 3 (its pooled gradient and argmax fetched a row ahead); dx row hp - 2 from
+//       the three tap responses phase D left in LDS;
+//   (B) dout1 row hp on the MFMA (ds rows hp - 1, hp) into the dc ring (2 rows), and the d w2 MFMAs of ds row
+//       hp - 2 x out1 rows hp - 2, hp - 1 (6 taps x 8 K steps, 12 per wave);
+//   (C) the BN + SELU backward of dout1 row hp in place and out1 row hp = selu(u) (c recomputed from x, one exp
+//       for both), a thread owning 2 channels (their frozen-BN / conv1 parameters in registers) x 8 positions;
+//   (D) on the MFMA: dx's three tap responses O[kw][k] = sum_co (dc rows hp, hp - 1 | ds row hp - 1) x (w1 | wd)
+//       (M = kw, K = 3 images x 32 channels, N = positions), and d w1 / d wd / d bias as dc^T / ds^T x the x taps
+//       (K = positions, N = taps; x kept as three bf16 copies shifted by kw).
+// Every sum counts the strip's own positions [126 s, 126 s + 126) (the K = position MFMAs run over 128 positions
+// and zero the last two); with Wo / 42 + 1 strips they partition every position that carries a gradient.
+// Per-workgroup sums go to one fp32 partial row (the caller sums the rows: no atomics).
 constexpr int BXB_DCR = 128;                         // dc image rows: positions q0 - 1 .. q0 + 126
 constexpr int BXB_XW = 136;                          // staged x positions q0 - 4 .. q0 + 131
 constexpr int BXB_NPART = 6 * 32 * 32 + 32 * 6 + 32 * 3 + 32 + 3 * 32;
-constexpr int BXB_LDS = 192 * 64 + 3 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + 32 * 64;
+constexpr int BXB_XS = 4 * 3 * 128 * 2;              // x rows as bf16, shifted by kw: [4 slots][3 kw][128]
+constexpr int BXB_WDX = 37 * 16;                     // dx weights, the MFMA A operand: [6 K steps][2][3 kw] + zeros
+constexpr int BXB_OB = 3 * 128 * 4;                  // dx tap responses [3 kw][128] fp32
+constexpr int BXB_PR = 6 * 16 * 16;                  // conv1 / frozen-BN records of the 16 channel pairs
+constexpr int BXB_LDS = 192 * 64 + 3 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + BXB_XS + BXB_WDX +
+                        BXB_OB + BXB_PR;
 constexpr int BXB_BLOCKS = 512;
+static_assert(2 * BXB_LDS <= 160 * 1024, "two workgroups per CU");
 
 typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 bxbf16x4v;
 typedef __attribute__((address_space(3))) bxbf16x4v lds_bxbf16x4v;
@@ -352,79 +365,97 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
   char* o1r = dsr + 3 * BX_IMG;                              // out1 ring (2): row i <-> q0 - 3 + i
   char* dcr = o1r + 2 * BX_IMG;                              // dO, then dc, ring (2): row i <-> q0 - 1 + i
   float* xr = reinterpret_cast<float*>(dcr + 2 * BXB_DCR * 64);   // x ring (4): index i <-> q0 - 4 + i
-  // per-channel record (four 16-byte reads): w1[0..5], wd[0..2], conv1 bias, mean, invstd * gamma, beta, invstd;
-  // part j of channel co at float4 j * 32 + co (the channels one instruction reads spread over the bank slots)
-  float4* prec = reinterpret_cast<float4*>(xr + 4 * BXB_XW);   // [4][32]
+  char* xs = reinterpret_cast<char*>(xr + 4 * BXB_XW);       // bf16 x ring (4) x kw: [kw][i] <-> q0 + i + kw - 1
+  char* wdx = xs + BXB_XS;                                   // chunk (s * 2 + h) * 3 + kw; chunk 36 = zeros
+  float* ob = reinterpret_cast<float*>(wdx + BXB_WDX);       // O[kw][k + 2], k = -2 .. 125
+  // channel pair cp's record, part k at float4 k * 16 + cp: w1[2cp][0..3] | w1[2cp][4..5] w1[2cp+1][0..1] |
+  // w1[2cp+1][2..5] | cb mean invstd*gamma beta (2cp) | invstd (2cp), cb mean invstd*gamma (2cp+1) | beta invstd
+  float4* prr = reinterpret_cast<float4*>(ob + 3 * 128);
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int H = a.H, W = a.W, Wo = a.Wo, W3 = 3 * a.Wo;
   for (int i = tid; i < 192 * 4; i += BX_T) {
     const int row = i >> 2, ch = i & 3;
     *reinterpret_cast<uint4*>(wsf + bx_img(row, ch)) = *reinterpret_cast<const uint4*>(a.w2f + row * BX_C + ch * 8);
   }
-  if (tid < 32) {
-    const float* w1 = a.w1 + tid * 6;
-    const float* wd = a.wd + tid * 3;
-    prec[tid] = make_float4(w1[0], w1[1], w1[2], w1[3]);
-    prec[32 + tid] = make_float4(w1[4], w1[5], wd[0], wd[1]);
-    prec[64 + tid] = make_float4(wd[2], a.bn[tid], a.bn[BX_C + tid], a.bn[2 * BX_C + tid]);
-    prec[96 + tid] = make_float4(a.bn[3 * BX_C + tid], a.bn[4 * BX_C + tid], 0.f, 0.f);
+  // dx weights as the MFMA A operand: chunk (s * 2 + h) * 3 + kw holds w_img[co][kw] for co = 16 (s & 1) + 8 h + j,
+  // image s >> 1 (0: w1 taps kh = 0 on dc row hp; 1: w1 taps kh = 1 on dc row hp - 1; 2: wd on ds row hp - 1)
+  if (tid < 36) {
+    const int kw = tid % 3, h = (tid / 3) & 1, s = tid / 6, img = s >> 1;
+    uint32_t pk[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int c0 = 16 * (s & 1) + 8 * h + 2 * jj;
+      const float v0 = img < 2 ? a.w1[c0 * 6 + 3 * img + kw] : a.wd[c0 * 3 + kw];
+      const float v1 = img < 2 ? a.w1[(c0 + 1) * 6 + 3 * img + kw] : a.wd[(c0 + 1) * 3 + kw];
+      pk[jj] = bx_pack2(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(wdx + tid * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  } else if (tid == 36) {
+    *reinterpret_cast<uint4*>(wdx + 36 * 16) = make_uint4(0u, 0u, 0u, 0u);
   }
-  // out1 image rows 130, 131 (positions q0 + 127, q0 + 128) meet only the zeroed ds elements of the d w2 MFMA
-  // (below): zeros, never stale LDS; phase C writes rows 2 .. 129
-  if (tid < 16)
-    *reinterpret_cast<uint4*>(o1r + (tid >> 3) * BX_IMG + bx_img(130 + ((tid >> 2) & 1), tid & 3)) =
+  // out1 image rows 130, 131 (positions q0 + 127, q0 + 128) meet only the zeroed ds elements of the d w2 MFMA:
+  // zeros, never stale LDS; phase C writes rows 2 .. 129
+  if (tid >= 64 && tid < 80) {
+    const int t = tid - 64;
+    *reinterpret_cast<uint4*>(o1r + (t >> 3) * BX_IMG + bx_img(130 + ((t >> 2) & 1), t & 3)) =
         make_uint4(0u, 0u, 0u, 0u);
-  // persistent per-thread sums. Phase C (dc) owns channels 8 c8 .. 8 c8 + 7 (c8 = tid & 3): BN sums;
-  // phase D (dx) owns channels 4 g .. 4 g + 3 (g = tid & 7): d w1, d wd, d bias; the d w2 MFMA tiles
-  const int c8 = tid & 3, g = tid & 7;
-  float bsum[3][8];
-  float aw1[4][6], awd[4][3], abias[4];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) bsum[0][k] = bsum[1][k] = bsum[2][k] = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 6; ++j) aw1[i][j] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) awd[i][j] = 0.f;
-    abias[i] = 0.f;
   }
-  bxf32x16 acc2[2];
+  // phase C: this thread's channels 2 cp, 2 cp + 1 (records read once per row), positions 8 pg .. 8 pg + 7
+  const int cp = tid & 15, pg = tid >> 4;
+  if (tid < 16) {
+    const float* w0 = a.w1 + 12 * tid;   // channel 2 tid, then 2 tid + 1
+    const int c0 = 2 * tid, c1 = c0 + 1;
+    prr[tid] = make_float4(w0[0], w0[1], w0[2], w0[3]);
+    prr[16 + tid] = make_float4(w0[4], w0[5], w0[6], w0[7]);
+    prr[32 + tid] = make_float4(w0[8], w0[9], w0[10], w0[11]);
+    prr[48 + tid] = make_float4(a.bn[c0], a.bn[BX_C + c0], a.bn[2 * BX_C + c0], a.bn[3 * BX_C + c0]);
+    prr[64 + tid] = make_float4(a.bn[4 * BX_C + c0], a.bn[c1], a.bn[BX_C + c1], a.bn[2 * BX_C + c1]);
+    prr[80 + tid] = make_float4(a.bn[3 * BX_C + c1], a.bn[4 * BX_C + c1], 0.f, 0.f);
+  }
+  float bsum[3][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int q = 0; q < 3; ++q) bsum[q][0] = bsum[q][1] = 0.f;
+  // d w2: acc2[0] = tap wv over every K step; acc2[1] = tap 4 + (wv >> 1) over K steps 4 (wv & 1) .. + 3.
+  // accw = D[co][n] over K steps 2 wv, 2 wv + 1: n < 6 d w1 (tap n, from dc), n = 8 + kw d wd and n = 11 d bias
+  // (from ds): the two B operands have disjoint nonzero columns, so both products accumulate into one tile
+  bxf32x16 acc2[2], accw;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc2[t][i] = 0.f;
+  for (int i = 0; i < 16; ++i) acc2[0][i] = acc2[1][i] = accw[i] = 0.f;
   const int pw = wv * 32 + r;    // dout1 position q0 - 1 + pw of this lane in phase B
   __syncthreads();
   constexpr int DSN = (BX_IR * 4 + BX_T - 1) / BX_T;   // ds items per thread (3)
   auto ds_slot = [&](int h) -> char* { return dsr + ((h + 3) % 3) * BX_IMG; };   // h >= -3
+  const int2 off_ds = bx_tr_off(2, lane);                // ds image rows 2 + k <-> positions q0 + k
+  const int2 off_dc = bx_tr_off(1, lane);                // dc image rows 1 + k <-> positions q0 + k
+  const bool tail_lane = hh == 1;                        // K rows 126, 127 (next strip): elements 6, 7 at step 7
 
   for (int64_t u = blockIdx.x; u < (int64_t)a.strips * a.N; u += gridDim.x) {
     const int strip = (int)(u % a.strips), n = (int)(u / a.strips);
     const int q0 = strip * BX_P;
     const __hip_bfloat16* xn = a.x + (int64_t)n * H * W;
     // x row `row` at position q0 - 4 + tid: raw bf16 bits from a clamped (always valid) address, so the load
-    // carries no branch and its wait falls where the row is stored (x_val), a phase or more later
+    // carries no branch and its wait falls where the row is stored (put_x), a phase or more later
     auto x_raw = [&](int row) -> uint32_t {
       const int q = q0 - 4 + tid;
       const int rc = row < 0 ? 0 : (row >= H ? H - 1 : row);
       const int qc = q < 0 ? 0 : (q >= W ? W - 1 : q);
       return reinterpret_cast<const uint16_t*>(xn)[(int64_t)rc * W + qc];
     };
-    auto x_val = [&](int row, uint32_t raw) -> float {   // zero outside the image
-      const int q = q0 - 4 + tid;
-      return (row >= 0 && row < H && q >= 0 && q < W) ? __uint_as_float(raw << 16) : 0.f;
-    };
     auto xslot = [&](int row) -> float* { return xr + (row & 3) * BXB_XW; };
-    // conv1 pre-activation c (bf16-rounded, the unfused kernel's FMA order) at x columns v0 / v1, from a record
-    auto conv1c = [&](const float (&v0)[3], const float (&v1)[3], const float4& r0, const float4& r1) -> float {
-      float acc = v0[0] * r0.x;
-      acc = fmaf(v0[1], r0.y, acc);
-      acc = fmaf(v0[2], r0.z, acc);
-      acc = fmaf(v1[0], r0.w, acc);
-      acc = fmaf(v1[1], r1.x, acc);
-      acc = fmaf(v1[2], r1.y, acc);
-      return bx_bf16(acc);
+    auto xsslot = [&](int row) -> char* { return xs + (row & 3) * (3 * 256); };
+    // x (zero outside the image) into the fp32 ring and the three kw-shifted bf16 copies
+    auto put_x = [&](int row, uint32_t raw) {
+      const int q = q0 - 4 + tid;
+      const uint32_t b = (row >= 0 && row < H && q >= 0 && q < W) ? raw : 0u;
+      if (tid < BXB_XW) {
+        xslot(row)[tid] = __uint_as_float(b << 16);
+        char* xsr = xsslot(row);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int i = tid - 3 - kw;
+          if (i >= 0 && i < 128) *reinterpret_cast<uint16_t*>(xsr + kw * 256 + 2 * i) = (uint16_t)b;
+        }
+      }
     };
     // ds row hrow: the pooled gradient where the window argmax hits, fetched a row ahead into registers
     uint4 pd[DSN];
@@ -439,7 +470,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         pa[j] = make_uint2(0xffffffffu, 0xffffffffu);
         if (it < BX_IR * 4 && hrow >= 0 && hrow < H && i < 130 && w >= 0 && w < W3) {
           const int jj = w / 3;
-          const int64_t off = (((int64_t)n * H + hrow) * Wo + jj) * BX_C + 8 * c8;
+          const int64_t off = (((int64_t)n * H + hrow) * Wo + jj) * BX_C + 8 * (tid & 3);
           pd[j] = *reinterpret_cast<const uint4*>(a.dp + off);
           pa[j] = *reinterpret_cast<const uint2*>(a.arg + off);
         }
@@ -462,7 +493,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
             const uint32_t m1 = (((bits >> 8) & 0xff) == t) ? 0xffff0000u : 0u;
             ow[e] = dw[e] & (m0 | m1);
           }
-          *reinterpret_cast<uint4*>(sl + bx_img(i, c8)) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          *reinterpret_cast<uint4*>(sl + bx_img(i, tid & 3)) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
       }
     };
@@ -472,28 +503,29 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) v[i] = x_raw(i - 1);
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (tid < BXB_XW) xslot(i - 1)[tid] = x_val(i - 1, v[i]);
+      for (int i = 0; i < 3; ++i) put_x(i - 1, v[i]);
     }
     fetch_ds(-1);
     store_ds(-1);       // zeros
     fetch_ds(0);
     BX_STAMP(4);
-    // iteration hp: dout1 / dc row hp (hp <= H), out1 row hp (phase C, used by the d w2 MFMAs of ds row hp - 1 and
-    // hp - 2 in the next two iterations), dx row hp - 1, d w2 of ds row hp - 2 (hp >= 2: out1 rows hp - 2, hp - 1)
+    // iteration hp: dout1 / dc row hp and out1 row hp (hp <= H), dx tap responses of row hp - 1 (stored at hp + 1),
+    // d w1 / d wd of rows hp, d w2 of ds row hp - 2 (hp >= 2)
     for (int hp = 0; hp <= H + 1; ++hp) {
       const bool rowc = hp <= H;
-      // ---- phase A: ds row hp (registers -> LDS), the next row's fetch, x row hp + 2 in flight
+      // ---- phase A: ds row hp (registers -> LDS), the next row's fetch, x row hp + 2 in flight; dx row hp - 2
       const uint32_t xnext = x_raw(hp + 2);
       store_ds(hp);
       fetch_ds(hp + 1);
+      if (hp >= 2 && tid < BX_P && q0 + tid < W)
+        a.dx[((int64_t)n * H + hp - 2) * W + q0 + tid] = (ob[tid + 2] + ob[128 + tid + 1]) + ob[256 + tid];
       __syncthreads();
       BX_STAMP(0);
       // ---- phase B: dout1 row hp = conv(ds rows hp - 1, hp) with the flipped weights -> bf16 into the dc slot;
-      // d w2 += ds row hp - 2 x out1 rows hp - 2, hp - 1 over K = ds image rows 2 .. 129 (positions q0 .. q0 + 127);
-      // rows 128 and 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed (in the last
-      // K step, element j of lane l holds row 2 + 112 + 8 (j >> 2) + 4 (l >> 5) + (j & 3): elements 6, 7 of lanes
-      // 32-63)
+      // d w2 += ds row hp - 2 x out1 rows hp - 2, hp - 1 over K = ds image rows 2 .. 129 (positions q0 ..
+      // q0 + 127); rows 128, 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed
+      // (in the last K step, element j of lane l holds row 2 + 112 + 8 (j >> 2) + 4 (l >> 5) + (j & 3): elements
+      // 6, 7 of lanes 32-63)
       if (rowc) {
         bxf32x16 acc;
 #pragma unroll
@@ -520,24 +552,21 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
       }
       if (hp >= 2) {
         const char* dsi = ds_slot(hp - 2);
-        const bool tail_lane = (lane >> 5) == 1;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int tap = wv + 4 * t;
-          if (tap < 6) {
-            const int kh = tap / 3, kw = tap - 3 * kh;
-            const char* oi = o1r + ((hp + kh) & 1) * BX_IMG;   // out1 row hp - 2 + kh
-            const int2 offa = bx_tr_off(2, lane), offb = bx_tr_off(2 + kw, lane);
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-              bxbf16x8 av = bx_read_tr_at(dsi, offa, s);
-              if (s == 7 && tail_lane) {
-                av[6] = (__bf16)0.0f;
-                av[7] = (__bf16)0.0f;
-              }
-              acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr_at(oi, offb, s), acc2[t], 0, 0, 0);
-            }
+        const int kh0 = wv / 3, kw0 = wv - 3 * kh0;      // tap wv: (0, 0), (0, 1), (0, 2), (1, 0)
+        const char* oi0 = o1r + ((hp + kh0) & 1) * BX_IMG;   // out1 row hp - 2 + kh
+        const char* oi1 = o1r + ((hp + 1) & 1) * BX_IMG;     // taps 4, 5: kh = 1
+        const int2 offb0 = bx_tr_off(2 + kw0, lane), offb1 = bx_tr_off(3 + (wv >> 1), lane);
+        const int s1 = 4 * (wv & 1);
+#pragma unroll 2
+        for (int s = 0; s < 8; ++s) {
+          bxbf16x8 av = bx_read_tr_at(dsi, off_ds, s);
+          if (s == 7 && tail_lane) {
+            av[6] = (__bf16)0.0f;
+            av[7] = (__bf16)0.0f;
           }
+          acc2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr_at(oi0, offb0, s), acc2[0], 0, 0, 0);
+          if (s >= s1 && s < s1 + 4)
+            acc2[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr_at(oi1, offb1, s), acc2[1], 0, 0, 0);
         }
       }
       __syncthreads();
@@ -545,121 +574,133 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
       if (rowc) {
         // ---- phase C: dc row hp = bf16(dO selu'(u) s) in place (rdx_sconv_dgrad_bnselu's arithmetic on c
         // recomputed from x), BN sums over the strip's own positions; out1 row hp = selu(u) (rdx_sincnet_b0_fwd's
-        // value, one exp for both) into the out1 slot of row hp - 2 (read for the last time in phase B above)
+        // value) into the out1 slot of row hp - 2 (read for the last time in phase B above)
         {
           char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
           char* o1s = o1r + (hp & 1) * BX_IMG;
-          const float* xa = xslot(hp - 1);
-          const float* xb = xslot(hp);
+          const int i0 = 8 * pg, cofs = 4 * (cp & 3), cch = cp >> 2;
+          float pw1[2][6], pcb[2], pmu[2], psg[2], psh[2], pis[2];
+          {
+            const float4 r0 = prr[cp], r1 = prr[16 + cp], r2 = prr[32 + cp], r3 = prr[48 + cp], r4 = prr[64 + cp],
+                         r5 = prr[80 + cp];
+            const float w[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
 #pragma unroll
-          for (int jt = 0; jt < 2; ++jt) {
-            const int it = tid + BX_T * jt;
-            const int i = it >> 2;
+            for (int k = 0; k < 6; ++k) {
+              pw1[0][k] = w[k];
+              pw1[1][k] = w[6 + k];
+            }
+            pcb[0] = r3.x, pmu[0] = r3.y, psg[0] = r3.z, psh[0] = r3.w, pis[0] = r4.x;
+            pcb[1] = r4.y, pmu[1] = r4.z, psg[1] = r4.w, psh[1] = r5.x, pis[1] = r5.y;
+          }
+#pragma unroll 1
+          for (int half = 0; half < 2; ++half) {
+          const int i4 = i0 + 4 * half;
+          float xwa[8], xwb[8];   // x ring indices i4 .. i4 + 7 of rows hp - 1 / hp
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const float4 fa = *reinterpret_cast<const float4*>(xslot(hp - 1) + i4 + 4 * v);
+            const float4 fb = *reinterpret_cast<const float4*>(xslot(hp) + i4 + 4 * v);
+            xwa[4 * v] = fa.x;
+            xwa[4 * v + 1] = fa.y;
+            xwa[4 * v + 2] = fa.z;
+            xwa[4 * v + 3] = fa.w;
+            xwb[4 * v] = fb.x;
+            xwb[4 * v + 1] = fb.y;
+            xwb[4 * v + 2] = fb.z;
+            xwb[4 * v + 3] = fb.w;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = i4 + j;   // dc image row <-> position q0 - 1 + i
             const int q = q0 - 1 + i;
             const bool inside = q >= 0 && q < W;
             const bool own = inside && i >= 1 && i <= BX_P;
-            uint4* slot = reinterpret_cast<uint4*>(dcs + bx_img(i, c8));
-            const uint4 dov = *slot;
-            const uint32_t dw[4] = {dov.x, dov.y, dov.z, dov.w};
-            const float v0[3] = {xa[i + 2], xa[i + 3], xa[i + 4]}, v1[3] = {xb[i + 2], xb[i + 3], xb[i + 4]};
-            uint32_t ow[4], oo[4];
+            uint32_t* slot = reinterpret_cast<uint32_t*>(dcs + bx_img(i, cch) + cofs);
+            const uint32_t dov = *slot;
+            float dz[2], yo[2];
 #pragma unroll
-            for (int k = 0; k < 8; k += 2) {
-              float dz[2], yo[2];
-#pragma unroll
-              for (int e = 0; e < 2; ++e) {
-                const int co = 8 * c8 + k + e;
-                const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co], r3 = prec[96 + co];
-                const float cv = conv1c(v0, v1, r0, r1);
-                const float zc = (cv + r2.y) - r2.z;
-                const float xhat = zc * r3.y;
-                const float uu = fmaf(zc, r2.w, r3.x);
-                const float ex = __expf(uu);
-                const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * ex;
-                yo[e] = BX_SELU_SCALE * (uu > 0.f ? uu : BX_SELU_ALPHA * (ex - 1.0f));   // bx_selu(uu)
-                const float dov_e = e == 0 ? bx_lo(dw[k >> 1]) : bx_hi(dw[k >> 1]);
-                const float du = dov_e * sd;
-                dz[e] = inside ? du * r2.w : 0.f;
-                if (own) {
-                  bsum[0][k + e] += dz[e];
-                  bsum[1][k + e] = fmaf(du, xhat, bsum[1][k + e]);
-                  bsum[2][k + e] += du;
-                }
-              }
-              ow[k >> 1] = bx_pack2(dz[0], dz[1]);
-              oo[k >> 1] = inside ? bx_pack2(yo[0], yo[1]) : 0u;
+            for (int e = 0; e < 2; ++e) {
+              // conv1 pre-activation c (bf16-rounded, the unfused kernel's FMA order)
+              float acc = xwa[j + 2] * pw1[e][0];
+              acc = fmaf(xwa[j + 3], pw1[e][1], acc);
+              acc = fmaf(xwa[j + 4], pw1[e][2], acc);
+              acc = fmaf(xwb[j + 2], pw1[e][3], acc);
+              acc = fmaf(xwb[j + 3], pw1[e][4], acc);
+              acc = fmaf(xwb[j + 4], pw1[e][5], acc);
+              const float cv = bx_bf16(acc);
+              const float zc = (cv + pcb[e]) - pmu[e];
+              const float xhat = zc * pis[e];
+              const float uu = fmaf(zc, psg[e], psh[e]);
+              const float ex = __expf(uu);
+              const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * ex;
+              yo[e] = BX_SELU_SCALE * (uu > 0.f ? uu : BX_SELU_ALPHA * (ex - 1.0f));   // bx_selu(uu)
+              const float du = (e == 0 ? bx_lo(dov) : bx_hi(dov)) * sd;
+              dz[e] = inside ? du * psg[e] : 0.f;
+              const float b0 = bsum[0][e] + dz[e], b1 = fmaf(du, xhat, bsum[1][e]), b2 = bsum[2][e] + du;
+              bsum[0][e] = own ? b0 : bsum[0][e];
+              bsum[1][e] = own ? b1 : bsum[1][e];
+              bsum[2][e] = own ? b2 : bsum[2][e];
             }
-            *slot = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-            *reinterpret_cast<uint4*>(o1s + bx_img(i + 2, c8)) = make_uint4(oo[0], oo[1], oo[2], oo[3]);
+            *slot = bx_pack2(dz[0], dz[1]);
+            *reinterpret_cast<uint32_t*>(o1s + bx_img(i + 2, cch) + cofs) = inside ? bx_pack2(yo[0], yo[1]) : 0u;
+          }
           }
         }
         __syncthreads();
         BX_STAMP(2);
-        // ---- phase D: dx row hp - 1, d w1 (dc row hp), d wd / d bias (ds row hp) over the strip's own positions
+        // ---- phase D (MFMA): dx tap responses of row hp - 1; d w1 (dc row hp x x rows hp - 1, hp), d wd and
+        // d bias (ds row hp x x row hp, ones)
         {
           const char* dcA = dcr + (hp & 1) * (BXB_DCR * 64);         // dc row hp
           const char* dcB = dcr + ((hp - 1) & 1) * (BXB_DCR * 64);   // dc row hp - 1
           const char* dsP = ds_slot(hp - 1);                         // ds row hp - 1
           const char* dsC = ds_slot(hp);                             // ds row hp
-          const float* xa = xslot(hp - 1);
-          const float* xb = xslot(hp);
-          const int gc = g >> 1, sub = 8 * (g & 1);
-          for (int it = tid; it < BX_P * 8; it += BX_T) {
-            const int k = it >> 3;
-            const int q = q0 + k;
-            const bool valid = q < W;
-            float pdx = 0.f;
-            if (hp >= 1 && valid) {
+          if (hp >= 1) {
+            // O[kw][k'] = sum_co dcA[k' + 2] w1[., kw] + dcB[k' + 2] w1[., 3 + kw] + dsP[k' + 3] wd[., kw],
+            // k' = 32 wv - 2 + r; dx[k] = O[0][k] + O[1][k - 1] + O[2][k - 2] (phase A of the next iteration)
+            bxf32x16 o;
 #pragma unroll
-              for (int kw = 0; kw < 3; ++kw) {
-                const uint2 A = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 2 - kw, gc) + sub);
-                const uint2 Bv = *reinterpret_cast<const uint2*>(dcB + bx_img(k + 2 - kw, gc) + sub);
-                const uint2 D = *reinterpret_cast<const uint2*>(dsP + bx_img(k + 3 - kw, gc) + sub);
-                const float av[4] = {bx_lo(A.x), bx_hi(A.x), bx_lo(A.y), bx_hi(A.y)};
-                const float bv[4] = {bx_lo(Bv.x), bx_hi(Bv.x), bx_lo(Bv.y), bx_hi(Bv.y)};
-                const float dv[4] = {bx_lo(D.x), bx_hi(D.x), bx_lo(D.y), bx_hi(D.y)};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  const int co = 4 * g + e;
-                  const float4 r0 = prec[co], r1 = prec[32 + co], r2 = prec[64 + co];
-                  const float w1a[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, wda[3] = {r1.z, r1.w, r2.x};
-                  pdx = fmaf(av[e], w1a[kw], pdx);
-                  pdx = fmaf(bv[e], w1a[3 + kw], pdx);
-                  pdx = fmaf(dv[e], wda[kw], pdx);
-                }
-              }
+            for (int i = 0; i < 16; ++i) o[i] = 0.f;
+            const int kp = 32 * wv - 2 + r;
+#pragma unroll 2
+            for (int s = 0; s < 6; ++s) {
+              const int img = s >> 1;
+              const char* src = img == 0 ? dcA : (img == 1 ? dcB : dsP);
+              const bxbf16x8 bv =
+                  *reinterpret_cast<const bxbf16x8*>(src + bx_img(kp + (img == 2 ? 3 : 2), 2 * (s & 1) + hh));
+              const bxbf16x8 wa = *reinterpret_cast<const bxbf16x8*>(wdx + (r < 3 ? (s * 6 + hh * 3 + r) * 16 : 576));
+              o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, bv, o, 0, 0, 0);
             }
-            pdx += __shfl_xor(pdx, 1, 64);
-            pdx += __shfl_xor(pdx, 2, 64);
-            pdx += __shfl_xor(pdx, 4, 64);
-            if (hp >= 1 && valid && g == 0) a.dx[((int64_t)n * H + hp - 1) * W + q] = pdx;
-            if (valid) {
-              const uint2 C = *reinterpret_cast<const uint2*>(dcA + bx_img(k + 1, gc) + sub);
-              const float cv[4] = {bx_lo(C.x), bx_hi(C.x), bx_lo(C.y), bx_hi(C.y)};
-              const float xv0[3] = {xa[k + 3], xa[k + 4], xa[k + 5]}, xv1[3] = {xb[k + 3], xb[k + 4], xb[k + 5]};
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int kw = 0; kw < 3; ++kw) {
-                  aw1[e][kw] = fmaf(cv[e], xv0[kw], aw1[e][kw]);
-                  aw1[e][3 + kw] = fmaf(cv[e], xv1[kw], aw1[e][3 + kw]);
-                }
-              if (hp < H) {
-                const uint2 S = *reinterpret_cast<const uint2*>(dsC + bx_img(k + 2, gc) + sub);
-                const float sv[4] = {bx_lo(S.x), bx_hi(S.x), bx_lo(S.y), bx_hi(S.y)};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  abias[e] += sv[e];
-#pragma unroll
-                  for (int kw = 0; kw < 3; ++kw) awd[e][kw] = fmaf(sv[e], xv1[kw], awd[e][kw]);
-                }
-              }
+            if (hh == 0) {   // D[m][n]: element i of lane n < 32 holds m = i for i < 3
+              ob[kp + 2] = o[0];
+              ob[128 + kp + 2] = o[1];
+              ob[256 + kp + 2] = o[2];
             }
+          }
+          // B operand: element j of lane (n, h) = X[16 s + 8 (j >> 2) + 4 h + (j & 3)][n] (the transposed A's K order)
+          const int nn1 = r < 6 ? r : 5, nn2 = r >= 8 && r < 11 ? r - 8 : 0;
+          const char* xb1 = xsslot(hp - 1 + nn1 / 3) + (nn1 % 3) * 256;
+          const char* xb2 = xsslot(hp) + nn2 * 256;
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) {
+            const int s = 2 * wv + ss;
+            bxbf16x8 ac = bx_read_tr_at(dcA, off_dc, s), as = bx_read_tr_at(dsC, off_ds, s);
+            if (s == 7 && tail_lane) {
+              ac[6] = ac[7] = as[6] = as[7] = (__bf16)0.0f;
+            }
+            const int kb = 2 * (16 * s + 4 * hh);
+            const uint2 p1a = *reinterpret_cast<const uint2*>(xb1 + kb), p1b = *reinterpret_cast<const uint2*>(xb1 + kb + 16);
+            const uint2 p2a = *reinterpret_cast<const uint2*>(xb2 + kb), p2b = *reinterpret_cast<const uint2*>(xb2 + kb + 16);
+            const uint32_t one2 = 0x3f803f80u;   // bf16 1.0 pair: the bias column
+            const uint4 w1v = r < 6 ? make_uint4(p1a.x, p1a.y, p1b.x, p1b.y) : make_uint4(0u, 0u, 0u, 0u);
+            const uint4 w2v = (r >= 8 && r < 11) ? make_uint4(p2a.x, p2a.y, p2b.x, p2b.y)
+                                                 : (r == 11 ? make_uint4(one2, one2, one2, one2) : make_uint4(0u, 0u, 0u, 0u));
+            accw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac, __builtin_bit_cast(bxbf16x8, w1v), accw, 0, 0, 0);
+            accw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as, __builtin_bit_cast(bxbf16x8, w2v), accw, 0, 0, 0);
           }
         }
       }
-      // x row hp + 2 into the slot of row hp - 2 (no reader in this row)
-      if (tid < BXB_XW) xslot(hp + 2)[tid] = x_val(hp + 2, xnext);
+      put_x(hp + 2, xnext);   // x row hp + 2 into the slots of row hp - 2 (no reader in this row)
       __syncthreads();
       BX_STAMP(3);
     }
@@ -669,47 +710,47 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) bx_prof[blockIdx.x][k] = (unsigned long long)prof_acc[k];
 #endif
+
   // ---- per-workgroup partial row (fixed-order sums: bitwise repeatable) ----
+  // D element i of lane (n, h) is [m = (i & 3) + 8 (i >> 2) + 4 h][n]
   float* out = a.part + (int64_t)blockIdx.x * BXB_NPART;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {   // d w2: lane owns ci = lane & 31, co = (i & 3) + 8 (i >> 2) + 4 hh
-    const int tap = wv + 4 * t;
-    if (tap < 6)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int co = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        out[(tap * BX_C + co) * BX_C + r] = acc2[t][i];
-      }
+  for (int i = 0; i < 16; ++i) {   // d w2 taps 0..3: [tap][co][ci], ci = n
+    const int co = (i & 3) + 8 * (i >> 2) + 4 * hh;
+    out[(wv * BX_C + co) * BX_C + r] = acc2[0][i];
   }
-  float* red = reinterpret_cast<float*>(lds);   // the rings are free: [256][40] + [256][24] thread sums
+  float* red = reinterpret_cast<float*>(lds);   // [2 tiles][4 waves][16][64] MFMA partials, then [256][6] BN sums
   __syncthreads();
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-#pragma unroll
-    for (int j = 0; j < 6; ++j) red[tid * 40 + e * 6 + j] = aw1[e][j];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) red[tid * 40 + 24 + e * 3 + j] = awd[e][j];
-    red[tid * 40 + 36 + e] = abias[e];
+  for (int i = 0; i < 16; ++i) {
+    red[((0 * 4 + wv) * 16 + i) * 64 + lane] = acc2[1][i];
+    red[((1 * 4 + wv) * 16 + i) * 64 + lane] = accw[i];
   }
-  float* bred = red + 256 * 40;
+  float* bred = red + 2 * 4 * 16 * 64;
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) bred[tid * 24 + q * 8 + k] = bsum[q][k];
+    for (int e = 0; e < 2; ++e) bred[tid * 6 + q * 2 + e] = bsum[q][e];
   __syncthreads();
-  // d w1 [32][6], d wd [32][3], d bias [32]: channel co = 4 g + e sums the 32 threads with tid & 7 == g
-  for (int i = tid; i < 32 * 10; i += BX_T) {
-    const int co = i / 10, j = i % 10, gq = co >> 2, e = co & 3;
-    const int slot = j < 6 ? e * 6 + j : (j < 9 ? 24 + e * 3 + (j - 6) : 36 + e);
-    float s = 0.f;
-    for (int t = 0; t < 32; ++t) s += red[(t * 8 + gq) * 40 + slot];
+  auto tile_at = [&](int t, int w, int m, int nn) -> float {   // element [m][nn] of tile t of wave w
+    const int h = (m >> 2) & 1, i = (m & 3) + 4 * (m >> 3);
+    return red[((t * 4 + w) * 16 + i) * 64 + nn + 32 * h];
+  };
+  for (int idx = tid; idx < 2 * 32 * 32; idx += BX_T) {   // d w2 taps 4 (waves 0 + 1), 5 (waves 2 + 3)
+    const int tap = idx >> 10, co = (idx >> 5) & 31, ci = idx & 31;
+    out[((4 + tap) * BX_C + co) * BX_C + ci] = tile_at(0, 2 * tap, co, ci) + tile_at(0, 2 * tap + 1, co, ci);
+  }
+  for (int idx = tid; idx < 32 * 10; idx += BX_T) {   // d w1 [32][6], d wd [32][3], d bias [32]: sum of 4 waves
+    const int co = idx / 10, j = idx % 10;
+    const int nn = j < 6 ? j : j + 2;
+    const float s = ((tile_at(1, 0, co, nn) + tile_at(1, 1, co, nn)) + tile_at(1, 2, co, nn)) + tile_at(1, 3, co, nn);
     const int dst = j < 6 ? 6144 + co * 6 + j : (j < 9 ? 6144 + 192 + co * 3 + (j - 6) : 6144 + 192 + 96 + co);
     out[dst] = s;
   }
-  if (tid < 96) {   // BN sums [3][32]: channel co = 8 c8 + k sums the 64 threads with tid & 3 == c8
-    const int q = tid / 32, co = tid % 32, cq = co >> 3, k = co & 7;
+  if (tid < 96) {   // BN sums [3][32]: channel co = 2 cp + e sums the 16 threads with tid & 15 == cp
+    const int q = tid / 32, co = tid % 32, c2 = co >> 1, e = co & 1;
     float s = 0.f;
-    for (int t = 0; t < 64; ++t) s += bred[(t * 4 + cq) * 24 + q * 8 + k];
+    for (int t = 0; t < 16; ++t) s += bred[(t * 16 + c2) * 6 + q * 2 + e];
     out[6144 + 192 + 96 + 32 + q * 32 + co] = s;
   }
 }
