@@ -94,10 +94,17 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
     sh[k] = a.bn[3 * BX_C + co];
   }
   const __hip_bfloat16* xn_base = a.x + (int64_t)n * H * W;
-  auto load_x = [&](int row) -> float {   // x[row][q0 - 2 + tid], zero outside the image
+  // x[row][q0 - 2 + tid] as raw bf16 bits from a clamped (always valid) address: no branch around the load, so
+  // its wait falls where the value is stored (x_val), after the row's MFMAs
+  auto x_raw = [&](int row) -> uint32_t {
     const int q = q0 - 2 + tid;
-    return (tid < BX_XW && row >= 0 && row < H && q >= 0 && q < W) ? __bfloat162float(xn_base[(int64_t)row * W + q])
-                                                                    : 0.f;
+    const int rc = row < 0 ? 0 : (row >= H ? H - 1 : row);
+    const int qc = q < 0 ? 0 : (q >= W ? W - 1 : q);
+    return reinterpret_cast<const uint16_t*>(xn_base)[(int64_t)rc * W + qc];
+  };
+  auto x_val = [&](int row, uint32_t raw) -> float {   // zero outside the image
+    const int q = q0 - 2 + tid;
+    return (row >= 0 && row < H && q >= 0 && q < W) ? __uint_as_float(raw << 16) : 0.f;
   };
   auto xslot = [&](int row) -> float* { return xr + (row & 3) * BX_XW; };
   auto oslot = [&](int row) -> char* { return os + (row % 3) * BX_IMG; };
@@ -133,19 +140,19 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   const int pw = wv * 32 + r;   // this lane's output position q0 + pw (B operand row of the MFMA)
 
   {  // prologue: x rows h0 - 1 .. h0 + 2, out1 rows h0 and h0 + 1
-    float v[4];
+    uint32_t v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = load_x(h0 - 1 + i);
+    for (int i = 0; i < 4; ++i) v[i] = x_raw(h0 - 1 + i);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (tid < BX_XW) xslot(h0 - 1 + i)[tid] = v[i];
+      if (tid < BX_XW) xslot(h0 - 1 + i)[tid] = x_val(h0 - 1 + i, v[i]);
   }
   __syncthreads();
   make_out1(h0);
   make_out1(h0 + 1);
   __syncthreads();
   for (int h = h0; h < h1; ++h) {
-    const float xnext = load_x(h + 3);
+    const uint32_t xnext = x_raw(h + 3);
     bxf32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
         *reinterpret_cast<float4*>(ss + pw * BX_SP + 8 * g + 4 * hh) = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
-    if (tid < BX_XW) xslot(h + 3)[tid] = xnext;   // the slot of x row h - 1 (no reader after the last barrier)
+    if (tid < BX_XW) xslot(h + 3)[tid] = x_val(h + 3, xnext);   // the slot of x row h - 1 (no reader after the last barrier)
     __syncthreads();
     if (tid < BX_J * 4) {   // pool: (window j, 8 channels) per thread, 16-byte stores of consecutive chunks
       const int j = tid >> 2, g = tid & 3;
@@ -258,16 +265,16 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
 // the unfused ones up to the order of their fp32 sums.
 //
 // A workgroup walks units (utterance, strip of 126 positions) in a grid-stride loop and, per unit, the rows
-// top-down; iteration hp has four phases:
-//   (A) ds row hp into an LDS ring of 3 (its pooled gradient and argmax fetched a row ahead); dx row hp - 2 from
-//       the three tap responses phase D left in LDS;
-//   (B) dout1 row hp on the MFMA (ds rows hp - 1, hp) into the dc ring (2 rows), and the d w2 MFMAs of ds row
-//       hp - 2 x out1 rows hp - 2, hp - 1 (6 taps x 8 K steps, 12 per wave);
+// top-down; iteration hp has three phases between barriers:
+//   (B) dx row hp - 2 from the three tap responses phase D left in LDS; dout1 row hp on the MFMA (ds rows hp - 1,
+//       hp) into the dc ring (2 rows), and the d w2 MFMAs of ds row hp - 2 x out1 rows hp - 2, hp - 1 (6 taps x
+//       8 K steps, 12 per wave);
 //   (C) the BN + SELU backward of dout1 row hp in place and out1 row hp = selu(u) (c recomputed from x, one exp
 //       for both), a thread owning 2 channels (their frozen-BN / conv1 parameters in registers) x 8 positions;
 //   (D) on the MFMA: dx's three tap responses O[kw][k] = sum_co (dc rows hp, hp - 1 | ds row hp - 1) x (w1 | wd)
 //       (M = kw, K = 3 images x 32 channels, N = positions), and d w1 / d wd / d bias as dc^T / ds^T x the x taps
-//       (K = positions, N = taps; x kept as three bf16 copies shifted by kw).
+//       (K = positions, N = taps; x kept as three bf16 copies shifted by kw); then ds row hp + 1 into the LDS
+//       ring of 3 (its pooled gradient and argmax fetched a row ahead) and x row hp + 2 into the x rings.
 // Every sum counts the strip's own positions [126 s, 126 s + 126) (the K = position MFMAs run over 128 positions
 // and zero the last two); with Wo / 42 + 1 strips they partition every position that carries a gradient.
 // Per-workgroup sums go to one fp32 partial row (the caller sums the rows: no atomics).
@@ -508,19 +515,18 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     fetch_ds(-1);
     store_ds(-1);       // zeros
     fetch_ds(0);
+    store_ds(0);
+    fetch_ds(1);
+    __syncthreads();
     BX_STAMP(4);
     // iteration hp: dout1 / dc row hp and out1 row hp (hp <= H), dx tap responses of row hp - 1 (stored at hp + 1),
     // d w1 / d wd of rows hp, d w2 of ds row hp - 2 (hp >= 2)
     for (int hp = 0; hp <= H + 1; ++hp) {
       const bool rowc = hp <= H;
-      // ---- phase A: ds row hp (registers -> LDS), the next row's fetch, x row hp + 2 in flight; dx row hp - 2
+      // x row hp + 2 in flight (stored at the end of phase D); dx row hp - 2 from the tap responses in LDS
       const uint32_t xnext = x_raw(hp + 2);
-      store_ds(hp);
-      fetch_ds(hp + 1);
       if (hp >= 2 && tid < BX_P && q0 + tid < W)
         a.dx[((int64_t)n * H + hp - 2) * W + q0 + tid] = (ob[tid + 2] + ob[128 + tid + 1]) + ob[256 + tid];
-      __syncthreads();
-      BX_STAMP(0);
       // ---- phase B: dout1 row hp = conv(ds rows hp - 1, hp) with the flipped weights -> bf16 into the dc slot;
       // d w2 += ds row hp - 2 x out1 rows hp - 2, hp - 1 over K = ds image rows 2 .. 129 (positions q0 ..
       // q0 + 127); rows 128, 129 (q0 + 126, q0 + 127) belong to the next strip: their A elements are zeroed
@@ -657,7 +663,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           const char* dsC = ds_slot(hp);                             // ds row hp
           if (hp >= 1) {
             // O[kw][k'] = sum_co dcA[k' + 2] w1[., kw] + dcB[k' + 2] w1[., 3 + kw] + dsP[k' + 3] wd[., kw],
-            // k' = 32 wv - 2 + r; dx[k] = O[0][k] + O[1][k - 1] + O[2][k - 2] (phase A of the next iteration)
+            // k' = 32 wv - 2 + r; dx[k] = O[0][k] + O[1][k - 1] + O[2][k - 2] (phase B of the next iteration)
             bxf32x16 o;
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[i] = 0.f;
@@ -699,9 +705,12 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
             accw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as, __builtin_bit_cast(bxbf16x8, w2v), accw, 0, 0, 0);
           }
         }
+        // the next row's ds into the slot of row hp - 2 (read for the last time in phase B), its successor's fetch
+        store_ds(hp + 1);
+        fetch_ds(hp + 2);
+        put_x(hp + 2, xnext);   // x row hp + 2 into the slots of row hp - 2 (no reader in this row)
+        __syncthreads();
       }
-      put_x(hp + 2, xnext);   // x row hp + 2 into the slots of row hp - 2 (no reader in this row)
-      __syncthreads();
       BX_STAMP(3);
     }
   }
