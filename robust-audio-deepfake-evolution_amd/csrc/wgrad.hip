@@ -41,26 +41,36 @@ __device__ __forceinline__ wrbf16x8 wr_read_tr(const char* img, int c0, int s, i
   return r;
 }
 
-// rows [m0, m0 + MC) x columns [c0, c0 + 64) of a [M][ld] bf16 matrix into an image (zeros outside)
-__device__ __forceinline__ void wr_stage(char* img, const __hip_bfloat16* __restrict__ src, int64_t ld, int M, int C,
-                                         int m0, int c0, int mc, bool vec) {
-  for (int i = threadIdx.x; i < mc * 8; i += WR_T) {
+// rows [m0, m0 + mc) x columns [c0, c0 + 64) of a [M][ld] bf16 matrix into an image (zeros outside): every
+// load of the thread is issued before the first LDS store, so their latencies overlap
+constexpr int WR_ITEMS = WR_MAXMC * 8 / WR_T;   // 16-byte items per thread, at most
+__device__ __forceinline__ void wr_gather(uint4 (&v)[WR_ITEMS], const __hip_bfloat16* __restrict__ src, int64_t ld,
+                                          int M, int C, int m0, int c0, int mc, bool vec) {
+#pragma unroll
+  for (int j = 0; j < WR_ITEMS; ++j) {
+    const int i = threadIdx.x + WR_T * j;
     const int row = i >> 3, ch = i & 7;
     const int m = m0 + row, c = c0 + 8 * ch;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (m < M) {
+    v[j] = make_uint4(0u, 0u, 0u, 0u);
+    if (i < mc * 8 && m < M) {
       const __hip_bfloat16* p = src + (int64_t)m * ld + c;
       if (vec && c + 8 <= C) {
-        v = *reinterpret_cast<const uint4*>(p);
+        v[j] = *reinterpret_cast<const uint4*>(p);
       } else {
         uint16_t e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = (c + j < C) ? __bfloat16_as_ushort(p[j]) : (uint16_t)0;
-        v = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
-                       e[6] | ((uint32_t)e[7] << 16));
+        for (int t = 0; t < 8; ++t) e[t] = (c + t < C) ? __bfloat16_as_ushort(p[t]) : (uint16_t)0;
+        v[j] = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
+                          e[6] | ((uint32_t)e[7] << 16));
       }
     }
-    *reinterpret_cast<uint4*>(img + wr_img(row, ch)) = v;
+  }
+}
+__device__ __forceinline__ void wr_put(char* img, const uint4 (&v)[WR_ITEMS], int mc) {
+#pragma unroll
+  for (int j = 0; j < WR_ITEMS; ++j) {
+    const int i = threadIdx.x + WR_T * j;
+    if (i < mc * 8) *reinterpret_cast<uint4*>(img + wr_img(i >> 3, i & 7)) = v[j];
   }
 }
 
@@ -82,8 +92,13 @@ __global__ __launch_bounds__(WR_T) void wgrad_part_kernel(WgradArgs a) {
   const int bn = blk / a.nbk, bk = blk - bn * a.nbk;
   const int n0 = bn * 64, k0 = bk * 64, m0 = s * a.mc;
   const int mc = a.mc;
-  wr_stage(iy, a.dy, a.ldy, a.M, a.N, m0, n0, mc, a.vy);
-  wr_stage(ix, a.x, a.ldx, a.M, a.K, m0, k0, mc, a.vx);
+  {
+    uint4 vy[WR_ITEMS], vx[WR_ITEMS];
+    wr_gather(vy, a.dy, a.ldy, a.M, a.N, m0, n0, mc, a.vy);
+    wr_gather(vx, a.x, a.ldx, a.M, a.K, m0, k0, mc, a.vx);
+    wr_put(iy, vy, mc);
+    wr_put(ix, vx, mc);
+  }
   __syncthreads();
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int tn = wv >> 1, tk = wv & 1;
@@ -113,21 +128,43 @@ __global__ __launch_bounds__(WR_T) void wgrad_part_kernel(WgradArgs a) {
   }
 }
 
-// dW[n][k] += sum_s part[s][n][k] (s in order); db[n] += sum_s partb[s][n]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ partb, int S, int N, int K,
-                                    float* __restrict__ dw, int64_t ldw, float* __restrict__ db) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// dW[n][k] += sum_s part[s][n][k], db[n] += sum_s partb[s][n]. A 256-thread block owns 64 consecutive outputs;
+// wave w sums the chunks s = w, w + 4, ... in four independent chains (the loads of a thread overlap instead of
+// running S dependent steps), and the four waves' sums are added in a fixed order: deterministic.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
+                                                           const float* __restrict__ partb, int S, int N, int K,
+                                                           float* __restrict__ dw, int64_t ldw,
+                                                           float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nk = (int64_t)N * K;
-  if (i < nk) {
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += part[(int64_t)s * nk + i];
-    const int n = (int)(i / K), k = (int)(i - (int64_t)n * K);
-    dw[(int64_t)n * ldw + k] += v;
-  } else if (db && i < nk + N) {
-    const int n = (int)(i - nk);
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += partb[(int64_t)s * N + n];
-    db[n] += v;
+  const int64_t tot = nk + (db ? N : 0);
+  const int64_t i = (int64_t)blockIdx.x * 64 + l;
+  float v = 0.f;
+  if (i < tot) {
+    const float* src = i < nk ? part + i : partb + (i - nk);
+    const int64_t st = i < nk ? nk : (int64_t)N;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = w;
+    for (; s + 12 < S; s += 16) {
+      a0 += src[(int64_t)s * st];
+      a1 += src[(int64_t)(s + 4) * st];
+      a2 += src[(int64_t)(s + 8) * st];
+      a3 += src[(int64_t)(s + 12) * st];
+    }
+    for (; s < S; s += 4) a0 += src[(int64_t)s * st];
+    v = (a0 + a1) + (a2 + a3);
+  }
+  red[w][l] = v;
+  __syncthreads();
+  if (w == 0 && i < tot) {
+    const float t = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
+    if (i < nk) {
+      const int n = (int)(i / K), k = (int)(i - (int64_t)n * K);
+      dw[(int64_t)n * ldw + k] += t;
+    } else {
+      db[i - nk] += t;
+    }
   }
 }
 
@@ -187,7 +224,7 @@ extern "C" int rdx_wgrad_acc(const void* dy, int64_t ldy, const void* x, int64_t
                      st, a);
   RDX_LAUNCH_CHECK();
   const int64_t tot = (int64_t)N * K + (db ? N : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ws, a.partb, S, N, K,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, st, ws, a.partb, S, N, K,
                      dw, ldw, db);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
