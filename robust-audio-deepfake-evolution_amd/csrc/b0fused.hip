@@ -62,7 +62,27 @@ struct BxFwdArgs {
   int N, H, W, Wo, rows_per;
 };
 
+#ifdef BX_PROF
+// tools/prof_b0x.hip: shader-cycle sums over every workgroup of the forward's row phases (conv2 MFMAs, out1 of
+// row h + 2, s = a + idn + bias staging, pool)
+__device__ unsigned long long bx_prof_f[4];
+#define BXF_STAMP(k)                    \
+  do {                                  \
+    const long long t_ = clock64();     \
+    pf_acc[k] += t_ - pf_t;             \
+    pf_t = t_;                          \
+  } while (0)
+#else
+#define BXF_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
+#ifdef BX_PROF
+  long long pf_acc[4] = {0, 0, 0, 0};
+  long long pf_t = clock64();
+#endif
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* ws = lds;                                           // conv2 weights: rows tap * 32 + co
   char* os = ws + 192 * 64;                                 // out1 ring: 3 slots
@@ -151,6 +171,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   make_out1(h0);
   make_out1(h0 + 1);
   __syncthreads();
+#ifdef BX_PROF
+  pf_t = clock64();
+#endif
   for (int h = h0; h < h1; ++h) {
     const uint32_t xnext = x_raw(h + 3);
     bxf32x16 acc;
@@ -168,7 +191,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf, acc, 0, 0, 0);   // Y^T: rows co, columns positions
         }
     }
+    BXF_STAMP(0);
     if (h + 1 < h1) make_out1(h + 2);   // the next row's second input row (slot of row h - 1: read last row)
+    BXF_STAMP(1);
     {  // s = (a + idn) + bias at position q0 + pw, channels 8g + 4hh + e
       const float* xh = xslot(h);
       const float x0 = xh[pw + 1], x1 = xh[pw + 2], x2 = xh[pw + 3];
@@ -188,6 +213,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
     }
     if (tid < BX_XW) xslot(h + 3)[tid] = x_val(h + 3, xnext);   // the slot of x row h - 1 (no reader after the last barrier)
     __syncthreads();
+    BXF_STAMP(2);
     if (tid < BX_J * 4) {   // pool: (window j, 8 channels) per thread, 16-byte stores of consecutive chunks
       const int j = tid >> 2, g = tid & 3;
       const int jo = strip * BX_J + j;
@@ -214,7 +240,13 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
       }
     }
     __syncthreads();
+    BXF_STAMP(3);
   }
+#ifdef BX_PROF
+  if (tid == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) atomicAdd(&bx_prof_f[k], (unsigned long long)pf_acc[k]);
+#endif
 }
 
 }  // namespace rdx

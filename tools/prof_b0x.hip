@@ -92,6 +92,8 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "fwd rc %d\n", rc);
       return 1;
     }
+    std::vector<unsigned long long> zf(4, 0);
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(rdx::bx_prof_f), zf.data(), 4 * 8));
     CK(hipEventRecord(e0));
     for (int i = 0; i < reps; ++i) rdx_b0x_fwd(x, w1, wd, bn, w2f, bn, y, yarg, N, H, W, nullptr);
     CK(hipEventRecord(e1));
@@ -99,6 +101,10 @@ int main(int argc, char** argv) {
     float fms;
     CK(hipEventElapsedTime(&fms, e0, e1));
     std::printf("forward ms/launch %.4f\n", fms / reps);
+    CK(hipMemcpyFromSymbol(zf.data(), HIP_SYMBOL(rdx::bx_prof_f), 4 * 8));
+    const double frows = (double)reps * N * ((Wo + BX_J - 1) / BX_J) * H;
+    const char* fn[4] = {"conv2 MFMA", "out1 h+2", "s staging", "pool"};
+    for (int k = 0; k < 4; ++k) std::printf("forward %-10s cycles/row %8.0f\n", fn[k], (double)zf[k] / frows);
   }
   std::vector<unsigned long long> prof((size_t)BXB_BLOCKS * 5);
   CK(hipMemcpyFromSymbol(prof.data(), HIP_SYMBOL(bx_prof), prof.size() * 8));
