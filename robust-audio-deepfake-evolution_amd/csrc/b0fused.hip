@@ -49,6 +49,23 @@ __device__ __forceinline__ uint32_t bx_pack2(float a, float b) {
 __device__ __forceinline__ int bx_img(int row, int ch) {
   return 512 * (row >> 3) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
+__device__ __forceinline__ float bx_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bx_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// Two channels at once on the packed fp32 VALU (v_pk_fma / v_pk_mul / v_pk_add: per component the same IEEE
+// operations, so the results keep the scalar code's bits): conv1's pre-activation c (the unfused kernel's FMA
+// order), rounded to bf16
+typedef float bxf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bxf2 bx_conv1_pair(const float (&v0)[3], const float (&v1)[3], const bxf2 (&w)[6]) {
+  bxf2 acc = v0[0] * w[0];
+  acc = __builtin_elementwise_fma((bxf2)v0[1], w[1], acc);
+  acc = __builtin_elementwise_fma((bxf2)v0[2], w[2], acc);
+  acc = __builtin_elementwise_fma((bxf2)v1[0], w[3], acc);
+  acc = __builtin_elementwise_fma((bxf2)v1[1], w[4], acc);
+  acc = __builtin_elementwise_fma((bxf2)v1[2], w[5], acc);
+  const uint32_t c = bx_pack2(acc.x, acc.y);
+  return (bxf2){bx_lo(c), bx_hi(c)};
+}
 
 struct BxFwdArgs {
   const __hip_bfloat16* x;   // [N, H, W] (the one input channel)
@@ -361,9 +378,6 @@ __device__ __forceinline__ bxbf16x8 bx_read_tr_at(const char* img, int2 off, int
   }
   return r;
 }
-__device__ __forceinline__ float bx_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bx_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-
 struct BxBwdArgs {
   const __hip_bfloat16* x;    // [N, H, W]
   const __hip_bfloat16* dp;   // [N, H, Wo, 32] pooled-output gradient
@@ -451,9 +465,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
     prr[64 + tid] = make_float4(a.bn[4 * BX_C + c0], a.bn[c1], a.bn[BX_C + c1], a.bn[2 * BX_C + c1]);
     prr[80 + tid] = make_float4(a.bn[3 * BX_C + c1], a.bn[4 * BX_C + c1], 0.f, 0.f);
   }
-  float bsum[3][2];
+  bxf2 bsum[3];   // channels 2 cp, 2 cp + 1: d cb, d gamma, d beta
 #pragma unroll
-  for (int q = 0; q < 3; ++q) bsum[q][0] = bsum[q][1] = 0.f;
+  for (int q = 0; q < 3; ++q) bsum[q] = (bxf2)0.f;
   // d w2: acc2[0] = tap wv over every K step; acc2[1] = tap 4 + (wv >> 1) over K steps 4 (wv & 1) .. + 3.
   // accw = D[co][n] over K steps 2 wv, 2 wv + 1: n < 6 d w1 (tap n, from dc), n = 8 + kw d wd and n = 11 d bias
   // (from ds): the two B operands have disjoint nonzero columns, so both products accumulate into one tile
@@ -617,18 +631,18 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
           char* o1s = o1r + (hp & 1) * BX_IMG;
           const int i0 = 8 * pg, cofs = 4 * (cp & 3), cch = cp >> 2;
-          float pw1[2][6], pcb[2], pmu[2], psg[2], psh[2], pis[2];
+          bxf2 pw1[6], pcb, pmu, psg, psh, pis;   // the pair's conv1 weights and frozen BN
           {
             const float4 r0 = prr[cp], r1 = prr[16 + cp], r2 = prr[32 + cp], r3 = prr[48 + cp], r4 = prr[64 + cp],
                          r5 = prr[80 + cp];
             const float w[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-              pw1[0][k] = w[k];
-              pw1[1][k] = w[6 + k];
-            }
-            pcb[0] = r3.x, pmu[0] = r3.y, psg[0] = r3.z, psh[0] = r3.w, pis[0] = r4.x;
-            pcb[1] = r4.y, pmu[1] = r4.z, psg[1] = r4.w, psh[1] = r5.x, pis[1] = r5.y;
+            for (int k = 0; k < 6; ++k) pw1[k] = (bxf2){w[k], w[6 + k]};
+            pcb = (bxf2){r3.x, r4.y};
+            pmu = (bxf2){r3.y, r4.z};
+            psg = (bxf2){r3.z, r4.w};
+            psh = (bxf2){r3.w, r5.x};
+            pis = (bxf2){r4.x, r5.y};
           }
 #pragma unroll 1
           for (int half = 0; half < 2; ++half) {
@@ -655,32 +669,25 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
             const bool own = inside && i >= 1 && i <= BX_P;
             uint32_t* slot = reinterpret_cast<uint32_t*>(dcs + bx_img(i, cch) + cofs);
             const uint32_t dov = *slot;
-            float dz[2], yo[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              // conv1 pre-activation c (bf16-rounded, the unfused kernel's FMA order)
-              float acc = xwa[j + 2] * pw1[e][0];
-              acc = fmaf(xwa[j + 3], pw1[e][1], acc);
-              acc = fmaf(xwa[j + 4], pw1[e][2], acc);
-              acc = fmaf(xwb[j + 2], pw1[e][3], acc);
-              acc = fmaf(xwb[j + 3], pw1[e][4], acc);
-              acc = fmaf(xwb[j + 4], pw1[e][5], acc);
-              const float cv = bx_bf16(acc);
-              const float zc = (cv + pcb[e]) - pmu[e];
-              const float xhat = zc * pis[e];
-              const float uu = fmaf(zc, psg[e], psh[e]);
-              const float ex = __expf(uu);
-              const float sd = uu > 0.f ? BX_SELU_SCALE : BX_SELU_SCALE * BX_SELU_ALPHA * ex;
-              yo[e] = BX_SELU_SCALE * (uu > 0.f ? uu : BX_SELU_ALPHA * (ex - 1.0f));   // bx_selu(uu)
-              const float du = (e == 0 ? bx_lo(dov) : bx_hi(dov)) * sd;
-              dz[e] = inside ? du * psg[e] : 0.f;
-              const float b0 = bsum[0][e] + dz[e], b1 = fmaf(du, xhat, bsum[1][e]), b2 = bsum[2][e] + du;
-              bsum[0][e] = own ? b0 : bsum[0][e];
-              bsum[1][e] = own ? b1 : bsum[1][e];
-              bsum[2][e] = own ? b2 : bsum[2][e];
-            }
-            *slot = bx_pack2(dz[0], dz[1]);
-            *reinterpret_cast<uint32_t*>(o1s + bx_img(i + 2, cch) + cofs) = inside ? bx_pack2(yo[0], yo[1]) : 0u;
+            // c (bf16-rounded, the unfused kernel's FMA order), u, and from one exp both selu'(u) and selu(u)
+            const float v0[3] = {xwa[j + 2], xwa[j + 3], xwa[j + 4]}, v1[3] = {xwb[j + 2], xwb[j + 3], xwb[j + 4]};
+            const bxf2 cv = bx_conv1_pair(v0, v1, pw1);
+            const bxf2 zc = (cv + pcb) - pmu;
+            const bxf2 xhat = zc * pis;
+            const bxf2 uu = __builtin_elementwise_fma(zc, psg, psh);
+            const bxf2 ex = {__expf(uu.x), __expf(uu.y)};
+            const bxf2 sdn = (BX_SELU_SCALE * BX_SELU_ALPHA) * ex;
+            const bxf2 sd = {uu.x > 0.f ? BX_SELU_SCALE : sdn.x, uu.y > 0.f ? BX_SELU_SCALE : sdn.y};
+            const bxf2 ng = BX_SELU_ALPHA * (ex - 1.0f);
+            const bxf2 yo = BX_SELU_SCALE * (bxf2){uu.x > 0.f ? uu.x : ng.x, uu.y > 0.f ? uu.y : ng.y};   // bx_selu
+            const bxf2 du = (bxf2){bx_lo(dov), bx_hi(dov)} * sd;
+            const bxf2 dz = inside ? du * psg : (bxf2)0.f;
+            const bxf2 b0 = bsum[0] + dz, b1 = __builtin_elementwise_fma(du, xhat, bsum[1]), b2 = bsum[2] + du;
+            bsum[0] = own ? b0 : bsum[0];
+            bsum[1] = own ? b1 : bsum[1];
+            bsum[2] = own ? b2 : bsum[2];
+            *slot = bx_pack2(dz.x, dz.y);
+            *reinterpret_cast<uint32_t*>(o1s + bx_img(i + 2, cch) + cofs) = inside ? bx_pack2(yo.x, yo.y) : 0u;
           }
           }
         }

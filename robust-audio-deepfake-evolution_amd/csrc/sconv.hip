@@ -539,8 +539,8 @@ extern "C" int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, co
   SC_DISPATCH(sconv_fwd_launch, a, st)
 }
 
-// conv2's input gradient continued through conv1's frozen BN + SELU backward (Residual_block, the 32-channel
-// blocks): dO1 = conv(dy[N, H, W, ci], w) (w: the flipped, transposed kernel, tap-major [kh*3][co][ci]; ph:
+// conv2's input gradient continued through conv1's frozen BN + SELU backward (Residual_block, the 32- and
+// 64-channel blocks): dO1 = conv(dy[N, H, W, ci], w) (w: the flipped, transposed kernel, tap-major [kh*3][co][ci]; ph:
 // kh - 1 - conv2's row padding), never stored; dc[N, Ho, W, co] = bf16(dO1) * selu'(u) * s with the saved
 // pre-activation c, and sums[3][co] += (sum dc, sum dc/s * xhat, sum dc/s) — exactly rdx_bnselu_bwd on the
 // unfused dO1. bn = [cb | mean | invstd*gamma | beta | invstd] (5 x co fp32); sums zeroed by the caller.
@@ -549,7 +549,7 @@ extern "C" int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void*
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   RDX_REQUIRE(dy && w && c && dc && bn && sums && N > 0 && H > 0 && W > 0 && ph >= 0 && ph <= kh);
   RDX_REQUIRE(al(dy) && al(w) && al(c) && al(dc) && N <= 65535);
-  if (!(ci == 32 && co == 32 && kh == 2)) return RDX_EUNSUPPORTED;
+  if (!((ci == 32 && co == 32) || (ci == 64 && co == 64)) || kh != 2) return RDX_EUNSUPPORTED;
   SConvArgs a;
   a.x = (const __hip_bfloat16*)dy;
   a.w = (const __hip_bfloat16*)w;
@@ -564,6 +564,7 @@ extern "C" int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void*
   a.ph = ph;
   a.Ho = H + 2 * ph - kh + 1;
   RDX_REQUIRE(a.Ho > 0);
+  if (ci == 64) return sconv_fwd_launch<64, 64, 2, true>(a, as_stream(stream));
   return sconv_fwd_launch<32, 32, 2, true>(a, as_stream(stream));
 }
 

@@ -762,14 +762,14 @@ class SConvBnSelu(torch.autograd.Function):
 
 def _conv2_grad_to_c(da, out1, c, wd2, w2_shape, bn5, f32):
     """From conv2's output gradient da back to conv1's pre-activation c: dc (bf16, c's shape), the frozen
-    BN / conv1-bias sums [3][C] (d conv_bias, d gamma, d beta) and dw2. The 32-channel blocks run conv2's input
-    gradient and the BN + SELU backward as ONE kernel (rdx_sconv_dgrad_bnselu: dO1 stays on chip); otherwise
-    the input gradient and rdx_bnselu_bwd run one after the other."""
+    BN / conv1-bias sums [3][C] (d conv_bias, d gamma, d beta) and dw2. The 32- and 64-channel blocks run conv2's
+    input gradient and the BN + SELU backward as ONE kernel (rdx_sconv_dgrad_bnselu: dO1 stays on chip);
+    otherwise the input gradient and rdx_bnselu_bwd run one after the other."""
     co2, ci2, kh2, _ = w2_shape
     N, C, Ho, W = c.shape
     dc = torch.empty_like(c)
     sums = torch.zeros(3, C, device=c.device, dtype=torch.float32)
-    if ci2 == 32 and co2 == 32 and kh2 == 2 and os.environ.get("RADHIP_FUSED_DGRAD_BN", "1") != "0":
+    if ci2 == co2 and ci2 in (32, 64) and kh2 == 2 and os.environ.get("RADHIP_FUSED_DGRAD_BN", "1") != "0":
         H = da.shape[2]
         nbytes = 2.0 * (N * H * W * co2 + 2 * N * Ho * W * C)
         with _timed("sconv_dgrad_bnselu", da, nbytes, shape=(N, H, W)):

@@ -86,10 +86,10 @@ def _bn_params(tag, co):
     return cb, mean, invstd, gamma, beta
 
 
-@pytest.mark.parametrize("ci,co,W", [(32, 32, 300), (32, 32, 7163), (32, 64, 257), (64, 64, 129)])
+@pytest.mark.parametrize("ci,co,W", [(32, 32, 300), (32, 32, 7163), (32, 64, 257), (32, 64, 2387), (64, 64, 129)])
 def test_sconv_pair_matches_unfused_ops(ci, co, W):
     """conv1 -> BN -> SELU -> conv2 as one op (SConvBnSeluSConv; its backward fuses conv2's input gradient with
-    the BN + SELU backward for 32 channels) against SConvBnSelu followed by SConv (separate kernels): the same
+    the BN + SELU backward for 32 and 64 channels) against SConvBnSelu followed by SConv (separate kernels): the same
     forward bits; gradients equal up to the summation order of the fp32 channel sums."""
     from radhip.ops import SConv, SConvBnSelu, SConvBnSeluSConv
     N, H = 2, 23
