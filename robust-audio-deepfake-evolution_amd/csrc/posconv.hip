@@ -126,15 +126,151 @@ __global__ __launch_bounds__(256) void posconv_kernel(const __hip_bfloat16* __re
   }
 }
 
+// T <= 256: one workgroup per (b, g) covers every row, each wave 64 rows (two M tiles) x 64 outputs, so a tap's B
+// fragments feed 16 MFMAs instead of 8. The tap's 64 x 64 weights (8 KB) are staged once per workgroup in a
+// double-buffered LDS image (144-byte rows, conflict-free like the input window) from global loads issued two
+// taps ahead, one barrier per tap, instead of every wave reading them from L2: a quarter of the weight traffic.
+// Same arithmetic per output as posconv_kernel (the same taps and K order into the same fp32 accumulators).
+constexpr int PC2_ROWS = 256;
+constexpr int PC2_WIN = PC2_ROWS + PC_K - 1;
+constexpr int PC2_WIMG = PC_C * PC_LDW;   // one tap's weight image (bf16 elements)
+constexpr int PC2_LDS = (PC2_WIN * PC_LDW + 2 * PC2_WIMG) * 2;
+template <bool kBwd>
+__global__ __launch_bounds__(256, 2) void posconv2_kernel(const __hip_bfloat16* __restrict__ in,
+                                                          const __hip_bfloat16* __restrict__ usave,
+                                                          const __hip_bfloat16* __restrict__ wk,
+                                                          const float* __restrict__ bias,
+                                                          __hip_bfloat16* __restrict__ out,
+                                                          __hip_bfloat16* __restrict__ uout, int T, int off) {
+  extern __shared__ __attribute__((aligned(16))) char pc2_lds[];
+  __bf16 (*win)[PC_LDW] = reinterpret_cast<__bf16 (*)[PC_LDW]>(pc2_lds);
+  __bf16* wimg = reinterpret_cast<__bf16*>(pc2_lds) + PC2_WIN * PC_LDW;   // [2][64 n][PC_LDW]
+  const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int64_t base = (int64_t)b * T * PC_E + g * PC_C;
+  const __hip_bfloat16* wg = wk + (int64_t)g * PC_K * PC_C * PC_C;
+  // tap k's [64 n][64 c] slice: 512 16-byte chunks, chunks tid and tid + 256 of this thread
+  const int wn0 = tid >> 3, wc0 = (tid & 7) * 8;   // chunk tid + 256: row wn0 + 32
+  auto wload = [&](int k, int j) -> uint4 {
+    return *reinterpret_cast<const uint4*>(wg + ((int64_t)k * PC_C + wn0 + 32 * j) * PC_C + wc0);
+  };
+  auto wstore = [&](int buf, uint4 v0, uint4 v1) {
+    *reinterpret_cast<uint4*>(wimg + buf * PC2_WIMG + wn0 * PC_LDW + wc0) = v0;
+    *reinterpret_cast<uint4*>(wimg + buf * PC2_WIMG + (wn0 + 32) * PC_LDW + wc0) = v1;
+  };
+  uint4 va0 = wload(0, 0), va1 = wload(0, 1), vb0 = wload(1, 0), vb1 = wload(1, 1);
+  for (int i = tid; i < PC2_WIN * (PC_C / 8); i += 256) {
+    const int wr = i >> 3, c8 = (i & 7) * 8;
+    const int tr = wr - off;
+    pc_bf16x8 v;
+    if (tr >= 0 && tr < T) {
+      const int64_t o = base + (int64_t)tr * PC_E + c8;
+      if (kBwd) {
+        const pc_bf16x8 d = *reinterpret_cast<const pc_bf16x8*>(in + o);
+        const pc_bf16x8 u = *reinterpret_cast<const pc_bf16x8*>(usave + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)d[j] * pc_gelu_d((float)u[j]));
+      } else {
+        v = *reinterpret_cast<const pc_bf16x8*>(in + o);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+    }
+    *reinterpret_cast<pc_bf16x8*>(&win[wr][c8]) = v;
+  }
+  wstore(0, va0, va1);
+  __syncthreads();
+  const int w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int r0 = 64 * w;
+  const bool one = r0 < T, two = r0 + 32 < T;   // the wave's M tiles holding rows below T (wave-uniform)
+  pc_f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
+  // tap kk from image buf: the B fragments [nt * 4 + s] = W[kk][nt * 32 + r][16 s + 8 hh .. + 7]
+  auto tap = [&](int kk, int buf) {
+    pc_bf16x8 bf[8];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        bf[nt * 4 + s2] =
+            *reinterpret_cast<const pc_bf16x8*>(wimg + buf * PC2_WIMG + (nt * 32 + r) * PC_LDW + 16 * s2 + 8 * hh);
+    if (one) pc_tap(acc[0], &win[r0 + r + kk][8 * hh], bf);
+    if (two) pc_tap(acc[1], &win[r0 + 32 + r + kk][8 * hh], bf);
+  };
+  static_assert(PC_K % 2 == 0, "taps in pairs");
+  for (int k = 0; k < PC_K; k += 2) {
+    // image 0 holds tap k, vb tap k + 1; va takes tap k + 2 (the last taps re-load tap K - 1: no conditional load)
+    va0 = wload(min(k + 2, PC_K - 1), 0);
+    va1 = wload(min(k + 2, PC_K - 1), 1);
+    tap(k, 0);
+    wstore(1, vb0, vb1);
+    __syncthreads();
+    vb0 = wload(min(k + 3, PC_K - 1), 0);
+    vb1 = wload(min(k + 3, PC_K - 1), 1);
+    tap(k + 1, 1);
+    wstore(0, va0, va1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    if (!(mt == 0 ? one : two)) continue;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int n = nt * 32 + r;
+      const float bs = kBwd ? 0.f : bias[g * PC_C + n];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int t = r0 + 32 * mt + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        if (t < T) {
+          const int64_t o = base + (int64_t)t * PC_E + n;
+          if (kBwd) {
+            out[o] = __float2bfloat16(acc[mt][nt][i]);
+          } else {
+            const __hip_bfloat16 ub = __float2bfloat16(acc[mt][nt][i] + bs);
+            uout[o] = ub;
+            out[o] = __float2bfloat16(pc_gelu(__bfloat162float(ub)));
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace rdx
 
 using namespace rdx;
+
+static int pc2_launch(bool bwd, const void* in, const void* u, const void* wk, const float* bias, void* out,
+                      void* uout, int B, int T, int off, hipStream_t st) {
+  constexpr int smem = PC2_LDS;
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {reinterpret_cast<const void*>(&posconv2_kernel<false>),
+                          reinterpret_cast<const void*>(&posconv2_kernel<true>)}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+      if (e != hipSuccess) return (int)e;
+    }
+    attr = true;
+  }
+  dim3 grid(PC_G, B);
+  if (bwd)
+    hipLaunchKernelGGL(posconv2_kernel<true>, grid, dim3(256), smem, st, (const __hip_bfloat16*)in,
+                       (const __hip_bfloat16*)u, (const __hip_bfloat16*)wk, nullptr, (__hip_bfloat16*)out, nullptr, T,
+                       off);
+  else
+    hipLaunchKernelGGL(posconv2_kernel<false>, grid, dim3(256), smem, st, (const __hip_bfloat16*)in, nullptr,
+                       (const __hip_bfloat16*)wk, bias, (__hip_bfloat16*)out, (__hip_bfloat16*)uout, T, off);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
 
 static bool pc_ok(const void* p) { return p && ((uintptr_t)p & 15) == 0; }
 
 extern "C" int rdx_posconv_fwd(const void* h, const void* wk, const float* bias, void* y, void* u, int B, int T,
                                void* stream) {
   RDX_REQUIRE(pc_ok(h) && pc_ok(wk) && bias && pc_ok(y) && pc_ok(u) && B > 0 && T > 0 && B <= 65535);
+  if (T <= PC2_ROWS) return pc2_launch(false, h, nullptr, wk, bias, y, u, B, T, PC_K / 2, as_stream(stream));
   dim3 grid((T + PC_ROWS - 1) / PC_ROWS, PC_G, B);
   hipLaunchKernelGGL(posconv_kernel<false>, grid, dim3(256), 0, as_stream(stream), (const __hip_bfloat16*)h, nullptr,
                      (const __hip_bfloat16*)wk, bias, (__hip_bfloat16*)y, (__hip_bfloat16*)u, T, PC_K / 2);
@@ -144,6 +280,7 @@ extern "C" int rdx_posconv_fwd(const void* h, const void* wk, const float* bias,
 
 extern "C" int rdx_posconv_bwd(const void* dy, const void* u, const void* wkt, void* dh, int B, int T, void* stream) {
   RDX_REQUIRE(pc_ok(dy) && pc_ok(u) && pc_ok(wkt) && pc_ok(dh) && B > 0 && T > 0 && B <= 65535);
+  if (T <= PC2_ROWS) return pc2_launch(true, dy, u, wkt, nullptr, dh, nullptr, B, T, PC_K / 2 - 1, as_stream(stream));
   dim3 grid((T + PC_ROWS - 1) / PC_ROWS, PC_G, B);
   hipLaunchKernelGGL(posconv_kernel<true>, grid, dim3(256), 0, as_stream(stream), (const __hip_bfloat16*)dy,
                      (const __hip_bfloat16*)u, (const __hip_bfloat16*)wkt, nullptr, (__hip_bfloat16*)dh, nullptr, T,

@@ -414,14 +414,16 @@ def test_gated_attention_ragged_lengths(B, T, H):
 
 def test_posconv_matches_torch():
     """WavLM positional conv (grouped conv1d 16 x 64 channels, 128 taps, padding 64, last frame dropped,
-    GELU; csrc/posconv.hip) vs torch fp32 on the same bf16 operands: output and input gradient."""
+    GELU; csrc/posconv.hip) vs torch fp32 on the same bf16 operands: output and input gradient. T <= 256 takes
+    the one-workgroup-per-(b, g) kernel (256 = every wave with two row tiles, 193 = the last wave with one), longer
+    sequences the row-block kernel (300)."""
     from radhip.ops import PosConv, posconv_weights
     torch.manual_seed(0)
     w = torch.randn(1024, 64, 128, device=DEV) * 0.01
     bias = torch.randn(1024, device=DEV) * 0.1
     wk, wkt = posconv_weights(w)
     wr = w.to(torch.bfloat16).float()
-    for B, T in ((2, 201), (1, 37), (1, 129)):
+    for B, T in ((2, 201), (1, 37), (1, 129), (1, 256), (1, 193), (1, 300)):
         h = torch.randn(B, T, 1024, device=DEV).to(torch.bfloat16).requires_grad_()
         y = PosConv.apply(h, wk, wkt, bias)
         go = torch.randn(B, T, 1024, device=DEV).to(torch.bfloat16)
