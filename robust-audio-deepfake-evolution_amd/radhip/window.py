@@ -396,14 +396,24 @@ class WindowStep:
             if self.adv:
                 # the captured attack perturbs feature_projection in place: keep the real values to put back
                 fp_saved = [p.detach().clone() for p in self.fp_real]
-                for k in range(self.K):
+                if chain and os.environ.get("RADHIP_ADV_GRAPHS", "one") == "one":
+                    # the K chain links back to back in ONE graph: every graph replay starts with the device
+                    # waiting on the host's submission of its first nodes (≈80-100 µs per kernel for the first
+                    # layer's launches in the rocprofv3 trace), once per window instead of once per link
                     g = new_graph()
                     with torch.cuda.graph(g):
-                        if chain:
+                        for k in range(self.K):
                             self._adv_step(k)
-                        else:
-                            self._adv_pass(k)
                     gadv.append(g)
+                else:
+                    for k in range(self.K):
+                        g = new_graph()
+                        with torch.cuda.graph(g):
+                            if chain:
+                                self._adv_step(k)
+                            else:
+                                self._adv_pass(k)
+                        gadv.append(g)
                 with torch.no_grad():
                     for p, v in zip(self.fp_real, fp_saved):
                         p.copy_(v)
