@@ -194,8 +194,9 @@ class Runner:
         ds = ds_cls(keys, base_dir)
         bs = int(self.config.get("test_config", {}).get("batch_size", self.config["batch_size"]))
         feeder = EvalFeeder(ds, bs, threads=self.threads, zero_on_error=zero_on_error)
+        eval_amp = None if self.args.eval_amp == "fp32" else AMP[self.args.eval_amp]
         produce_evaluation_file_sharded(ds, model, self.device, save_path, trial_path, batch_size=bs,
-                                        criterion=self.criterion, batches=feeder.batches, fmt=fmt)
+                                        criterion=self.criterion, batches=feeder.batches, fmt=fmt, amp=eval_amp)
         self.barrier()
 
     def tdcf(self, score_file, output_file, printout=True):
@@ -515,6 +516,10 @@ def parse_args(argv=None):
     parser.add_argument("--pretrained_weights", type=str, default=None, help="pretrained weights for fine-tuning")
     parser.add_argument("--model", type=str, default=None, help="override the model architecture")
     parser.add_argument("--amp", default="bf16", choices=sorted(AMP), help="autocast dtype (reference: fp16)")
+    parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "bf16"],
+                        help="scoring precision: fp32 as the reference scores (default), or bf16 autocast, which runs "
+                             "the hand-written HIP encoder / SincNet path (tools/bench_eval.py: throughput and score "
+                             "deviation)")
     parser.add_argument("--eager", action="store_true", help="launch kernel by kernel (no HIP graphs)")
     parser.add_argument("--no-window", dest="no_window", action="store_true",
                         help="replay one graph pair per micro-batch instead of the batched accumulation window")

@@ -13,14 +13,20 @@ contiguous shard of the trial list; the fp32 scores are all-gathered; rank 0 wri
 protocol order. The bytes match the single-process file, because the scores are per-utterance and
 the order is fixed by the protocol.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
 
-def _scores(model, batch_x, criterion=None):
-    feats, out = model(batch_x)
+def _scores(model, batch_x, criterion=None, amp=None):
+    """amp: None (fp32, the reference's eval) or a dtype to autocast the forward to (bf16: the fused HIP path)."""
+    ctx = torch.autocast("cuda", dtype=amp) if amp is not None and batch_x.is_cuda else contextlib.nullcontext()
+    with ctx:
+        feats, out = model(batch_x)
+    feats, out = feats.float(), out.float()
     if criterion is not None and hasattr(criterion, "center"):
         w = F.normalize(criterion.center, p=2, dim=1)
         return F.normalize(feats, p=2, dim=1).mm(w.t()).view(-1)
@@ -91,7 +97,7 @@ def _item_batches(dataset, batch_size):
 
 @torch.no_grad()
 def produce_evaluation_file_sharded(dataset, model, device, save_path, trial_path, batch_size=32,
-                                    criterion=None, group=None, batches=None, fmt="2019"):
+                                    criterion=None, group=None, batches=None, fmt="2019", amp=None):
     """dataset[i] -> (x [64600], utt_id) in protocol order. Every rank calls this; rank 0 writes.
     `batches(lo, hi, device)` (e.g. data.EvalFeeder.batches: native decode + GPU pad) replaces the
     item-wise path when given. fmt "2019": "utt src key score" checked against the 5-column trial
@@ -104,7 +110,7 @@ def produce_evaluation_file_sharded(dataset, model, device, save_path, trial_pat
     batches = batches or _item_batches(dataset, batch_size)
     local = []
     for xb, _ in batches(lo, hi, device):
-        local.append(_scores(model, xb, criterion).float())
+        local.append(_scores(model, xb, criterion, amp).float())
     local = torch.cat(local) if local else torch.zeros(0, device=device)
     if world > 1:
         width = shard_bounds(n, world, 0)[1]

@@ -3,6 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${TAG:-abn}
+[ -n "$VARIANTS_FILE" ] && VARIANTS=$(cat $VARIANTS_FILE)
 mkdir -p gpurun_out/$TAG
 if [ -n "$TESTS" ]; then
   timeout -k 10 ${TTIME:-900} python -u -m pytest ${TESTS} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1; rc=$?
