@@ -503,6 +503,11 @@ int rdx_fe_ln_gelu(void* io, int64_t rows, const float* gamma, const float* beta
  * ------------------------------------------------------------------------------------------ */
 int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, const float* bn, int N, int H, int W, int ci,
                   int co, int kh, int ph, void* stream);
+/* rdx_sconv_fwd with a residual added in the epilogue: y = bf16(bf16(conv(x, w)) + res), res bf16 [N, Ho, W, co]
+ * NHWC (16-byte aligned). A residual block's input gradient in one pass: conv1's input gradient plus the identity
+ * branch's gradient, the bits autograd's add would produce (radhip.ops.ResBlockIdentity). */
+int rdx_sconv_fwd_res(const void* x, const void* w, void* y, const void* res, int N, int H, int W, int ci, int co,
+                      int kh, int ph, void* stream);
 /* conv2's input gradient continued through conv1's frozen BN + SELU backward (Residual_block.forward,
  * src/models/DualStreamSEMamba.py:182-200; replaces rdx_sconv_fwd on dY followed by rdx_bnselu_bwd): the
  * 32-channel blocks (ci = co = 32, kh = 2). dO1 = conv(dy, w) (w: conv2's flipped, transposed kernel

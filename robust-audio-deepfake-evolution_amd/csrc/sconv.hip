@@ -63,6 +63,7 @@ struct SConvArgs {
                             //   backward epilogue reads a fifth row, invstd
   const __hip_bfloat16* c;  // backward epilogue: the saved pre-activation [N, Ho, W, CO]
   float* sums;              // backward epilogue: [3][CO] d conv_bias | d gamma | d beta (fp32 atomics)
+  const __hip_bfloat16* res;  // optional [N, Ho, W, CO]: y = bf16(bf16(conv) + res) (a residual branch's gradient)
   int N, H, W, Ho, ph;
   int rows_per;             // output rows per workgroup (grid.z chunks of the Ho rows)
 };
@@ -163,6 +164,17 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
           for (int g = 0; g < 4; ++g) cpre[t][g] = *reinterpret_cast<const uint2*>(cpre_src + obase + t * 32 + 8 * g + 4 * h);
       }
     }
+    // residual epilogue: this row's residual, loaded before the MFMAs as the saved pre-activations are
+    uint2 rres[kBnBwd ? 1 : NT][4];
+    if constexpr (!kBnBwd) {
+      if (a.res && p < a.W) {
+        const int64_t obase = (((int64_t)n * a.Ho + ho) * a.W + p) * CO;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) rres[t][g] = *reinterpret_cast<const uint2*>(a.res + obase + t * 32 + 8 * g + 4 * h);
+      }
+    }
     sf32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -222,6 +234,13 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
             }
             *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(dz[0], dz[1]), sc_pack2(dz[2], dz[3]));
             continue;
+          }
+          if (a.res) {   // the sum autograd would form: the bf16 convolution output plus the residual gradient
+            const uint2 rr = rres[kBnBwd ? 0 : t][g];
+            v[0] = sc_bf16(v[0]) + __uint_as_float(rr.x << 16);
+            v[1] = sc_bf16(v[1]) + __uint_as_float(rr.x & 0xffff0000u);
+            v[2] = sc_bf16(v[2]) + __uint_as_float(rr.y << 16);
+            v[3] = sc_bf16(v[3]) + __uint_as_float(rr.y & 0xffff0000u);
           }
           *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]));
           if (a.y2) {
@@ -529,6 +548,34 @@ extern "C" int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, co
   a.bn = bn;
   a.c = nullptr;
   a.sums = nullptr;
+  a.res = nullptr;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.ph = ph;
+  a.Ho = H + 2 * ph - kh + 1;
+  RDX_REQUIRE(a.Ho > 0 && N <= 65535);
+  hipStream_t st = as_stream(stream);
+  SC_DISPATCH(sconv_fwd_launch, a, st)
+}
+
+// The same convolution with a residual added in the epilogue: y = bf16(bf16(conv(x, w)) + res), res [N, Ho, W, co]
+// bf16 — a residual block's input gradient, conv1's input gradient plus the identity branch's, in one pass
+// (autograd's separate add reads both and writes the sum: the same bits, one full-size round trip less).
+extern "C" int rdx_sconv_fwd_res(const void* x, const void* w, void* y, const void* res, int N, int H, int W, int ci,
+                                 int co, int kh, int ph, void* stream) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  RDX_REQUIRE(x && w && y && res && N > 0 && H > 0 && W > 0 && (kh == 1 || kh == 2) && ph >= 0 && ph <= kh);
+  RDX_REQUIRE(al(x) && al(w) && al(y) && al(res));
+  SConvArgs a;
+  a.x = (const __hip_bfloat16*)x;
+  a.w = (const __hip_bfloat16*)w;
+  a.y = (__hip_bfloat16*)y;
+  a.y2 = nullptr;
+  a.bn = nullptr;
+  a.c = nullptr;
+  a.sums = nullptr;
+  a.res = (const __hip_bfloat16*)res;
   a.N = N;
   a.H = H;
   a.W = W;
@@ -558,6 +605,7 @@ extern "C" int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void*
   a.bn = bn;
   a.c = (const __hip_bfloat16*)c;
   a.sums = sums;
+  a.res = nullptr;
   a.N = N;
   a.H = H;
   a.W = W;

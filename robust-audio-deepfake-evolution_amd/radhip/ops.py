@@ -676,15 +676,23 @@ def _sconv_w_prep(weight):
     return wf, wd
 
 
-def _sconv_run(x, w_tap, ci, co, kh, ph, y2=None, bn=None):
+def _sconv_run(x, w_tap, ci, co, kh, ph, y2=None, bn=None, res=None):
+    """res: a bf16 [N, co, Ho, W] channels_last tensor added in the epilogue (y = bf16(bf16(conv) + res))."""
     N, _, H, W = x.shape
     Ho = H + 2 * ph - kh + 1
     y = torch.empty(N, co, Ho, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
     # algorithmic HBM bytes (the convolution is HBM-bound: ~100 FLOP per byte at these channel counts)
-    nbytes = 2.0 * (N * H * W * ci + N * Ho * W * co * (2 if y2 is not None else 1))
+    nbytes = 2.0 * (N * H * W * ci + N * Ho * W * co * (2 if (y2 is not None or res is not None) else 1))
     with _timed("sconv_fwd", x, nbytes, shape=(N, H, W, ci, co, kh, ph)):
-        check(lib().rdx_sconv_fwd(_p(x), _p(w_tap), _p(y), _p(y2) if y2 is not None else None,
-                                  _p(bn) if bn is not None else None, N, H, W, ci, co, kh, ph, _stream(x)), "sconv_fwd")
+        if res is not None:
+            if res.shape != y.shape or res.dtype != torch.bfloat16 or not res.is_contiguous(memory_format=torch.channels_last):
+                raise ValueError("radhip sconv: residual must be bf16 NHWC of the output's shape")
+            check(lib().rdx_sconv_fwd_res(_p(x), _p(w_tap), _p(y), _p(res), N, H, W, ci, co, kh, ph, _stream(x)),
+                  "sconv_fwd_res")
+        else:
+            check(lib().rdx_sconv_fwd(_p(x), _p(w_tap), _p(y), _p(y2) if y2 is not None else None,
+                                      _p(bn) if bn is not None else None, N, H, W, ci, co, kh, ph, _stream(x)),
+                  "sconv_fwd")
     return y
 
 
@@ -821,6 +829,57 @@ class SConvBnSeluSConv(torch.autograd.Function):
         dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
         dx, dw1 = _sconv_backward(x, dc, wd1, s1, ph1, ctx.needs_input_grad[0])
         return dx, dw1.to(w1dt), None, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt)
+
+
+class ResBlockIdentity(torch.autograd.Function):
+    """A residual block without downsampling (SincNet blocks 1, 3-5: Residual_block.forward,
+    src/models/DualStreamSEMamba.py:182-200, frozen BN): MaxPool2d((1, 3))(conv2(selu(bn2(conv1(x) + cb))) + x + b2)
+    as one autograd op. Forward: SConvBnSeluSConv's and ResTail's kernels. Backward: ResTail's scatter, conv2's input
+    gradient with the BN + SELU backward, then the block input's gradient in ONE pass, conv1's input gradient with
+    the identity branch's gradient added in its epilogue (rdx_sconv_fwd_res): the bits autograd's separate add of
+    the two full-size gradients produces, without that read-read-write pass."""
+
+    @staticmethod
+    def forward(ctx, x, w1, conv_bias, mean, invstd, gamma, beta, w2, b2):
+        _require_gpu(x)
+        x_dtype = x.dtype
+        x = _nhwc(x.to(torch.bfloat16))
+        co, ci, kh, _ = w1.shape
+        wf1, wd1 = _sconv_w(w1)
+        wf2, wd2 = _sconv_w(w2)
+        f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
+        N, _, H, W = x.shape
+        out1 = torch.empty(N, co, H + 1, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        c = _sconv_run(x, wf1, ci, co, kh, 1, y2=out1, bn=bn5[:4])
+        co2, ci2, kh2, _ = w2.shape
+        a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
+        if a.shape != x.shape:
+            raise ValueError(f"radhip: residual shapes differ {tuple(a.shape)} vs {tuple(x.shape)}")
+        y = torch.empty(N, co2, H, W // 3, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        arg = torch.empty(N, co2, H, W // 3, device=x.device, dtype=torch.uint8, memory_format=torch.channels_last)
+        bf = b2.detach().contiguous().float()
+        check(lib().rdx_res_tail_fwd(_dtype_code(a), _p(a), _p(x), _p(bf), _p(y), _p(arg), N * H, W, co2, _stream(a)),
+              "res_tail_fwd")
+        ctx.save_for_backward(x, wd1, c, out1, wd2, bn5, arg, *f32)
+        ctx.meta = (tuple(w1.shape), w1.dtype, tuple(w2.shape), w2.dtype, x_dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wd1, c, out1, wd2, bn5, arg, *f32 = ctx.saved_tensors
+        s1, w1dt, s2, w2dt, x_dtype = ctx.meta
+        N, C, H, W = x.shape
+        dy = _nhwc(dy.to(torch.bfloat16))
+        ds = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        dbias = torch.zeros(C, device=dy.device, dtype=torch.float32)
+        check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(ds), _p(dbias), N * H, W, C, _stream(dy)),
+              "res_tail_bwd")
+        dc, sums, dw2 = _conv2_grad_to_c(ds, out1, c, wd2, s2, bn5, f32)
+        co, ci, kh, _ = s1
+        dx = _sconv_run(dc, wd1, co, ci, kh, kh - 1 - 1, res=ds) if ctx.needs_input_grad[0] else None
+        _, dw1 = _sconv_backward(x, dc, wd1, s1, 1, False)
+        return (dx.to(x_dtype) if dx is not None else None, dw1.to(w1dt), sums[0], None, None, sums[1], sums[2],
+                dw2.to(w2dt), dbias)
 
 
 class BnSeluSConv(torch.autograd.Function):

@@ -12,7 +12,7 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import (Block0Convs, Block0Front, Block0Fused, BnSelu, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
+from .ops import (Block0Convs, Block0Front, Block0Fused, BnSelu, ResBlockIdentity, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
                   sconv_weight_ok, sincconv_absmaxpool)
 
 
@@ -153,6 +153,10 @@ class Residual_block(nn.Module):
                     else:
                         out = BnSelu.apply(c, *bnp)
             elif bf and sconv_ok(x, self.conv1.weight):
+                if pair and not self.downsample and os.environ.get("RADHIP_RES_FUSED", "1") != "0":
+                    # the whole block as one autograd op: the block input's gradient in one pass
+                    # (conv1's input gradient + the identity branch's, radhip.ops.ResBlockIdentity)
+                    return ResBlockIdentity.apply(x, self.conv1.weight, *bnp, w2, self.conv2.bias)
                 if pair:
                     a = SConvBnSeluSConv.apply(x, self.conv1.weight, 1, *bnp, w2)
                 else:

@@ -141,3 +141,50 @@ def test_bnselu_sconv_block0_matches_unfused():
     assert torch.equal(gg[0], rg[0])           # dc: the same arithmetic on the same bf16 dO1
     for g, r, nm in zip(gg[1:], rg[1:], ("dw2", "dcb", "dgamma", "dbeta")):
         _close(g, r, 2e-3, nm)
+
+
+@pytest.mark.parametrize("C,W", [(32, 7163), (64, 795), (32, 301)])
+def test_res_block_identity_matches_autograd_sum(C, W, monkeypatch):
+    """A non-downsampling Residual_block as one op (radhip.ops.ResBlockIdentity: the block input's gradient = conv1's
+    input gradient + the identity branch's, added in the input-gradient kernel's epilogue) against the same block
+    with autograd summing the two branches (RADHIP_RES_FUSED=0): the same kernels and the same bf16 add, so the
+    output, the input gradient and the weight gradients are bit-identical (the bias / BN channel sums come from fp32
+    atomics in both paths: equal to their summation order)."""
+    from radhip.sinc import Residual_block
+    torch.manual_seed(C + W)
+    blk = Residual_block([C, C]).cuda()
+    with torch.no_grad():
+        blk.bn2.running_mean.normal_(0, 0.2)
+        blk.bn2.running_var.uniform_(0.5, 2.0)
+        blk.bn2.weight.normal_(1, 0.2)
+        blk.bn2.bias.normal_(0, 0.2)
+        blk.conv2.bias.normal_(0, 0.1)
+    blk.eval()
+    N, H = 2, 23
+    x0 = _t(f"rb.x{C}{W}", (N, C, H, W), 1.0).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = None
+
+    def run(fused):
+        nonlocal dy
+        monkeypatch.setenv("RADHIP_RES_FUSED", "1" if fused else "0")
+        for p in blk.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = blk(x)
+        if dy is None:
+            dy = _t(f"rb.dy{C}{W}", tuple(y.shape), 1.0).to(y.dtype).contiguous(memory_format=torch.channels_last)
+        y.backward(dy)
+        return y.detach(), x.grad.detach().clone(), {n: p.grad.clone() for n, p in blk.named_parameters()
+                                                     if p.grad is not None}
+
+    y0, dx0, g0 = run(False)
+    y1, dx1, g1 = run(True)
+    assert torch.equal(y1, y0)
+    assert torch.equal(dx1, dx0)
+    assert g1.keys() == g0.keys()
+    for k in g0:
+        if k in ("conv1.bias", "bn2.weight", "bn2.bias", "conv2.bias"):   # fp32 atomic channel sums: their order
+            _close(g1[k], g0[k], 1e-5, k)
+        else:
+            assert torch.equal(g1[k], g0[k]), k
