@@ -171,6 +171,25 @@ def roofline_from_rows(rows, steps, graphed=False, split=False):
     return roof, rows
 
 
+def shape_table(shape_rows, kernel, steps):
+    """Per-shape rows of `kernel` (keys "name[M, N, K]" for the GEMMs): launches and ms per step, µs per launch,
+    work per launch and the achieved rate against its peak."""
+    if not kernel:
+        return None
+    bound, kind = KERNEL_BOUND.get(kernel, ("hbm", None))
+    out = {}
+    for k, r in shape_rows.items():
+        if not k.startswith(kernel + "["):
+            continue
+        rate = r["avg_work"] / (r["avg_ms"] * 1e-3) / (1e12 if bound == "mfma" else 1e9)
+        peak = PEAKS[kind] if bound == "mfma" else PEAKS["hbm"]
+        out[k[len(kernel):]] = {"launches_per_step": round(r["launches"] / steps, 2),
+                                "ms_per_step": round(r["total_ms"] / steps, 4), "us_per_launch": round(1e3 * r["avg_ms"], 2),
+                                "work_per_launch": r["avg_work"], "achieved": round(rate, 1),
+                                "frac": round(rate / peak, 4)}
+    return out or None
+
+
 def host_cpu():
     """(CPU model, physical cores of the machine, logical CPUs this process may run on)."""
     model, cores = None, set()
@@ -457,6 +476,7 @@ def main():
         cur["window"] = window
     timing, ops.TIMING = ops.TIMING, None
     rows = ops.event_rows(timing)            # eager launches (augmentation, FGM)
+    shape_rows = graph_timer.rows(by_shape=True) if graph_timer is not None else {}
     if graph_timer is not None:              # launches inside the replayed graphs
         for k, r in graph_timer.rows().items():
             if k in rows:
@@ -492,6 +512,8 @@ def main():
             "step_mfma_frac": round(value / ws * TRAIN_FLOP_PER_UTT / 2.5e15, 4),
             "kernels": {k: {kk: round(vv, 5) if isinstance(vv, float) else vv for kk, vv in v.items()}
                         for k, v in rows.items()},
+            # the dominant kernel per (kernel, shape): every shape sampled in every graph (GraphTimer keys)
+            "kernel_shapes": shape_table(shape_rows, roof["kernel"] if roof else None, args.steps),
             "final_loss": round(loss, 6),
         }
         if ws == 1 and not args.no_cpu_baseline:

@@ -447,6 +447,24 @@ int rdx_wgemm_bf16_ex(const void* A, int64_t lda, const void* B, int64_t ldb, vo
 int64_t rdx_wgemm_ws_bytes(int M, int N, int tile, int splits);
 int64_t rdx_wgemm_counters(int M, int N, int tile);
 
+/* ---- Deep-pipelined bf16 MFMA GEMM of the WavLM encoder projections (csrc/pgemm.hip) ------------------------
+ * Same operands, layouts and epilogues as rdx_wgemm_bf16 (K % 64 == 0; the q/k/v, out_proj, FFN1, FFN2 GEMMs and
+ * their input gradients of HF WavLMEncoderLayerStableLayerNorm, src/models/DualStreamSEMamba.py:292-439), on
+ * one 512-thread workgroup per output tile: 8 waves, an NST-deep LDS-DMA ring kept in flight across the one
+ * barrier per K step, fragment reads one phase ahead of the MFMAs. tile codes (csrc/pgemm.hip pg::geometry):
+ * 0 / 8 / 9 = 256 x 256, 1 / 6 = 256 x 128, 2 / 5 = 128 x 256, 3 / 7 = 128 x 128, 4 = 128 x 192 output tiles
+ * (0-3, 8, 9: 32-deep K steps, 4-8 stage rings; 4-7: 64-deep, 3-4 stages); + 100 raises the wave priority around the MFMA clusters. group_m: tiles are dealt to XCDs in
+ * contiguous runs and ordered group_m row tiles x every column tile (0 = all row tiles: column-panel order). */
+int rdx_pgemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                   const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao,
+                   int tile, int group_m, void* stream);
+/* Diagnostic form (bias epilogue, tiles 0 / 2 / 4; + 10 = without refills in the K loop, + 20 = without MFMA;
+ * group_m -1 puts every workgroup on tile (0, 0)): also stores 8 words per workgroup into prof [grid][8]: shader-clock
+ * stamps at entry / stage 0 landed / main loop done / exit, 100 MHz real-time stamps at entry / exit, the
+ * (XCC id << 32 | HW_ID) word and (row tile << 32 | column tile). */
+int rdx_pgemm_prof(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                   const void* bias, int tile, int group_m, void* prof, void* stream);
+
 /* ---- Weight / bias gradients of the head's linears, accumulated in fp32 (csrc/wgrad.hip) ----------------
  * dW[n][k] += sum_m dY[m][n] X[m][k], db[n] += sum_m dY[m][n] (db may be NULL): bf16 dY [M, ldy] and X [M, ldx],
  * fp32 dW [N, ldw] (the flat gradient buffer's views), the token rows split over the chip in chunks of

@@ -111,6 +111,10 @@ SIGNATURES = {
     "rdx_wgrad_ws_floats": (c_i64, [c_int, c_int, c_int]),
     "rdx_wgrad_acc": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rdx_wgemm_counters": (c_i64, [c_int, c_int, c_int]),
+    "rdx_pgemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
+                               c_vp, c_i64, c_int, c_int, c_vp]),
+    "rdx_pgemm_prof": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp,
+                               c_vp]),
     "rdx_gemm_bf16_strided": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                                       c_vp, c_vp]),
     "rdx_fe_conv0": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_int, c_int, c_vp, c_vp]),

@@ -51,26 +51,28 @@ class GraphTimer:
         grp["sampled"] += 1
         if len(self.sites) >= self.acc.shape[0]:
             raise RuntimeError("GraphTimer: out of slots")
-        self.sites.append((name, float(work), grp))
+        self.sites.append((name, float(work), grp, shape))
         return self.acc[len(self.sites) - 1]
 
     def reset(self):
         self.acc.zero_()
 
-    def rows(self):
+    def rows(self, by_shape=False):
         """{name: {launches, total_ms, avg_ms, avg_work, sampled_launches}} over everything replayed since
-        reset(): launches / total_ms count every launch site of the graphs (sampled sites scaled)."""
+        reset(): launches / total_ms count every launch site of the graphs (sampled sites scaled). by_shape:
+        keyed "name[shape]" for the sites that carry a shape key (one row per (kernel, shape))."""
         khz = lib().rdx_wallclock_khz(self.device.index or 0)
         if khz <= 0:
             raise RuntimeError("rdx_wallclock_khz failed")
         acc = self.acc.cpu().numpy()
         out = {}
-        for i, (name, work, grp) in enumerate(self.sites):
+        for i, (name, work, grp, shape) in enumerate(self.sites):
             ticks, cnt = int(acc[i, 0]), int(acc[i, 1])
             if cnt == 0:
                 continue
             mult = grp["total"] / grp["sampled"]
-            r = out.setdefault(name, {"launches": 0.0, "total_ms": 0.0, "work_sum": 0.0, "sampled_launches": 0})
+            key = name if not by_shape or shape is None else f"{name}{list(shape)}"
+            r = out.setdefault(key, {"launches": 0.0, "total_ms": 0.0, "work_sum": 0.0, "sampled_launches": 0})
             r["launches"] += cnt * mult
             r["total_ms"] += ticks / khz * mult
             r["work_sum"] += work * cnt * mult
@@ -1248,7 +1250,7 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
         out = torch.empty(M, N, device=a.device, dtype=dt)
     if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
         aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
-    with _timed(name, a, gemm_flops(M, N, K)):
+    with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
         check(lib().rdx_gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
                                   _p(bias) if bias is not None else None, int(epilogue),
                                   _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
@@ -1301,7 +1303,7 @@ def wgrad_acc(dy, x, dw, db=None):
     if db is not None and (db.shape != (N,) or db.dtype != torch.float32 or not db.is_contiguous()):
         raise ValueError("radhip wgrad_acc: db must be fp32 [N]")
     ws = torch.empty(int(lib().rdx_wgrad_ws_floats(M, N, K)), device=dy.device, dtype=torch.float32)
-    with _timed("wgrad_acc", dy, gemm_flops(N, K, M)):
+    with _timed("wgrad_acc", dy, gemm_flops(N, K, M), shape=(M, N, K)):
         check(lib().rdx_wgrad_acc(_p(dy), dy.stride(0), _p(x), x.stride(0), M, N, K, _p(dw), dw.stride(0),
                                   _p(db) if db is not None else None, _p(ws), ws.numel(), _stream(dy)), "wgrad_acc")
 
@@ -1355,7 +1357,7 @@ def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
             raise ValueError(f"radhip wgemm: no split-K geometry for tile {tile}")
         ws, cnt = _wgemm_workspace(a.device, ws_bytes, n_cnt)
         ws_bytes, n_cnt = ws.numel(), cnt.numel()
-    with _timed(name, a, gemm_flops(M, N, K)):
+    with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
         check(lib().rdx_wgemm_bf16_ex(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
                                       _p(bias) if bias is not None else None, int(epilogue),
                                       _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,

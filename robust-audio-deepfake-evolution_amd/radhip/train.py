@@ -12,6 +12,7 @@ HBM; the loss is accumulated on the device (no per-micro-batch .item() sync); gr
 trainable tensors live in ONE flat fp32 buffer so a data-parallel step is one RCCL all-reduce.
 """
 import math
+import os
 import random
 
 import numpy as np
@@ -355,6 +356,23 @@ class Augmenter:
 
 
 # --------------------------------------------------------------------------- trainer ---------
+def refuse_step_tuning():
+    """PyTorch TunableOp tuning over the window's passes tries every rocBLAS solution rocBLAS accepts for the
+    head's n = 1 strided-batched GEMM (tn_201_1_144_B_32: the attention-pooling bmm in the clean pass's backward),
+    and one of them faults the GPU (gpurun_out/tune3: the fault follows the first accepted solution, 618385, in
+    the eager warm-up before any capture). Every step kind runs that backward (the window, the
+    graphed micro-step, the eager micro-step), so Trainer checks this at construction. Tune the WavLM shapes
+    offline (tools/tune_wavlm_gemms.py) and run with tuning off."""
+    tun = getattr(torch.cuda, "tunable", None)
+    env_on = (os.environ.get("PYTORCH_TUNABLEOP_ENABLED", "0") == "1"
+              and os.environ.get("PYTORCH_TUNABLEOP_TUNING", "1") == "1")
+    api_on = tun is not None and torch.cuda.is_available() and tun.is_enabled() and tun.tuning_is_enabled()
+    if env_on or api_on:
+        raise RuntimeError("TunableOp tuning is on (PYTORCH_TUNABLEOP_TUNING): tuning inside the training step runs "
+                           "rocBLAS solutions that fault on the head's n=1 batched GEMM; tune offline with "
+                           "tools/tune_wavlm_gemms.py and set PYTORCH_TUNABLEOP_TUNING=0")
+
+
 class Trainer:
     """One Phase-6 training process (one GPU). Mirrors main.py's optimizer/scheduler construction and
     train_epoch ordering."""
@@ -362,6 +380,8 @@ class Trainer:
     def __init__(self, model, config, device, total_steps, amp_dtype=torch.bfloat16, world_group=None,
                  criterion=None, param_groups=None):
         self.model, self.config, self.device = model, config, torch.device(device)
+        if self.device.type == "cuda":
+            refuse_step_tuning()
         tc = config.get("training_config", {})
         oc = config["optim_config"]
         self.accum = max(1, int(tc.get("accumulation_steps", 1)))

@@ -588,14 +588,23 @@ class PeftWrapped(nn.Module):
         return self.base_model.model(*a, **k)
 
 
+# The attention projections HF WavLMAttention hands to F.multi_head_attention_forward by their .weight / .bias
+# instead of calling them (so a peft adapter on them never runs in the reference); every other Linear is called.
+ATTN_PROJECTIONS = ("q_proj", "k_proj", "v_proj", "out_proj")
+
+
 def inject_lora(model, r=8, alpha=32, dropout=0.1, targets=("q_proj", "v_proj"), active=True):
     """Replace every nn.Linear whose attribute name is in `targets` by a LoraLinear (peft semantics:
-    base frozen by the caller, LoRA trainable). Returns the wrapped model and the adapter count."""
+    base frozen by the caller, LoRA trainable). Returns the wrapped model and the adapter count.
+    active=False (lora_mode "reference") bypasses only the adapters the reference's HF WavLM never calls: the
+    attention module's q/k/v/out projections; an adapter on any other Linear (e.g. the FFN's intermediate_dense /
+    output_dense, which HF calls as modules) stays active, as peft applies it there."""
     n = 0
     for mod in list(model.modules()):
         for name, child in list(mod.named_children()):
             if name in targets and isinstance(child, nn.Linear):
-                setattr(mod, name, LoraLinear(child, r, alpha, dropout, active=active))
+                bypassed = isinstance(mod, Attention) and name in ATTN_PROJECTIONS
+                setattr(mod, name, LoraLinear(child, r, alpha, dropout, active=active or not bypassed))
                 n += 1
     return PeftWrapped(model), n
 

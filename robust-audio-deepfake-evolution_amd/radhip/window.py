@@ -25,7 +25,7 @@ import torch
 
 from . import ops
 from .linear import direct_grad
-from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay, layerdrop_draws
+from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay, layerdrop_draws, refuse_step_tuning  # noqa: F401
 from .wavlm import compute_time_mask
 
 
@@ -35,22 +35,6 @@ def window_eligible(trainer):
     if trainer.freeze_bn:
         return True
     return not any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in trainer.model.modules())
-
-
-def refuse_step_tuning():
-    """PyTorch TunableOp tuning over the window's passes tries every rocBLAS solution rocBLAS accepts for the
-    head's n = 1 strided-batched GEMM (tn_201_1_144_B_32: the attention-pooling bmm in the clean pass's backward),
-    and one of them faults the GPU (gpurun_out/tune3: the fault follows the first accepted solution, 618385, in
-    the eager warm-up before any capture). Tune the WavLM shapes offline
-    (tools/tune_wavlm_gemms.py) and run with tuning off."""
-    tun = getattr(torch.cuda, "tunable", None)
-    env_on = (os.environ.get("PYTORCH_TUNABLEOP_ENABLED", "0") == "1"
-              and os.environ.get("PYTORCH_TUNABLEOP_TUNING", "1") == "1")
-    api_on = tun is not None and torch.cuda.is_available() and tun.is_enabled() and tun.tuning_is_enabled()
-    if env_on or api_on:
-        raise RuntimeError("TunableOp tuning is on (PYTORCH_TUNABLEOP_TUNING): tuning inside the training step runs "
-                           "rocBLAS solutions that fault on the head's n=1 batched GEMM; tune offline with "
-                           "tools/tune_wavlm_gemms.py and set PYTORCH_TUNABLEOP_TUNING=0")
 
 
 class WindowStep:

@@ -88,3 +88,32 @@ def test_product_reference_mode_leaves_adapters_out_of_the_step():
     assert float((on(x) - lin(x)).abs().max()) > 1e-4
     ids = {id(p) for p in inert_lora_params(nn.ModuleList([on, off]))}
     assert ids == {id(p) for p in list(off.lora_A.parameters()) + list(off.lora_B.parameters())}
+
+
+def test_reference_mode_bypasses_only_the_attention_projections():
+    """HF WavLM skips calling only q/k/v/out_proj (it hands their tensors to
+    F.multi_head_attention_forward); an adapter on the FFN's Linears is called as a module, so peft applies it.
+    In lora_mode "reference" the product therefore bypasses the attention adapters and keeps the others active."""
+    import torch.nn as nn
+    from radhip.wavlm import Attention, LoraLinear, inject_lora
+
+    class Layer(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.attention = Attention.__new__(Attention)
+            nn.Module.__init__(self.attention)
+            self.attention.q_proj, self.attention.v_proj = nn.Linear(4, 4), nn.Linear(4, 4)
+            self.feed_forward = nn.Module()
+            self.feed_forward.intermediate_dense = nn.Linear(4, 8)
+    targets = ("q_proj", "v_proj", "intermediate_dense")
+    _, n = inject_lora(Layer(), r=2, alpha=4, dropout=0.0, targets=targets, active=False)
+    wrapped, _ = inject_lora(Layer(), r=2, alpha=4, dropout=0.0, targets=targets, active=False)
+    layer = wrapped.model if hasattr(wrapped, "model") else next(iter(wrapped.children()))
+    assert n == 3
+    assert isinstance(layer.attention.q_proj, LoraLinear) and not layer.attention.q_proj.active
+    assert not layer.attention.v_proj.active
+    assert isinstance(layer.feed_forward.intermediate_dense, LoraLinear)
+    assert layer.feed_forward.intermediate_dense.active
+    wrapped2, _ = inject_lora(Layer(), r=2, alpha=4, dropout=0.0, targets=targets, active=True)
+    layer2 = wrapped2.model if hasattr(wrapped2, "model") else next(iter(wrapped2.children()))
+    assert layer2.attention.q_proj.active and layer2.feed_forward.intermediate_dense.active
