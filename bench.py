@@ -34,7 +34,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAKS = {"hbm": 8000.0, "fp32": 157.3, "bf16": 2500.0}  # GB/s ; TFLOP/s (MI355X_MICROARCH.md, dense)
-KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "selective_scan_fwd": ("hbm", None),
+KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "sincconv_mfma": ("mfma", "bf16"), "selective_scan_fwd": ("hbm", None),
                 "selective_scan_bwd": ("hbm", None), "layer_wsum_fwd": ("hbm", None),
                 "layer_wsum_bwd": ("hbm", None), "rawboost_batch": ("hbm", None),
                 "attn_fwd": ("mfma", "bf16"), "attn_bwd": ("mfma", "bf16"),
@@ -43,7 +43,7 @@ KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "selective_scan_fwd": (
                 "b0x_fwd": ("mfma", "bf16"), "b0x_bwd": ("mfma", "bf16"), "wgrad_acc": ("mfma", "bf16"), "sconv_fwd": ("hbm", None), "sconv_wgrad": ("hbm", None),
                 "sconv_dgrad_bnselu": ("hbm", None),
                 "fe_conv0": ("hbm", None), "fe_ln_gelu": ("hbm", None), "fe_conv_gemm": ("mfma", "bf16"),
-                "gemm": ("mfma", "bf16"), "wgemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}
+                "gemm": ("mfma", "bf16"), "wgemm": ("mfma", "bf16"), "pgemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}
 TRAIN_FLOP_PER_UTT = 0.72e12                # SURVEY.md §8d (algorithmic, FGM step)
 
 

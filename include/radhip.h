@@ -55,6 +55,13 @@ int rdx_sincconv_absmaxpool_fwd_devmask(const float* x, int64_t batch, int64_t l
                                         const float* filters, int channels, int ksize,
                                         const int32_t* mask_dev, int mask_stride, float* out,
                                         void* stream);
+/* f16 MFMA form for the autocast paths (the reference's autocast runs this F.conv1d in fp16, src/main.py:1049):
+ * x and the bank rounded to fp16, fp32 accumulation, fp32 pooled output. mask_dev null: the band mask
+ * [mask_lo, mask_hi); else per-batch / per-utterance as rdx_sincconv_absmaxpool_fwd_devmask (mask_stride 0 / 2).
+ * ksize <= 160, channels <= 80 (csrc/sincconv.hip sincconv_mfma_kernel). */
+int rdx_sincconv_absmaxpool_f16mfma(const float* x, int64_t batch, int64_t len, const float* filters, int channels,
+                                    int ksize, int mask_lo, int mask_hi, const int32_t* mask_dev, int mask_stride,
+                                    float* out, void* stream);
 /* RawNet2 front end (legacy plugin, models/RawNet2Spoof.py:77-103 SincConv.forward and :244-245
  * `F.max_pool1d(torch.abs(x), 3)`): the same fused sinc conv + |.|, pooled over time only.
  *   out [batch, channels, (len-ksize+1)/3] fp32 = max over 3 consecutive conv times of |conv| */
@@ -422,6 +429,23 @@ int rdx_wl_lora_pack(int nl, const float* const* bq, const float* const* bv, voi
 int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                   const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao,
                   const int64_t* seed_dev, int salt, float p_drop, void* stream);
+
+/* ---- Chunked two-level selective scan (csrc/scan2.hip) -----------------------------------------------------
+ * Same operands and results as rdx_selective_scan_fwd / _bwd (src/models/modules/mamba_block.py:65-122, both
+ * directions at original positions, the same checkpoint layout), the steps cut into rdx_scan2_chunks(L) chunks of
+ * 16: per-chunk local states and decay products, then every chunk from its composed carry. Forward: P (the
+ * per-chunk decay products, kept for the backward) and hloc are [dirs][B][chunks][D][N] fp32
+ * (rdx_scan2_rec_elems). Backward: gloc is a workspace of the same size; dA_part [dirs * B * chunks][D][N],
+ * dD_part / dbias_part [dirs * B * chunks][D] (summed by the caller); dBC zeroed by the caller. */
+int rdx_scan2_chunks(int L);
+int64_t rdx_scan2_rec_elems(int B, int L, int D, int N, int dirs);
+int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm, const void* Cm,
+                  int64_t ldbc, const float* Dp, const float* dt_bias, float* y, float* ckpt, float* P, float* hloc,
+                  int B, int L, int D, int N, int dirs, void* stream);
+int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm, const void* Cm,
+                  int64_t ldbc, const float* Dp, const float* dt_bias, const float* ckpt, const float* P,
+                  const float* dy, int64_t dy_dir_stride, void* du, void* ddelta, float* dBC, float* dA_part,
+                  float* dD_part, float* dbias_part, float* gloc, int B, int L, int D, int N, int dirs, void* stream);
 
 /* ---- bf16 MFMA GEMM of the WavLM encoder projections, LDS-DMA pipeline (csrc/wgemm.hip) ---------------
  * Same contract as rdx_gemm_bf16 for the RDX_EPI_BIAS / _BIAS_GELU / _GELU_BWD epilogues, with K % 64 == 0;

@@ -79,6 +79,142 @@ __global__ __launch_bounds__(SINC_T3) void sincconv_absmaxpool_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// The same fused conv + |.| + 3x3 max-pool on the f16 MFMA, for the autocast paths: under the reference's
+// torch.cuda.amp.autocast (src/main.py:1049) F.conv1d runs in fp16, so x and the filter bank are rounded to
+// fp16 here as well (fp32 accumulation; the pooled output stays fp32). The conv is a GEMM with a Hankel
+// operand, conv[c][p] = sum_k W[c][k] x[p + k]: M = channels (70 -> 5 x 16-row fragments), K = taps (129 ->
+// 5 x 32, zero-padded), N = positions.
+//   * block = 4 waves over SM_RANGE conv positions of one utterance; every wave keeps the whole filter bank as
+//     MFMA A fragments in registers (25 x 8 f16, read once per block);
+//   * the sample window is staged in LDS as 8 f16 copies shifted by 0..7 samples, so the B fragment of
+//     v_mfma_f32_16x16x32_f16 (lane: 8 consecutive samples from p + (lane & 15) + 8 (lane >> 4)) is ONE
+//     16-byte aligned ds_read from copy (lane & 7);
+//   * per sub-tile of SM_SUB positions (12 fragments, 3 per wave) |conv| goes to an LDS image [70][SM_SUB]
+//     fp32 (band-masked channels as 0, the reference zeroes those filter rows), and the 3 x 3 max-pool of the
+//     image is stored as coalesced pooled rows.
+constexpr int SM_SUB = 192;                  // conv positions per sub-tile (64 pooled)
+constexpr int SM_NSUB = 6;
+constexpr int SM_RANGE = SM_SUB * SM_NSUB;   // conv positions per block
+constexpr int SM_KP = 160;                   // taps padded to 5 x 32
+constexpr int SM_XW = SM_RANGE + SM_KP;      // staged samples per copy (multiple of 8)
+constexpr int SM_CF = 5;                     // 16-channel fragments (80 >= 70)
+
+typedef __attribute__((ext_vector_type(8))) _Float16 h16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4s;
+
+__global__ __launch_bounds__(256, 2) void sincconv_mfma_kernel(
+    const float* __restrict__ x, int64_t len, const float* __restrict__ filters, int channels, int K,
+    int mask_lo, int mask_hi, const int32_t* __restrict__ mask_dev, int mask_stride, float* __restrict__ out,
+    int64_t T3, int C3) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  _Float16* xc = reinterpret_cast<_Float16*>(smem);                       // [8][SM_XW]
+  float* s_c = reinterpret_cast<float*>(smem + 8 * SM_XW * 2);             // [channels][SM_SUB + 4]
+  constexpr int CP = SM_SUB + 4;
+  const int b = blockIdx.y;
+  if (mask_dev != nullptr) {
+    mask_lo = mask_dev[(int64_t)b * mask_stride];
+    mask_hi = mask_dev[(int64_t)b * mask_stride + 1];
+  }
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t p0 = (int64_t)blockIdx.x * SM_RANGE;
+  const float* xb = x + (int64_t)b * len;
+  // 8 shifted copies: xc[s][i] = x[p0 + i + s] (0 past the utterance), 8 samples (16 bytes) per store
+  for (int q = tid; q < 8 * (SM_XW / 8); q += 256) {
+    const int s = q / (SM_XW / 8), i0 = (q - s * (SM_XW / 8)) * 8;
+    h16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t g = p0 + i0 + s + j;
+      v[j] = (_Float16)(g < len ? xb[g] : 0.f);
+    }
+    *reinterpret_cast<h16x8*>(xc + s * SM_XW + i0) = v;
+  }
+  // the filter bank as A fragments: lane (row = lane & 15, kq = lane >> 4) holds W[16 cf + row][32 ks + 8 kq + j]
+  h16x8 wf[SM_CF][5];
+  {
+    const int row = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int cf = 0; cf < SM_CF; ++cf) {
+      const int c = 16 * cf + row;
+#pragma unroll
+      for (int ks = 0; ks < 5; ++ks) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * ks + 8 * kq + j;
+          wf[cf][ks][j] = (_Float16)((c < channels && k < K) ? filters[(int64_t)c * K + k] : 0.f);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* ob = out + (int64_t)b * C3 * T3;
+  const int col = lane & 15, kq = lane >> 4;
+  for (int sub = 0; sub < SM_NSUB; ++sub) {
+    // 12 position fragments of 16 per sub-tile, 3 per wave
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int pl = sub * SM_SUB + (wave * 3 + f) * 16;     // block-local position of the fragment
+      f32x4s acc[SM_CF];
+#pragma unroll
+      for (int cf = 0; cf < SM_CF; ++cf) acc[cf] = f32x4s{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 5; ++ks) {
+        const int e = pl + (col & ~7) + 32 * ks + 8 * kq;     // multiple of 8: 16-byte aligned in copy col & 7
+        const h16x8 xv = *reinterpret_cast<const h16x8*>(xc + (col & 7) * SM_XW + e);
+#pragma unroll
+        for (int cf = 0; cf < SM_CF; ++cf)
+          acc[cf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[cf][ks], xv, acc[cf], 0, 0, 0);
+      }
+      // lane holds conv[16 cf + 4 kq + i][pl + col]
+      const int pc = pl - sub * SM_SUB + col;
+#pragma unroll
+      for (int cf = 0; cf < SM_CF; ++cf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * cf + 4 * kq + i;
+          if (c < channels) s_c[c * CP + pc] = (c >= mask_lo && c < mask_hi) ? 0.f : fabsf(acc[cf][i]);
+        }
+    }
+    __syncthreads();
+    // 3 x 3 max-pool of the sub-tile: C3 x (SM_SUB / 3) outputs
+    const int64_t t3b = (p0 + (int64_t)sub * SM_SUB) / 3;
+    for (int q = tid; q < C3 * (SM_SUB / 3); q += 256) {
+      const int c3 = q / (SM_SUB / 3), u = q - c3 * (SM_SUB / 3);
+      const int64_t t3 = t3b + u;
+      if (t3 >= T3) continue;
+      const float* r0 = s_c + (3 * c3) * CP + 3 * u;
+      float m = fmaxf(fmaxf(r0[0], r0[1]), r0[2]);
+      m = fmaxf(m, fmaxf(fmaxf(r0[CP], r0[CP + 1]), r0[CP + 2]));
+      m = fmaxf(m, fmaxf(fmaxf(r0[2 * CP], r0[2 * CP + 1]), r0[2 * CP + 2]));
+      ob[(int64_t)c3 * T3 + t3] = m;
+    }
+    __syncthreads();
+  }
+}
+
+static int sincconv_mfma_launch(const float* x, int64_t batch, int64_t len, const float* filters, int channels,
+                                int ksize, int mask_lo, int mask_hi, const int32_t* mask_dev, int mask_stride,
+                                float* out, hipStream_t st) {
+  const int64_t T = len - ksize + 1, T3 = T / 3;
+  const int C3 = channels / 3;
+  if (T3 <= 0) return RDX_EINVAL;
+  if (ksize > SM_KP || channels > 16 * SM_CF) return RDX_EUNSUPPORTED;
+  const size_t smem = (size_t)8 * SM_XW * 2 + (size_t)channels * (SM_SUB + 4) * 4;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sincconv_mfma_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  dim3 grid((unsigned)((3 * T3 + SM_RANGE - 1) / SM_RANGE), (unsigned)batch);
+  hipLaunchKernelGGL(sincconv_mfma_kernel, grid, dim3(256), smem, st, x, len, filters, channels, ksize, mask_lo,
+                     mask_hi, mask_dev, mask_stride, out, T3, C3);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
 }  // namespace rdx
 
 using namespace rdx;
@@ -138,4 +274,16 @@ extern "C" int rdx_sincconv_abspool1d_fwd(const float* x, int64_t batch, int64_t
                      filters, channels, ksize, mask_lo, mask_hi, (const int32_t*)nullptr, 0, out, T3, C3);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
+}
+
+// f16 MFMA form (autocast paths; see sincconv_mfma_kernel): same output as rdx_sincconv_absmaxpool_fwd[_devmask]
+// with x and the bank rounded to fp16. mask_dev null: the band mask [mask_lo, mask_hi); else mask_dev as in
+// rdx_sincconv_absmaxpool_fwd_devmask. ksize <= 160, channels <= 80.
+extern "C" int rdx_sincconv_absmaxpool_f16mfma(const float* x, int64_t batch, int64_t len, const float* filters,
+                                               int channels, int ksize, int mask_lo, int mask_hi,
+                                               const int32_t* mask_dev, int mask_stride, float* out, void* stream) {
+  RDX_REQUIRE(x && filters && out && batch > 0 && channels >= 3 && ksize > 0 && len >= ksize);
+  RDX_REQUIRE(batch <= 65535 && (mask_stride == 0 || mask_stride == 2));
+  return sincconv_mfma_launch(x, batch, len, filters, channels, ksize, mask_lo, mask_hi, mask_dev, mask_stride, out,
+                              as_stream(stream));
 }

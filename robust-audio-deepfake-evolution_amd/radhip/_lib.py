@@ -111,6 +111,12 @@ SIGNATURES = {
     "rdx_wgrad_ws_floats": (c_i64, [c_int, c_int, c_int]),
     "rdx_wgrad_acc": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rdx_wgemm_counters": (c_i64, [c_int, c_int, c_int]),
+    "rdx_sincconv_absmaxpool_f16mfma": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int,
+                                                c_vp, c_vp]),
+    "rdx_scan2_chunks": (c_int, [c_int]),
+    "rdx_scan2_rec_elems": (c_i64, [c_int, c_int, c_int, c_int, c_int]),
+    "rdx_scan2_fwd": (c_int, [c_int] + [c_vp] * 5 + [c_i64] + [c_vp] * 6 + [c_int] * 5 + [c_vp]),
+    "rdx_scan2_bwd": (c_int, [c_int] + [c_vp] * 5 + [c_i64] + [c_vp] * 5 + [c_i64] + [c_vp] * 7 + [c_int] * 5 + [c_vp]),
     "rdx_pgemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
                                c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_pgemm_prof": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp,

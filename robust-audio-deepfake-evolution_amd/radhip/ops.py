@@ -149,6 +149,13 @@ def _p(t):
 
 
 # --------------------------------------------------------------------------------- SincConv ----
+def sinc_mfma_enabled(C, K):
+    """The f16 MFMA SincConv under CUDA autocast (bf16 or fp16: the reference's autocast runs this conv in fp16),
+    for banks of <= 80 channels x 160 taps; RADHIP_SINC_MFMA=0 keeps the fp32 kernel (A/B measurement)."""
+    return (torch.is_autocast_enabled("cuda") and C <= 80 and K <= 160
+            and os.environ.get("RADHIP_SINC_MFMA", "1") != "0")
+
+
 def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
     """|conv1d(x, filters)| max-pooled 3x3 over (channel, time): [B, L] -> [B, C//3, (L-K+1)//3].
 
@@ -161,6 +168,19 @@ def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
     B, L = x.shape
     C, K = filters.shape
     out = torch.empty(B, C // 3, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
+    if sinc_mfma_enabled(C, K):
+        # autocast (the training step and bf16 eval): the reference's conv1d runs in fp16 there
+        # (src/main.py:1049) -> the f16 MFMA form; the fp32 paths keep the exact fp32 kernel below
+        per_utt = mask_dev is not None and mask_dev.dim() == 2
+        if mask_dev is not None:
+            assert mask_dev.dtype == torch.int32 and mask_dev.is_cuda and mask_dev.is_contiguous()
+            assert (mask_dev.shape == (B, 2)) if per_utt else mask_dev.numel() >= 2
+        with _timed("sincconv_mfma", x, sinc_flops(B, C, K, L)):
+            check(lib().rdx_sincconv_absmaxpool_f16mfma(_p(x), B, L, _p(filters), C, K, int(mask_lo), int(mask_hi),
+                                                        _p(mask_dev) if mask_dev is not None else None,
+                                                        2 if per_utt else 0, _p(out), _stream(x)),
+                  "sincconv_absmaxpool_f16mfma")
+        return out
     with _timed("sincconv_absmaxpool", x, sinc_flops(B, C, K, L)):
         if mask_dev is not None:
             # int32 [2] (one mask for the batch) or [B, 2] (one per utterance)
@@ -237,6 +257,12 @@ class DWConvBidir(torch.autograd.Function):
         return dx, dw_part.sum(0).view(ctx.wshape), db_part.sum(0), None
 
 
+def scan2_enabled():
+    """The chunked two-level scan (csrc/scan2.hip) by default; RADHIP_SCAN2=0 runs csrc/bimamba.hip's segmented
+    kernels (A/B measurement, parity tests of both)."""
+    return os.environ.get("RADHIP_SCAN2", "1") != "0"
+
+
 class SelectiveScan(torch.autograd.Function):
     """y[dir] = scan(u[dir], softplus(delta[dir] + dt_bias), A = -exp(A_log), B, C) + D*u[dir]."""
 
@@ -259,17 +285,29 @@ class SelectiveScan(torch.autograd.Function):
         y = torch.empty(dirs, B, L, D, device=u.device, dtype=torch.float32)
         ck = torch.empty(lib().rdx_scan_ckpt_elems(B, L, D, N, dirs), device=u.device, dtype=torch.float32)
         es = u.element_size()
-        with _timed("selective_scan_fwd", u, dirs * B * L * (D * (2 * es + 4) + 2 * N * es)):
-            check(lib().rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc,
-                                               _p(Dp), _p(dt_bias), _p(y), _p(ck), B, L, D, N, dirs, _stream(u)),
-                  "selective_scan_fwd")
-        ctx.save_for_backward(u, delta, A_log, Bm, Cm, Dp, dt_bias, ck)
+        chunked = scan2_enabled()
+        if chunked:     # csrc/scan2.hip: per-chunk decay products P are kept for the backward
+            nrec = int(lib().rdx_scan2_rec_elems(B, L, D, N, dirs))
+            P = torch.empty(nrec, device=u.device, dtype=torch.float32)
+            hloc = torch.empty(nrec, device=u.device, dtype=torch.float32)
+            with _timed("selective_scan_fwd", u, dirs * B * L * (D * (2 * es + 4) + 2 * N * es)):
+                check(lib().rdx_scan2_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc, _p(Dp),
+                                          _p(dt_bias), _p(y), _p(ck), _p(P), _p(hloc), B, L, D, N, dirs, _stream(u)),
+                      "scan2_fwd")
+        else:
+            P = torch.empty(0, device=u.device, dtype=torch.float32)
+            with _timed("selective_scan_fwd", u, dirs * B * L * (D * (2 * es + 4) + 2 * N * es)):
+                check(lib().rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
+                                                   ldbc, _p(Dp), _p(dt_bias), _p(y), _p(ck), B, L, D, N, dirs,
+                                                   _stream(u)), "selective_scan_fwd")
+        ctx.save_for_backward(u, delta, A_log, Bm, Cm, Dp, dt_bias, ck, P)
         ctx.ldbc = ldbc
+        ctx.chunked = chunked
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        u, delta, A_log, Bm, Cm, Dp, dt_bias, ck = ctx.saved_tensors
+        u, delta, A_log, Bm, Cm, Dp, dt_bias, ck, P = ctx.saved_tensors
         dirs, B, L, D = u.shape
         N = A_log.shape[1]
         dy = dy.float()
@@ -281,15 +319,24 @@ class SelectiveScan(torch.autograd.Function):
         du = torch.empty_like(u)
         ddelta = torch.empty_like(u)
         dBC = torch.zeros(dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)  # accumulated atomically
-        dA = torch.empty(dirs * B, D, N, device=u.device, dtype=torch.float32)
-        dD = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
-        dbias = torch.empty(dirs * B, D, device=u.device, dtype=torch.float32)
+        parts = dirs * B * (int(lib().rdx_scan2_chunks(L)) if ctx.chunked else 1)
+        dA = torch.empty(parts, D, N, device=u.device, dtype=torch.float32)
+        dD = torch.empty(parts, D, device=u.device, dtype=torch.float32)
+        dbias = torch.empty(parts, D, device=u.device, dtype=torch.float32)
         es = u.element_size()
-        with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
-            check(lib().rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
-                                               ctx.ldbc, _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du),
-                                               _p(ddelta), _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs,
-                                               _stream(u)), "selective_scan_bwd")
+        if ctx.chunked:
+            gloc = torch.empty(int(lib().rdx_scan2_rec_elems(B, L, D, N, dirs)), device=u.device, dtype=torch.float32)
+            with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
+                check(lib().rdx_scan2_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ctx.ldbc,
+                                          _p(Dp), _p(dt_bias), _p(ck), _p(P), _p(dy), dy_stride, _p(du), _p(ddelta),
+                                          _p(dBC), _p(dA), _p(dD), _p(dbias), _p(gloc), B, L, D, N, dirs, _stream(u)),
+                      "scan2_bwd")
+        else:
+            with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
+                check(lib().rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
+                                                   ctx.ldbc, _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du),
+                                                   _p(ddelta), _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs,
+                                                   _stream(u)), "selective_scan_bwd")
         dBC = dBC.to(Bm.dtype)
         return du, ddelta, dA.sum(0), dBC[..., :N], dBC[..., N:], dD.sum(0), dbias.sum(0)
 
@@ -1269,16 +1316,17 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
 # GELU backward, so it stays unfused. out_proj / its input gradient (64 x 64 tiles, 10.3 us vs 20-27) and FFN1 +
 # GELU (28.3 vs 32.7) run here; every B = 32 shape and the N = 1024, K = 3072 / 4096 ones stay on hipBLASLt.
 WGEMM_POLICY = {
-    "b8": {"qkv": (21, 1), "out": (5, 1), "d_out": (5, 1), "ffn1": (6, 1)},
+    "b8": {"qkv": ("pg", 4, 4), "out": (5, 1), "d_out": (5, 1), "ffn1": (6, 1)},
     "b32": {},
 }
 
 
 def wgemm_policy(name, M, N, K):
-    """(tile, splits) for the fused WavLM layer's GEMM `name` (qkv, out, ffn1, ffn2 and the input gradients
-    d_qkv, d_out, d_ffn1 (FFN1's), d_ffn2 (FFN2's, with the GELU backward fused)) at M token rows, or None for
-    hipBLASLt. RADHIP_WGEMM=0 routes everything to hipBLASLt; RADHIP_WGEMM_POLICY (JSON, same layout as
-    WGEMM_POLICY) overrides the table for A/B runs."""
+    """The kernel for the fused WavLM layer's GEMM `name` (qkv, out, ffn1, ffn2 and the input gradients d_qkv,
+    d_out, d_ffn1 (FFN1's), d_ffn2 (FFN2's, with the GELU backward fused)) at M token rows: (tile, splits) of
+    csrc/wgemm.hip, ("pg", tile, group_m) of csrc/pgemm.hip, or None for hipBLASLt. RADHIP_WGEMM=0 routes
+    everything to hipBLASLt; RADHIP_WGEMM_POLICY (JSON, same layout as WGEMM_POLICY) overrides the table for A/B
+    runs."""
     if os.environ.get("RADHIP_WGEMM", "1") == "0" or K % 64 or N % 8:
         return None
     table = WGEMM_POLICY
@@ -1287,7 +1335,18 @@ def wgemm_policy(name, M, N, K):
         import json
         table = json.loads(env)
     ent = table.get("b8" if M <= 2048 else "b32", {}).get(name)
-    return (int(ent[0]), int(ent[1])) if ent is not None else None
+    if ent is None:
+        return None
+    if ent[0] == "pg":
+        return ("pg", int(ent[1]), int(ent[2]))
+    return (int(ent[0]), int(ent[1]))
+
+
+def layer_gemm(pol, a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None):
+    """Run a WavLM layer GEMM C = a @ b^T (+ epilogue) on the kernel `pol` names (wgemm_policy, not None)."""
+    if pol[0] == "pg":
+        return pgemm(a, b, bias, epilogue=epilogue, aux=aux, tile=pol[1], group_m=pol[2])
+    return wgemm(a, b, bias, epilogue=epilogue, aux=aux, tile=pol[0], splits=pol[1])
 
 
 def wgrad_acc(dy, x, dw, db=None):
@@ -1366,6 +1425,32 @@ def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
                                       _p(ws) if ws is not None else None, ws_bytes,
                                       _p(cnt) if cnt is not None else None, n_cnt, st),
               "wgemm_bf16")
+    return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
+
+
+def pgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=4, group_m=4,
+          name="pgemm"):
+    """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/pgemm.hip (8-wave deep-pipelined MFMA GEMM, one
+    workgroup per output tile): bf16 row views a, b (unit inner stride, 16-byte aligned, K % 64 == 0); returns C, or
+    (C, gelu(C)) for EPI_BIAS_GELU."""
+    _require_gpu(a, b)
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip pgemm: bf16 operands with unit inner stride required")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2 or K % 64:
+        raise ValueError(f"radhip pgemm: K {K} vs {K2} (K % 64 == 0 required)")
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
+        aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
+        check(lib().rdx_pgemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+                                   _p(bias) if bias is not None else None, int(epilogue),
+                                   _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                                   _p(aux_out) if aux_out is not None else None,
+                                   aux_out.stride(0) if aux_out is not None else 0, int(tile), int(group_m),
+                                   _stream(a)), "pgemm_bf16")
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
 
 

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, lib
-from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, rel_bias_table, wgemm, wgemm_policy
+from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, layer_gemm, rel_bias_table, wgemm_policy
 
 E_FUSED = 1024
 
@@ -203,7 +203,7 @@ class WavLMLayerFn(torch.autograd.Function):
                                        ldx, _p(gate), _p(mean1), _p(rstd1), M, E, st), "wl_ln1_fwd")
         pol = _gemm("qkv", M, 3 * E, ldx)
         if pol is not None:
-            qkv = wgemm(x1, cache.wext, cache.bqkv, tile=pol[0], splits=pol[1])
+            qkv = layer_gemm(pol, x1, cache.wext, cache.bqkv)
         else:
             qkv = F.linear(x1, cache.wext, cache.bqkv)                      # [M, 3E] (LoRA folded in)
         o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
@@ -216,7 +216,7 @@ class WavLMLayerFn(torch.autograd.Function):
                                      _p(mask) if mask is not None else None, B, T, H, 64, st), "attn_fwd")
         pol = _gemm("out", M, E, E)
         if pol is not None:
-            aout = wgemm(o, cache.wo, cache.bo, tile=pol[0], splits=pol[1])
+            aout = layer_gemm(pol, o, cache.wo, cache.bo)
         else:
             aout = F.linear(o, cache.wo, cache.bo)
         h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -229,14 +229,14 @@ class WavLMLayerFn(torch.autograd.Function):
         F4 = cache.w1.shape[0]
         pol = _gemm("ffn1", M, F4, E)
         if pol is not None:                             # FFN1 + bias + GELU in one launch
-            u, v = wgemm(x2, cache.w1, cache.b1, epilogue=_lib.EPI_BIAS_GELU, tile=pol[0], splits=pol[1])
+            u, v = layer_gemm(pol, x2, cache.w1, cache.b1, epilogue=_lib.EPI_BIAS_GELU)
         else:
             u = F.linear(x2, cache.w1, cache.b1)
             v = torch.empty_like(u)
             check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
         pol = _gemm("ffn2", M, E, F4)
         if pol is not None:
-            fo = wgemm(v, cache.w2, cache.b2, tile=pol[0], splits=pol[1])
+            fo = layer_gemm(pol, v, cache.w2, cache.b2)
         else:
             fo = F.linear(v, cache.w2, cache.b2)
         out = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -274,14 +274,14 @@ class WavLMLayerFn(torch.autograd.Function):
         F4 = u.shape[1]
         pol = _gemm("d_ffn2", M, F4, E)
         if pol is not None:                             # FFN2's input gradient with the GELU backward fused
-            du = wgemm(dfo, cache.t("w2"), epilogue=_lib.EPI_GELU_BWD, aux=u, tile=pol[0], splits=pol[1])
+            du = layer_gemm(pol, dfo, cache.t("w2"), epilogue=_lib.EPI_GELU_BWD, aux=u)
         else:
             dv = torch.mm(dfo, cache.w2)
             du = torch.empty_like(u)
             check(lib().rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
         pol = _gemm("d_ffn1", M, E, F4)
         if pol is not None:
-            dx2 = wgemm(du, cache.t("w1"), tile=pol[0], splits=pol[1])
+            dx2 = layer_gemm(pol, du, cache.t("w1"))
         else:
             dx2 = torch.mm(du, cache.w1)
         dh2 = torch.empty(M, E, device=dev, dtype=torch.float32)
@@ -291,7 +291,7 @@ class WavLMLayerFn(torch.autograd.Function):
                                   salt + 1, p_hidden, _p(daout), M, E, st), "wl_ln_bwd")
         pol = _gemm("d_out", M, E, E)
         if pol is not None:
-            do = wgemm(daout, cache.t("wo"), tile=pol[0], splits=pol[1])
+            do = layer_gemm(pol, daout, cache.t("wo"))
         else:
             do = torch.mm(daout, cache.wo)
         D = torch.empty(B, H, T, device=dev, dtype=torch.float32)
@@ -303,7 +303,7 @@ class WavLMLayerFn(torch.autograd.Function):
                             _off(dqkv, 2 * E), 3 * E, dgate, B, T, H, st)
         pol = _gemm("d_qkv", M, ldx, 3 * E) if not lora else None   # (active LoRA: wext changes every step)
         if pol is not None:
-            dx1 = wgemm(dqkv, cache.t("wqkv"), tile=pol[0], splits=pol[1])
+            dx1 = layer_gemm(pol, dqkv, cache.t("wqkv"))
         else:
             dx1 = torch.mm(dqkv, cache.wext)                                 # [M, E + 2r]
         dh = torch.empty(M, E, device=dev, dtype=torch.float32)

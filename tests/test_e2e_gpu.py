@@ -42,6 +42,9 @@ GRAD_REL_BF16 = {"reference": {"layer_weights": 0.09, "feature_projection": 0.05
                             "fusion": 0.16, "backbone": 0.18, "head": 0.12}}
 
 
+FLOOR_RATIOS = {}      # bf16 product error / fp16 reference-floor error, filled by the reference-mode run
+
+
 def _cfg(lora_mode):
     from radhip.build import load_config
     from radhip.wavlm import WAVLM_LARGE
@@ -107,9 +110,12 @@ def _inputs():
     return xm, y, lam, perm
 
 
-def _oracle_step(o, xo, y, lam, perm, host):
+def _oracle_step(o, xo, y, lam, perm, host, amp=None, scale=1.0):
     """src/main.py:1036-1097 at accumulation 1: mixup loss, backward, FGM attack on the clean gradient,
-    adversarial pass with its own band / SpecAugment masks, backward, restore."""
+    adversarial pass with its own band / SpecAugment masks, backward, restore. amp = torch.float16 runs the
+    passes under fp16 autocast with the losses multiplied by `scale` before backward, as the reference's
+    torch.cuda.amp.autocast() + GradScaler do (src/main.py:28,1049,1077-1108; FGM's g / ||g|| is scale-free); the
+    caller divides the gradients by `scale` (the scaler's unscale_)."""
     from oracle.model import focal_loss
     ya = torch.from_numpy(y).to(DEV)
     yb = ya[torch.tensor(perm, device=DEV)]
@@ -120,10 +126,12 @@ def _oracle_step(o, xo, y, lam, perm, host):
 
     def fwd(mask, tmask):
         lo, hi = int(mask[0]), int(mask[1])
-        _, out = o(xo, mask=(lo, hi), time_mask=torch.from_numpy(tmask).to(DEV))
+        with torch.autocast("cuda", dtype=amp or torch.float32, enabled=amp is not None):
+            _, out = o(xo, mask=(lo, hi), time_mask=torch.from_numpy(tmask).to(DEV))
+        out = out.float() if amp is not None else out
         return lam * focal_loss(out, ya) + (1.0 - lam) * focal_loss(out, yb)
     loss = fwd(host["c_mask"][0], host["c_tmask"])
-    loss.backward()
+    (loss * scale).backward()
     fp = [(n, p) for n, p in o.named_parameters() if p.requires_grad and "feature_projection" in n]
     backup = {}
     with torch.no_grad():
@@ -133,7 +141,7 @@ def _oracle_step(o, xo, y, lam, perm, host):
             if nrm != 0 and not torch.isnan(nrm):
                 p.add_(0.5 * p.grad / nrm)
     adv = fwd(host["a_mask"][0], host["a_tmask"][0])
-    adv.backward()
+    (adv * scale).backward()
     with torch.no_grad():
         for n, p in fp:                            # FGM.restore
             p.copy_(backup[n])
@@ -234,6 +242,41 @@ def test_bench_path_window_bf16_vs_fp64_oracle(lora_mode):
     errs = {g: _rel(torch.cat(a), torch.cat(b)) for g, (a, b) in groups.items()}
     e16 = float((lp16 - lo).abs().max())
     e32 = float((lp32 - lo).abs().max())
+    # The reference's own error floor: the oracle's module code (transformers' WavLM + the
+    # restated reference modules) in fp32 weights under fp16 autocast + loss scaling 2^16 (GradScaler's initial
+    # scale), the same inputs and masks, against the same fp64 run.
+    if lora_mode == "reference":
+        import copy
+        S = 65536.0
+        og64 = {n: g for n, g in og.items()}
+        o32 = copy.deepcopy(o).float()
+        for p in o32.parameters():
+            p.grad = None
+        o32.eval()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            _, lo_f16 = o32(xo.float())
+        l_f16 = _oracle_step(o32, xo.float(), y, lam, perm, hosts[0], amp=torch.float16, scale=S)
+        og16 = {n: p.grad.double() / S for n, p in o32.named_parameters() if p.grad is not None}
+        gf = {}
+        for n in trainable:
+            if n in dead:
+                continue
+            g = _group(n)
+            a, b = og16[omap_inv[n]].reshape(-1), og64[omap_inv[n]].reshape(-1)
+            ga, gb = gf.setdefault(g, ([], []))
+            ga.append(a)
+            gb.append(b)
+        floor = {g: _rel(torch.cat(a), torch.cat(b)) for g, (a, b) in gf.items()}
+        ef16 = float((lo_f16.double() - lo).abs().max())
+        print(f"\n[e2e fp16 floor] reference modules under fp16 autocast + GradScaler vs fp64: eval logits max abs "
+              f"err {ef16:.3e}; clean loss {l_f16:.6f} vs {o_loss:.6f}; grad rel L2: "
+              + ", ".join(f"{g} {e:.3e}" for g, e in sorted(floor.items())))
+        print("[e2e fp16 floor] bf16 product / fp16 reference floor: logits "
+              f"{e16 / max(ef16, 1e-12):.2f}x; grads "
+              + ", ".join(f"{g} {errs[g] / max(floor[g], 1e-12):.2f}x" for g in sorted(floor)))
+        FLOOR_RATIOS.update({"logits": e16 / max(ef16, 1e-12)})
+        FLOOR_RATIOS.update({g: errs[g] / max(floor[g], 1e-12) for g in floor})
+        del o32
     print(f"\n[e2e {lora_mode}] logits |oracle| max {float(lo.abs().max()):.4f}; bf16 eval max abs err {e16:.3e}; "
           f"fp32 eval max abs err {e32:.3e}")
     print(f"[e2e {lora_mode}] clean loss product {losses[0]:.6f} (replay 2: {losses[1]:.6f}) oracle {o_loss:.6f}")

@@ -144,7 +144,7 @@ def test_wgemm_policy_shapes_match_hipblaslt():
     """Every (GEMM, token count) the fused WavLM layer routes to wgemm (radhip.ops.wgemm_policy) agrees with
     hipBLASLt's bf16 result to bf16 rounding, with its epilogue."""
     from radhip import _lib
-    from radhip.ops import wgemm, wgemm_policy
+    from radhip.ops import layer_gemm, wgemm_policy
     shapes = {"qkv": (3072, 1024), "out": (1024, 1024), "ffn1": (4096, 1024), "ffn2": (1024, 4096),
               "d_ffn2": (4096, 1024), "d_ffn1": (1024, 4096), "d_out": (1024, 1024), "d_qkv": (1024, 3072)}
     n = 0
@@ -157,14 +157,14 @@ def test_wgemm_policy_shapes_match_hipblaslt():
             a, b, bias = _ops(M, N, K, seed=N + K)
             if name == "d_ffn2":
                 uu = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-                got = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=pol[0], splits=pol[1])
+                got = layer_gemm(pol, a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu)
                 x = uu.float()
                 grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
                 ref = torch.mm(a, b.t()).float() * grad
                 assert _rel(got, ref) < 2e-2, name
                 continue
             epi = _lib.EPI_BIAS_GELU if name == "ffn1" else _lib.EPI_BIAS
-            got = wgemm(a, b, bias, epilogue=epi, tile=pol[0], splits=pol[1])
+            got = layer_gemm(pol, a, b, bias, epilogue=epi)
             got = got[0] if isinstance(got, tuple) else got
             ref = torch.nn.functional.linear(a, b, bias)
             assert _rel(got, ref) < 1e-2, name
@@ -194,3 +194,63 @@ def test_wgemm_split_k(tile, splits, M, N, K):
     du = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile, splits=splits)
     du1 = wgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile)
     assert _rel(du, du1) < 1e-2
+
+
+# ---- csrc/pgemm.hip: the deep-pipelined 8-wave GEMM (every tile code, both K-step forms, group orders) ----
+PG_TILES = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 104]
+
+
+@pytest.mark.parametrize("tile", PG_TILES)
+@pytest.mark.parametrize("M,N,K,gm", [(1608, 1024, 1024, 4), (333, 3072, 1024, 0), (1608, 4096, 128, 2),
+                                      (64, 768, 4096, 1), (6432, 1024, 192, 8)])
+def test_pgemm_bias_every_tile(tile, M, N, K, gm):
+    """Row tails (rows past M read as zeros through the buffer range), column tiles, K = 2 steps (shorter than the
+    ring) up to deep K, every group order."""
+    from radhip.ops import pgemm
+    a, b, bias = _ops(M, N, K, seed=tile + gm)
+    got = pgemm(a, b, bias, tile=tile, group_m=gm)
+    assert got.dtype == torch.bfloat16 and got.shape == (M, N)
+    assert _rel(got, a.float() @ b.float().t() + bias.float()) < 1e-2
+    assert _rel(pgemm(a, b, tile=tile, group_m=gm), a.float() @ b.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [0, 2, 4, 5, 7])
+def test_pgemm_epilogues_match_wgemm(tile):
+    """The bias / bias + GELU / GELU-backward epilogues round where csrc/wgemm.hip's do: same values up to the
+    fp32 summation order of the accumulator (bf16 rounding of C), the aux output gelu(u) of the stored u."""
+    from radhip import _lib
+    from radhip.ops import pgemm, wgemm
+    a, b, bias = _ops(1608, 3072, 1024, seed=5)
+    u, v = pgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=tile)
+    u2, v2 = wgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=5)
+    assert float((u.float() - u2.float()).abs().max()) <= 2 ** -7 * float(u2.float().abs().max())
+    ref_v = torch.nn.functional.gelu(u.float())
+    assert float((v.float() - ref_v.to(torch.bfloat16).float()).abs().max()) <= 2 ** -7 * float(ref_v.abs().max())
+    uu = torch.randn(1608, 3072, device=DEV).to(torch.bfloat16)
+    du = pgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile)
+    x = uu.float()
+    grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    assert _rel(du, (a.float() @ b.float().t()).to(torch.bfloat16).float() * grad) < 2e-2
+    # repeatable: the same launch twice gives the same bits (no split, fixed summation order)
+    assert torch.equal(pgemm(a, b, bias, tile=tile), pgemm(a, b, bias, tile=tile))
+
+
+def test_pgemm_probe_stamps():
+    """The diagnostic form stores per-workgroup stamps in order (entry <= stage 0 landed <= loop done <= exit) and
+    the same C as the product form."""
+    import ctypes
+    from radhip import _lib
+    from radhip.ops import pgemm
+    a, b, bias = _ops(1608, 3072, 1024, seed=9)
+    c = torch.empty(1608, 3072, device=DEV, dtype=torch.bfloat16)
+    grid = 13 * 16
+    prof = torch.zeros(grid, 8, dtype=torch.int64, device=DEV)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = _lib.lib().rdx_pgemm_prof(P(a), 1024, P(b), 1024, P(c), 3072, 1608, 3072, 1024, P(bias), 4, 4, P(prof), st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(c, pgemm(a, b, bias, tile=4, group_m=4))
+    d = prof.cpu()
+    assert bool(((d[:, 0] <= d[:, 1]) & (d[:, 1] <= d[:, 2]) & (d[:, 2] <= d[:, 3])).all())
+    assert bool((d[:, 5] >= d[:, 4]).all())

@@ -1,4 +1,6 @@
 """Parity of every HIP kernel (through the C ABI) with the oracle on the same seeded inputs."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -29,6 +31,32 @@ def test_sincconv_absmaxpool_full_length(mask):
     np.testing.assert_allclose(out, ref, rtol=1e-4, atol=2e-6)
 
 
+@pytest.mark.parametrize("mask", [(0, 0), (12, 31), (60, 70)])
+@pytest.mark.parametrize("L", [64600, 3001])
+def test_sincconv_f16_mfma_vs_oracle(mask, L):
+    """The autocast form (f16 MFMA; the reference's autocast runs this conv in fp16): equal to the fp64 oracle
+    on the fp16-rounded waveform and bank up to fp32 accumulation order, and to the exact fp32 conv within fp16
+    input rounding. L = 3001: a partial last block (positions past the utterance read as zeros)."""
+    from oracle.sinc import sinc_filterbank, sincconv_absmaxpool
+    from radhip.ops import sincconv_absmaxpool as hip_sinc
+    bank = sinc_filterbank()
+    x = seeded_array(f"k.sinc16.{L}", (3, L), scale=0.1).astype(np.float32)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = hip_sinc(torch.from_numpy(x).to(DEV), bank.to(DEV), *mask).cpu().numpy()
+    x16 = x.astype(np.float16).astype(np.float32)
+    b16 = bank.numpy().astype(np.float16).astype(np.float32)
+    ref16 = sincconv_absmaxpool(x16, b16, *mask)
+    assert out.shape == ref16.shape == (3, 23, (L - 128) // 3)
+    np.testing.assert_allclose(out, ref16, rtol=1e-4, atol=2e-6)
+    ref = sincconv_absmaxpool(x, bank.numpy(), *mask)
+    assert float(np.abs(out - ref).max()) <= 2e-3 * float(np.abs(ref).max())
+    # the per-utterance device mask (the window's graph-replayable form) gives the same rows
+    md = torch.tensor([list(mask)] * 3, dtype=torch.int32, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out2 = hip_sinc(torch.from_numpy(x).to(DEV), bank.to(DEV), mask_dev=md).cpu().numpy()
+    assert np.array_equal(out, out2)
+
+
 def test_sincconv_golden(golden):
     from radhip.ops import sincconv_absmaxpool as hip_sinc
     g = golden("sinc_conv.npz")
@@ -50,9 +78,14 @@ def _mamba_pair(d_model, seed):
 
 # L covers fewer checkpoint chunks than time segments (19, 23: the segmented forward's empty segments), chunk-
 # aligned and ragged lengths, and the Phase-6 201
+@pytest.mark.parametrize("scan2", ["1", "0"])     # csrc/scan2.hip (chunked, the default) and csrc/bimamba.hip
 @pytest.mark.parametrize("dirs,d_model,L,B", [(1, 16, 23, 2), (2, 16, 19, 2), (2, 144, 201, 2), (1, 144, 201, 3),
-                                              (2, 32, 64, 2), (2, 32, 65, 1), (2, 16, 7, 2)])
-def test_mamba_fwd_bwd_fp32(dirs, d_model, L, B):
+                                              (2, 32, 64, 2), (2, 32, 65, 1), (2, 16, 7, 2), (2, 16, 16, 1),
+                                              (2, 24, 33, 2)])
+def test_mamba_fwd_bwd_fp32(dirs, d_model, L, B, scan2, monkeypatch):
+    """Also L = 16 (one full chunk, no checkpoint), L = 33 (a 1-step last chunk) and Di = 48 (a partial 32-channel
+    group in csrc/scan2.hip)."""
+    monkeypatch.setenv("RADHIP_SCAN2", scan2)
     from oracle.mamba import bimamba_ref
     ref, hip = _mamba_pair(d_model, 100 + d_model)
     x = seeded_array(f"k.mamba.{d_model}.{L}", (B, L, d_model))
@@ -84,6 +117,34 @@ def test_mamba_golden_reference_block(golden):
     np.testing.assert_allclose(x.grad.cpu().numpy(), g["dx"], rtol=1e-3, atol=1e-5)
     for k, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.cpu().numpy(), g[f"grad:{k}"], rtol=2e-3, atol=1e-5, err_msg=k)
+
+
+def test_scan2_matches_segmented_scan_bf16():
+    """The chunked scan against csrc/bimamba.hip's segmented kernels at the Phase-6 shape in bf16 storage: the same
+    outputs and gradients up to fp32 summation order (both chains run in fp32)."""
+    from radhip import ops
+    g = torch.Generator(device=DEV).manual_seed(3)
+    dirs, B, L, D, N, R = 2, 4, 201, 288, 16, 9
+    u = torch.randn(dirs, B, L, D, device=DEV, generator=g).to(torch.bfloat16)
+    delta = (0.5 * torch.randn(dirs, B, L, D, device=DEV, generator=g)).to(torch.bfloat16)
+    xdbl = torch.randn(dirs, B, L, R + 2 * N, device=DEV, generator=g).to(torch.bfloat16)
+    A_log = torch.log(torch.arange(1, N + 1, device=DEV, dtype=torch.float32)).repeat(D, 1)
+    Dp = torch.randn(D, device=DEV, generator=g)
+    bias = 0.1 * torch.randn(D, device=DEV, generator=g)
+    dy = torch.randn(dirs, B, L, D, device=DEV, generator=g)
+    outs = {}
+    for kind in ("0", "1"):
+        os.environ["RADHIP_SCAN2"] = kind
+        try:
+            leaves = [t.clone().requires_grad_() for t in (u, delta, xdbl, A_log, Dp, bias)]
+            uu, dd, xx, al, dp, bb = leaves
+            y = ops.SelectiveScan.apply(uu, dd, al, xx[..., R:R + N], xx[..., R + N:], dp, bb)
+            y.backward(dy)
+            outs[kind] = [y.detach()] + [t.grad for t in leaves]
+        finally:
+            os.environ.pop("RADHIP_SCAN2", None)
+    for a, b in zip(outs["1"], outs["0"]):
+        assert _rel(a.float().cpu(), b.float().cpu()) < 1e-2
 
 
 def test_mamba_bf16_autocast():
