@@ -56,26 +56,34 @@ __device__ __forceinline__ int tstep(const Geo& g, int i, int L) {
 }
 
 // LDS staging of the chunk: u, dt = softplus(delta + bias) [CK][CH] (+ dy), B / C [CK][N]
+// (+ with s_sig: softplus'(pre) = sigmoid(pre), the ddelta factor, once per (t, d) instead of per state)
 template <typename T, bool WITH_C, bool WITH_DY>
 __device__ __forceinline__ void stage(const Geo& g, const T* __restrict__ u, const T* __restrict__ delta,
                                       const float* __restrict__ dt_bias, const T* __restrict__ Bm,
                                       const T* __restrict__ Cm, int64_t ldbc, const float* __restrict__ dy,
                                       int64_t dy_dir_stride, float* s_u, float* s_dt, float* s_dy, float* s_B,
-                                      float* s_C, int B, int L, int D) {
+                                      float* s_C, int B, int L, int D, float* s_sig = nullptr) {
   const int tid = threadIdx.x;
   {
     const int i = tid >> 5, c = tid & 31, dd = g.d0 + c;
-    float uu = 0.f, dv = 0.f, dyv = 0.f;
+    float uu = 0.f, dv = 0.f, dyv = 0.f, sg = 0.f;
     if (i < g.cnt && dd < D) {
       const int t = tstep(g, i, L);
       const int64_t o = ((int64_t)g.db * L + t) * D + dd;
       uu = ld(u, o);
-      dv = softplusf_(ld(delta, o) + dt_bias[dd]);
-      if (WITH_DY) dyv = dy[g.dir * dy_dir_stride + ((int64_t)g.b * L + t) * D + dd];
+      const float pre = ld(delta, o) + dt_bias[dd];
+      dv = softplusf_(pre);
+      if (WITH_DY) {
+        dyv = dy[g.dir * dy_dir_stride + ((int64_t)g.b * L + t) * D + dd];
+        sg = 1.0f / (1.0f + expf(-pre));
+      }
     }
     s_u[i * CH + c] = uu;
     s_dt[i * CH + c] = dv;
-    if (WITH_DY) s_dy[i * CH + c] = dyv;
+    if (WITH_DY) {
+      s_dy[i * CH + c] = dyv;
+      s_sig[i * CH + c] = sg;
+    }
   }
   if (tid < CK * N) {
     const int i = tid >> 4, j = tid & 15;
@@ -114,7 +122,7 @@ __global__ __launch_bounds__(NT) void fwd_chunk_kernel(const T* __restrict__ u, 
   for (int i = 0; i < CK; ++i) {
     if (i < g.cnt) {
       const float dtv = s_dt[i * CH + g.dl];
-      const float a = exp2f(dtv * A2);
+      const float a = __builtin_amdgcn_exp2f(dtv * A2);
       h = fmaf(a, h, dtv * s_u[i * CH + g.dl] * s_B[i * N + g.n]);
       prod *= a;
     }
@@ -135,22 +143,23 @@ __global__ __launch_bounds__(NT) void fwd_out_kernel(const T* __restrict__ u, co
   __shared__ float s_u[CK * CH], s_dt[CK * CH], s_B[CK * N], s_C[CK * N], s_y[CK * CH];
   const Geo g = geo(B, L, D);
   stage<T, true, false>(g, u, delta, dt_bias, Bm, Cm, ldbc, nullptr, 0, s_u, s_dt, nullptr, s_B, s_C, B, L, D);
-  // carry-in from the chunks before this one, in step order (loads issued together, then the FMA chain)
+  // carry-in from the chunks before this one, in step order: every load issued unconditionally from a clamped
+  // index (a per-load runtime test makes hipcc branch and wait around each load), the unused ones masked to the
+  // identity (P = 1, h = 0) in registers, then the FMA chain
   float h = 0.f;
   if (g.active) {
-    float pk[CK], hk[CK];
     const int nprev = g.c;
     for (int k0 = 0; k0 < nprev; k0 += CK) {
       const int m = min(CK, nprev - k0);
+      float pk[CK], hk[CK];
 #pragma unroll
-      for (int k = 0; k < CK; ++k)
-        if (k < m) {
-          pk[k] = P[rec(g, k0 + k, D)];
-          hk[k] = hloc[rec(g, k0 + k, D)];
-        }
+      for (int k = 0; k < CK; ++k) {
+        const int kk = k0 + min(k, m - 1);
+        pk[k] = P[rec(g, kk, D)];
+        hk[k] = hloc[rec(g, kk, D)];
+      }
 #pragma unroll
-      for (int k = 0; k < CK; ++k)
-        if (k < m) h = fmaf(pk[k], h, hk[k]);
+      for (int k = 0; k < CK; ++k) h = fmaf(k < m ? pk[k] : 1.f, h, k < m ? hk[k] : 0.f);
     }
   }
   __syncthreads();
@@ -161,7 +170,7 @@ __global__ __launch_bounds__(NT) void fwd_out_kernel(const T* __restrict__ u, co
     if (i < g.cnt) {    // block-uniform
       const float dtv = s_dt[i * CH + g.dl];
       const float uu = s_u[i * CH + g.dl];
-      const float a = exp2f(dtv * A2);
+      const float a = __builtin_amdgcn_exp2f(dtv * A2);
       h = fmaf(a, h, dtv * uu * s_B[i * N + g.n]);
       const float pv = row16_sum(s_C[i * N + g.n] * h);
       if (g.n == 0) s_y[i * CH + g.dl] = fmaf(Dd, uu, pv);
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(NT) void bwd_chunk_kernel(const T* __restrict__ del
 #pragma unroll
   for (int i = CK - 1; i >= 0; --i) {
     if (i < g.cnt) {
-      const float a = exp2f(s_dt[i * CH + g.dl] * A2);
+      const float a = __builtin_amdgcn_exp2f(s_dt[i * CH + g.dl] * A2);
       X = a * fmaf(s_C[i * N + g.n], s_dy[i * CH + g.dl], X);
     }
   }
@@ -227,26 +236,26 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
     const float* __restrict__ dy, int64_t dy_dir_stride, T* __restrict__ du, T* __restrict__ ddelta,
     float* __restrict__ dBC, float* __restrict__ dA_part, float* __restrict__ dD_part, float* __restrict__ dbias_part,
     int B, int L, int D) {
-  __shared__ float s_u[CK * CH], s_dt[CK * CH], s_dy[CK * CH], s_B[CK * N], s_C[CK * N];
+  __shared__ float s_u[CK * CH], s_dt[CK * CH], s_dy[CK * CH], s_sig[CK * CH], s_B[CK * N], s_C[CK * N];
   __shared__ float s_red[CK][8][2 * N];     // [step][wave][dB 16 | dC 16]
   const Geo g = geo(B, L, D);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = lane >> 4;
-  stage<T, true, true>(g, u, delta, dt_bias, Bm, Cm, ldbc, dy, dy_dir_stride, s_u, s_dt, s_dy, s_B, s_C, B, L, D);
+  stage<T, true, true>(g, u, delta, dt_bias, Bm, Cm, ldbc, dy, dy_dir_stride, s_u, s_dt, s_dy, s_B, s_C, B, L, D,
+                       s_sig);
   // the carry entering from the right: compose the later chunks, nearest last
   float X = 0.f, h0 = 0.f;
   if (g.active) {
-    float pk[CK], gk[CK];
     for (int k1 = g.nc - 1; k1 > g.c; k1 -= CK) {
       const int m = min(CK, k1 - g.c);
+      float pk[CK], gk[CK];
 #pragma unroll
-      for (int k = 0; k < CK; ++k)
-        if (k < m) {
-          pk[k] = P[rec(g, k1 - k, D)];
-          gk[k] = gloc[rec(g, k1 - k, D)];
-        }
+      for (int k = 0; k < CK; ++k) {      // unconditional loads from clamped indices (see fwd_out_kernel)
+        const int kk = k1 - min(k, m - 1);
+        pk[k] = P[rec(g, kk, D)];
+        gk[k] = gloc[rec(g, kk, D)];
+      }
 #pragma unroll
-      for (int k = 0; k < CK; ++k)
-        if (k < m) X = fmaf(pk[k], X, gk[k]);
+      for (int k = 0; k < CK; ++k) X = fmaf(k < m ? pk[k] : 1.f, X, k < m ? gk[k] : 0.f);
     }
     if (g.c > 0) h0 = ckpt[(((int64_t)g.db * (g.nc - 1) + (g.c - 1)) * D + g.d) * N + g.n];
   }
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
     for (int i = 0; i < CK; ++i) {
       if (i < g.cnt) {
         const float dtv = s_dt[i * CH + g.dl];
-        h = fmaf(exp2f(dtv * A2), h, dtv * s_u[i * CH + g.dl] * s_B[i * N + g.n]);
+        h = fmaf(__builtin_amdgcn_exp2f(dtv * A2), h, dtv * s_u[i * CH + g.dl] * s_B[i * N + g.n]);
       }
       hs[i] = h;
     }
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
       const int o = i * CH + g.dl;
       const float dtv = s_dt[o], uu = s_u[o], dyv = s_dy[o];
       const float Bn = s_B[i * N + g.n], Cn = s_C[i * N + g.n];
-      const float a = exp2f(dtv * A2);
+      const float a = __builtin_amdgcn_exp2f(dtv * A2);
       const float hprev = i > 0 ? hs[i > 0 ? i - 1 : 0] : h0;
       const float G = fmaf(Cn, dyv, X);
       const float ah = a * hprev;
@@ -292,7 +301,7 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
       dA = fmaf(G * dtv, ah, dA);
       const float ddt = row16_sum(G * fmaf(Aval, ah, Bn * uu));
       const float dus = row16_sum(G * dtv * Bn);
-      const float ddl = ddt * -expm1f(-dtv);   // softplus' = sigmoid(pre) = 1 - exp(-dt)
+      const float ddl = ddt * s_sig[o];         // softplus'(pre) = sigmoid(pre) (= 1 - exp(-dt))
       r_du[i] = fmaf(Dd, dyv, dus);
       r_dd[i] = ddl;
       dDacc = fmaf(dyv, uu, dDacc);

@@ -519,7 +519,8 @@ def parse_args(argv=None):
     parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "bf16"],
                         help="scoring precision: fp32 as the reference scores (default), or bf16 autocast, which runs "
                              "the hand-written HIP encoder / SincNet path (tools/bench_eval.py: throughput and score "
-                             "deviation)")
+                             "deviation). bf16 scores are parity-unpinned against the reference (no fixture pins its "
+                             "EER); with --eval_amp bf16 they also drive the dev-set best-model selection")
     parser.add_argument("--eager", action="store_true", help="launch kernel by kernel (no HIP graphs)")
     parser.add_argument("--no-window", dest="no_window", action="store_true",
                         help="replay one graph pair per micro-batch instead of the batched accumulation window")

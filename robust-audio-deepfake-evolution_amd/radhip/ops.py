@@ -1169,16 +1169,17 @@ _ATTN_WS = {}
 
 
 def _attn_split_workspace(dev, n_floats, n_counters):
-    """fp32 partial dQ / d gate and the per-(b, h) tickets of the split attention backward, one per device (every
-    attention backward of the product runs on the encoder's compute stream, one after another); the tickets are
-    zeroed here once and left at zero by each launch. Grown outside graph capture only."""
-    cur = _ATTN_WS.get(dev.index)
+    """fp32 partial dQ / d gate and the per-(b, h) tickets of the split attention backward, one per (device,
+    stream): launches on one stream run one after another, launches in flight on two streams must not share them;
+    the tickets are zeroed here once and left at zero by each launch. Grown outside graph capture only."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    cur = _ATTN_WS.get(key)
     if cur is None or cur[0].numel() < n_floats or cur[1].numel() < n_counters:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("radhip attention: split-backward workspace must be allocated before graph capture")
         cur = (torch.empty(max(n_floats, cur[0].numel() if cur else 0), dtype=torch.float32, device=dev),
                torch.zeros(max(n_counters, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
-        _ATTN_WS[dev.index] = cur
+        _ATTN_WS[key] = cur
     return cur
 
 
@@ -1372,11 +1373,11 @@ _WG_WS = {}
 
 def _wgemm_workspace(dev, ws_bytes, n_counters):
     """Split-K workspace of csrc/wgemm.hip: fp32 partial slabs and per-tile arrival tickets (zeroed once here;
-    the last arriver re-zeroes its ticket). One per device: every split-K launch of the product is on the
-    encoder's compute stream, one after another (graph replays included), and two launches in flight at once
-    must not share a workspace. Grown outside graph capture only: the first launch of every shape happens in
-    the eager warm-up."""
-    key = dev.index
+    the last arriver re-zeroes its ticket). One per (device, stream): launches on one stream run one after
+    another (graph replays included), while two launches in flight at once on different streams (the SincNet
+    side stream, SideLinear's) must not share slabs or tickets. Grown outside graph capture only: the first
+    launch of every shape on a stream happens in the eager warm-up."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     cur = _WG_WS.get(key)
     if cur is None or cur[0].numel() < ws_bytes or cur[1].numel() < n_counters:
         if torch.cuda.is_current_stream_capturing():

@@ -22,7 +22,9 @@ OPS = {
     "wgemm": r"wgemm_kernel<", "b0x_bwd": r"b0x_bwd_kernel", "b0x_fwd": r"b0x_fwd_kernel",
     "sconv_fwd": r"sconv_fwd_kernel<\d+, \d+, \d+, false>", "sconv_dgrad_bnselu": r"sconv_fwd_kernel<\d+, \d+, \d+, true>",
     "sconv_wgrad": r"sconv_wgrad_kernel<", "attn_fwd": r"attn_fwd_kernel<", "attn_bwd": r"attn_bwd_fused_kernel<",
-    "selective_scan_fwd": r"scan_fwd_seg_kernel<", "selective_scan_bwd": r"scan_bwd_kernel<",
+    "selective_scan_fwd": r"scan_fwd_seg_kernel<|s2::fwd_chunk_kernel<|s2::fwd_out_kernel<",
+    "selective_scan_bwd": r"[^_]scan_bwd_kernel<|s2::bwd_chunk_kernel<|s2::bwd_out_kernel<",
+    "pgemm": r"pgemm_kernel<", "sincconv_mfma": r"sincconv_mfma_kernel",
     "wgrad_acc": r"wgrad_part_kernel|wgrad_reduce_kernel", "posconv_fwd": r"posconv_kernel<false>",
     "posconv_bwd": r"posconv_kernel<true>", "sincconv_absmaxpool": r"sincconv_absmaxpool_kernel",
     "fe_conv_gemm": r"gemm_nt_kernel|strided_gemm", "layer_wsum_fwd": r"lws_fwd_kernel", "layer_wsum_bwd": r"lws_bwd_kernel",
@@ -57,8 +59,9 @@ def main(d):
         wk = [v for n, v in write.values() if rx.search(n)]
         if not fk or not wk:
             continue
-        # wgrad_acc and similar two-kernel ops: count launches of the first kernel pattern only
-        first = re.compile(pat.split("|")[0])
+        # wgrad_acc, scan2 and similar two-kernel ops: count launches of the first alternative that occurs
+        alts = [re.compile(a) for a in pat.split("|")]
+        first = next(a for a in alts if any(a.search(n) for n, _ in fetch.values()))
         nl = max(1, sum(1 for n, _ in fetch.values() if first.search(n)))
         f_b = 2 * 1024 * sum(fk) / nl
         w_b = 1024 * sum(wk) / max(1, sum(1 for n, _ in write.values() if first.search(n)))
