@@ -30,10 +30,7 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
-typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 bf16x4v;
-typedef __attribute__((address_space(3))) bf16x4v lds_bf16x4v;
 constexpr int AT_DH = 64;                  // head dim
 constexpr int AT_TILE = 32;                // rows per wave
 constexpr int AT_MAXNT = 8;                // tiles per sequence: T <= 256
@@ -56,26 +53,26 @@ __device__ uint64_t rdx_probe[1 << 16];
   } while (0)
 #endif
 
-__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x16 mfma32(hx8 a, hx8 b, f32x16 c) {
+  return mfma32x32x16(a, b, c);
 }
 // C/D row held in accumulator register i by lane half h
 __device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-__device__ __forceinline__ bf16x8 pack8(const float* x) {
-  bf16x8 r;
+__device__ __forceinline__ hx8 pack8(const float* x) {
+  hx8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[j];
+  for (int j = 0; j < 8; ++j) r[j] = (hel)x[j];
   return r;
 }
-__device__ __forceinline__ bf16x8 load8(const __hip_bfloat16* p, bool ok) {
+__device__ __forceinline__ hx8 load8(const hst* p, bool ok) {
   if (!ok) {
-    bf16x8 z;
+    hx8 z;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+    for (int j = 0; j < 8; ++j) z[j] = (hel)0.f;
     return z;
   }
-  return *reinterpret_cast<const bf16x8*>(p);
+  return *reinterpret_cast<const hx8*>(p);
 }
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
@@ -117,32 +114,32 @@ __device__ __forceinline__ int img_off(int row, int ch) {
 
 // rows [0, 32 nt) of the head slice (columns col0 .. col0 + 63) of a [B, T, ld] bf16 tensor into an LDS
 // image; rows past T are zero. Every thread of the workgroup takes part.
-__device__ __forceinline__ void stage_image(char* img, const __hip_bfloat16* src, int64_t ld, int b, int T,
+__device__ __forceinline__ void stage_image(char* img, const hst* src, int64_t ld, int b, int T,
                                             int64_t col0, int nt, int nthreads = AT_WAVES * 64) {
   for (int i = threadIdx.x; i < nt * AT_TILE * 8; i += nthreads) {
     const int row = i >> 3, ch = i & 7;
-    *reinterpret_cast<bf16x8*>(img + img_off(row, ch)) =
+    *reinterpret_cast<hx8*>(img + img_off(row, ch)) =
         load8(src + ((int64_t)b * T + row) * ld + col0 + 8 * ch, row < T);
   }
 }
 // fragment along a row: element j = X[row][16 s + 8 h + j]
-__device__ __forceinline__ bf16x8 read_row(const char* img, int row, int s, int h) {
-  return *reinterpret_cast<const bf16x8*>(img + img_off(row, 2 * s + h));
+__device__ __forceinline__ hx8 read_row(const char* img, int row, int s, int h) {
+  return *reinterpret_cast<const hx8*>(img + img_off(row, 2 * s + h));
 }
 // fragment down a column in the k order of an accumulator fed back as an operand:
 //   element j = X[r0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)][c0 + (lane & 31)].
 // Each ds_read_b64_tr_b16 gives 16-lane group g the 4 x 16 block at rows r0 + 16 s + 4 (g >> 1) (+ 8 for
 // elements 4..7), columns c0 + 16 (g & 1) .. + 15, column-major (lane i of the group gets column i, row q in
 // element q); lane 4q + p of the group supplies the address of row q, columns 4p .. 4p + 3.
-__device__ __forceinline__ bf16x8 read_tr(char* img, int r0, int c0, int s, int lane) {
+__device__ __forceinline__ hx8 read_tr(char* img, int r0, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = r0 + 16 * s + 4 * (g >> 1) + (i >> 2);
   const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
   const int sub = 2 * (col & 7);  // 0 or 8 bytes into the chunk
-  const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)(img + img_off(row, col >> 3) + sub));
-  const bf16x4v hi =
-      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)(img + img_off(row + 8, col >> 3) + sub));
-  bf16x8 r;
+  const hx4v lo = ds_tr4((img + img_off(row, col >> 3) + sub));
+  const hx4v hi =
+      ds_tr4((img + img_off(row + 8, col >> 3) + sub));
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = lo[j];
@@ -152,7 +149,7 @@ __device__ __forceinline__ bf16x8 read_tr(char* img, int r0, int c0, int s, int 
 }
 
 struct AttnArgs {
-  const __hip_bfloat16 *q, *k, *v;
+  const hst *q, *k, *v;
   int64_t ldq, ldk, ldv;
   const float* gate;  // [B, T, H]
   const float* rel;   // [H, 2T - 1] relative-position bias table
@@ -165,7 +162,7 @@ struct AttnArgs {
 };
 
 struct AttnBwdArgs {
-  const __hip_bfloat16* dO;
+  const hst* dO;
   int64_t lddo;
   const float* lse;  // [B, H, T]
   float* D;          // [B, H, T]: written by the dQ kernel, read by the dK/dV kernel
@@ -204,7 +201,7 @@ constexpr int AT_MERGE_STRIDE = 2 * 16 + 2;   // floats per lane: O^T (2 x 16), 
 template <bool kSplit>
 constexpr int at_fwd_threads() { return (kSplit ? 2 : 1) * AT_WAVES * 64; }
 template <bool kDrop, bool kIdx32, bool kSplit>
-__global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(AttnArgs a, __hip_bfloat16* __restrict__ o,
+__global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(AttnArgs a, hst* __restrict__ o,
                                                                  int64_t ldo, float* __restrict__ lse,
                                                                  uint32_t* __restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) char at_lds[];
@@ -232,7 +229,7 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
   f32x16 oacc[2] = {zero16(), zero16()};
   const int64_t bh = (int64_t)b * H + head;
   if (active) {
-    bf16x8 qf[4];
+    hx8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = load8(a.q + ((int64_t)b * T + qc) * a.ldq + col0 + 16 * s + 8 * hh, qvalid);
     const float g2 = a.gate[((int64_t)b * T + qc) * H + head] * kLog2e;   // base-2 domain: exp2 of log2e-scaled scores
@@ -282,7 +279,7 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = pack8(sv + 8 * s);
+        const hx8 pf = pack8(sv + 8 * s);
 #pragma unroll
         for (int db = 0; db < 2; ++db) oacc[db] = mfma32(read_tr(Vs, kb * AT_TILE, db * 32, s, lane), pf, oacc[db]);
       }
@@ -317,11 +314,11 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
   }
   if (qvalid) {
     const float inv = 1.f / l;
-    __hip_bfloat16* orow = o + ((int64_t)b * T + qi) * ldo + col0;
+    hst* orow = o + ((int64_t)b * T + qi) * ldo + col0;
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) orow[db * 32 + crow(i, hh)] = __float2bfloat16(oacc[db][i] * inv);
+      for (int i = 0; i < 16; ++i) orow[db * 32 + crow(i, hh)] = f2h(oacc[db][i] * inv);
     if (hh == 0) lse[bh * T + qi] = (m + __log2f(l)) * 0.69314718055994531f;  // natural-log LSE
   }
 }
@@ -329,8 +326,8 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
 // query-stationary: dQ, d gate and D = rowsum(dO o O) of the wave's 32 query rows
 template <bool kDrop>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArgs g,
-                                                          const __hip_bfloat16* __restrict__ O, int64_t ldo,
-                                                          __hip_bfloat16* __restrict__ dq, int64_t ldg,
+                                                          const hst* __restrict__ O, int64_t ldo,
+                                                          hst* __restrict__ dq, int64_t ldg,
                                                           float* __restrict__ dgate) {
   extern __shared__ __attribute__((aligned(16))) char at_lds[];
   const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE;
@@ -350,13 +347,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArg
   const bool qvalid = qi < T;
   const int qc = qvalid ? qi : T - 1;
   const int64_t trow = (int64_t)b * T + qc;
-  bf16x8 qf[4], dof[4];
+  hx8 qf[4], dof[4];
   float dpart = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     qf[s] = load8(a.q + trow * a.ldq + col0 + 16 * s + 8 * hh, qvalid);
     dof[s] = load8(g.dO + trow * g.lddo + col0 + 16 * s + 8 * hh, qvalid);
-    const bf16x8 of = load8(O + trow * ldo + col0 + 16 * s + 8 * hh, qvalid);
+    const hx8 of = load8(O + trow * ldo + col0 + 16 * s + 8 * hh, qvalid);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dpart = fmaf((float)dof[s][j], (float)of[j], dpart);
   }
@@ -392,18 +389,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArg
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8 xs = pack8(dS + 8 * s);
+      const hx8 xs = pack8(dS + 8 * s);
 #pragma unroll
       for (int db = 0; db < 2; ++db) dqacc[db] = mfma32(read_tr(Ks, kb * AT_TILE, db * 32, s, lane), xs, dqacc[db]);
     }
   }
   dg += __shfl_xor(dg, 32, 64);
   if (qvalid) {
-    __hip_bfloat16* row = dq + ((int64_t)b * T + qi) * ldg + col0;
+    hst* row = dq + ((int64_t)b * T + qi) * ldg + col0;
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) row[db * 32 + crow(i, hh)] = __float2bfloat16(dqacc[db][i] * a.scale);
+      for (int i = 0; i < 16; ++i) row[db * 32 + crow(i, hh)] = f2h(dqacc[db][i] * a.scale);
     if (hh == 0) dgate[((int64_t)b * T + qi) * H + head] = dg;
   }
 }
@@ -411,8 +408,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a, AttnBwdArg
 // key-stationary: dK and dV of the wave's 32 keys
 template <bool kDrop>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdArgs g,
-                                                            __hip_bfloat16* __restrict__ dk,
-                                                            __hip_bfloat16* __restrict__ dv, int64_t ldg) {
+                                                            hst* __restrict__ dk,
+                                                            hst* __restrict__ dv, int64_t ldg) {
   extern __shared__ __attribute__((aligned(16))) char at_lds[];
   const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE, tp = nt * AT_TILE;
   const int head = blockIdx.y, b = blockIdx.z;
@@ -439,7 +436,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdA
   if (kb >= nt) return;
   const int key = kb * AT_TILE + r;  // this lane's key column
   const bool kvalid = key < T;
-  bf16x8 kf[4], vf[4];
+  hx8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     kf[s] = load8(a.k + ((int64_t)b * T + key) * a.ldk + col0 + 16 * s + 8 * hh, kvalid);
@@ -485,7 +482,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdA
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8 xp = pack8(P + 8 * s), xs = pack8(dS + 8 * s);
+      const hx8 xp = pack8(P + 8 * s), xs = pack8(dS + 8 * s);
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
         dvacc[db] = mfma32(xp, read_tr(dOs, qb * AT_TILE, db * 32, s, lane), dvacc[db]);
@@ -501,8 +498,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a, AttnBwdA
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
         const int64_t off = ((int64_t)b * T + kk) * ldg + col0 + db * 32 + r;
-        dk[off] = __float2bfloat16(dkacc[db][i] * a.scale);
-        dv[off] = __float2bfloat16(dvacc[db][i]);
+        dk[off] = f2h(dkacc[db][i] * a.scale);
+        dv[off] = f2h(dvacc[db][i]);
       }
     }
   }
@@ -529,14 +526,14 @@ __device__ __forceinline__ int pan_off(int row, int ch) {
   return 512 * (row >> 3) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 // read_tr on a 32-column panel: element j = X[r0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)][lane & 31]
-__device__ __forceinline__ bf16x8 read_tr_pan(char* pan, int r0, int s, int lane) {
+__device__ __forceinline__ hx8 read_tr_pan(char* pan, int r0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = r0 + 16 * s + 4 * (g >> 1) + (i >> 2);
   const int col = 16 * (g & 1) + 4 * (i & 3);
   const int sub = 2 * (col & 7);
-  const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)(pan + pan_off(row, col >> 3) + sub));
-  const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)(pan + pan_off(row + 8, col >> 3) + sub));
-  bf16x8 r;
+  const hx4v lo = ds_tr4((pan + pan_off(row, col >> 3) + sub));
+  const hx4v hi = ds_tr4((pan + pan_off(row + 8, col >> 3) + sub));
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = lo[j];
@@ -568,11 +565,11 @@ __device__ __forceinline__ int fb_pan_off(int lane, int hi) {
   const int row = 4 * (g >> 1) + (i >> 2) + 8 * hi, col = 16 * (g & 1) + 4 * (i & 3);
   return pan_off(row, col >> 3) + 2 * (col & 7);
 }
-__device__ __forceinline__ bf16x8 lds8(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
-__device__ __forceinline__ bf16x8 lds_tr(const char* lo, const char* hi) {
-  const bf16x4v a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)lo);
-  const bf16x4v b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4v*)hi);
-  bf16x8 r;
+__device__ __forceinline__ hx8 lds8(const char* p) { return *reinterpret_cast<const hx8*>(p); }
+__device__ __forceinline__ hx8 lds_tr(const char* lo, const char* hi) {
+  const hx4v a = ds_tr4(lo);
+  const hx4v b = ds_tr4(hi);
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = a[j];
@@ -590,8 +587,8 @@ constexpr int FB_WSP = AT_FUSED_MAXNT * AT_TILE * (AT_DH + 1);   // fp32 per (b,
 template <bool kDrop, bool kSplit = false>
 __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     AttnArgs a, AttnBwdArgs g, const uint32_t* __restrict__ mask,
-    const __hip_bfloat16* __restrict__ O, int64_t ldo,
-    __hip_bfloat16* __restrict__ dq, __hip_bfloat16* __restrict__ dk, __hip_bfloat16* __restrict__ dv, int64_t ldg,
+    const hst* __restrict__ O, int64_t ldo,
+    hst* __restrict__ dq, hst* __restrict__ dk, hst* __restrict__ dv, int64_t ldg,
     float* __restrict__ dgate, float* __restrict__ ws, int* __restrict__ counters) {
   extern __shared__ __attribute__((aligned(16))) char at_lds[];
   char* const L = at_lds;
@@ -632,9 +629,9 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
   const bool kact = kb < kend;       // this wave has a key tile in phase 1
   const int key = kb * AT_TILE + r;
   const bool kvalid = kact && key < T;
-  bf16x8 kf[4], vf[4];
+  hx8 kf[4], vf[4];
   {
-    bf16x8 qv[4], ov[4], xo[8];
+    hx8 qv[4], ov[4], xo[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = threadIdx.x + j * nthr, row = i >> 3, ch = i & 7;
@@ -658,8 +655,8 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = threadIdx.x + j * nthr, row = i >> 3, ch = i & 7;
-      *reinterpret_cast<bf16x8*>(L + FB_Q + img_off(row, ch)) = qv[j];
-      *reinterpret_cast<bf16x8*>(L + FB_DO + img_off(row, ch)) = ov[j];
+      *reinterpret_cast<hx8*>(L + FB_Q + img_off(row, ch)) = qv[j];
+      *reinterpret_cast<hx8*>(L + FB_DO + img_off(row, ch)) = ov[j];
     }
     if (t < tp) {
       s_gate[t] = gq;
@@ -672,7 +669,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
       float dd = 0.f;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const bf16x8 xd = lds8(L + FB_DO + img_off(t, c));
+        const hx8 xd = lds8(L + FB_DO + img_off(t, c));
 #pragma unroll
         for (int j = 0; j < 8; ++j) dd = fmaf((float)xd[j], (float)xo[c][j], dd);
       }
@@ -752,7 +749,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
       char* pan = L + qb * tp * 64;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 xp = pack8(P + 8 * s), xs = pack8(dS + 8 * s);
+        const hx8 xp = pack8(P + 8 * s), xs = pack8(dS + 8 * s);
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
           const int o = 2048 * s + 512 * db;
@@ -762,10 +759,10 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
         // dS rows crow(8s + 4t + e, hh) = 16 s + 8 t + 4 hh + e of the query panel -> [key][q] image
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          bf16x4v v4;
+          hx4v v4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v4[e] = xs[4 * t + e];
-          *reinterpret_cast<bf16x4v*>(pan + dso[2 * s + t]) = v4;
+          *reinterpret_cast<hx4v*>(pan + dso[2 * s + t]) = v4;
         }
       }
     }
@@ -777,8 +774,8 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
           const int64_t off = (row0 + kk) * ldg + col0 + db * 32 + r;
-          dk[off] = __float2bfloat16(dkacc[db][i] * a.scale);
-          dv[off] = __float2bfloat16(dvacc[db][i]);
+          dk[off] = f2h(dkacc[db][i] * a.scale);
+          dv[off] = f2h(dvacc[db][i]);
         }
       }
     }
@@ -791,7 +788,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
   __syncthreads();  // every dS panel is complete; the Q image is free
   if (kact) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(L + FB_Q + img_off(kb * AT_TILE + r, 2 * s + hh)) = kf[s];
+    for (int s = 0; s < 4; ++s) *reinterpret_cast<hx8*>(L + FB_Q + img_off(kb * AT_TILE + r, 2 * s + hh)) = kf[s];
   }
   __syncthreads();
   RDX_PROBE(3);
@@ -817,7 +814,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int po = 2048 * kb2 + 1024 * s;
-        const bf16x8 xs = lds_tr(P0 + po, P1 + po);  // dS[qi][keys of step s]
+        const hx8 xs = lds_tr(P0 + po, P1 + po);  // dS[qi][keys of step s]
 #pragma unroll
         for (int j = 0; j < 8; ++j) dg = fmaf((float)xs[j], pbv[8 * s + j], dg);
 #pragma unroll
@@ -849,7 +846,7 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
         if (qq < T) {
 #pragma unroll
           for (int db = 0; db < 2; ++db)
-            dq[(row0 + qq) * ldg + col0 + db * 32 + r] = __float2bfloat16(dqacc[db][i] * a.scale);
+            dq[(row0 + qq) * ldg + col0 + db * 32 + r] = f2h(dqacc[db][i] * a.scale);
         }
       }
     }
@@ -879,11 +876,11 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
         const int qq = i / (AT_DH / 4), c4 = (i - qq * (AT_DH / 4)) * 4;
         const float4 x0 = *reinterpret_cast<const float4*>(w0 + qq * AT_DH + c4);
         const float4 x1 = *reinterpret_cast<const float4*>(w1 + qq * AT_DH + c4);
-        __hip_bfloat16* dst = dq + (row0 + qq) * ldg + col0 + c4;
-        dst[0] = __float2bfloat16((x0.x + x1.x) * a.scale);
-        dst[1] = __float2bfloat16((x0.y + x1.y) * a.scale);
-        dst[2] = __float2bfloat16((x0.z + x1.z) * a.scale);
-        dst[3] = __float2bfloat16((x0.w + x1.w) * a.scale);
+        hst* dst = dq + (row0 + qq) * ldg + col0 + c4;
+        dst[0] = f2h((x0.x + x1.x) * a.scale);
+        dst[1] = f2h((x0.y + x1.y) * a.scale);
+        dst[2] = f2h((x0.z + x1.z) * a.scale);
+        dst[3] = f2h((x0.w + x1.w) * a.scale);
       }
       for (int t = threadIdx.x; t < T; t += nthr)
         dgate[(row0 + t) * H + head] = w0[AT_FUSED_MAXNT * AT_TILE * AT_DH + t] + w1[AT_FUSED_MAXNT * AT_TILE * AT_DH + t];
@@ -915,9 +912,9 @@ inline AttnArgs make_args(const void* q, int64_t ldq, const void* k, int64_t ldk
                           const float* gate, const float* rel, const int64_t* seed_dev, int salt,
                           float p_drop, float scale, int B, int T, int H) {
   AttnArgs a;
-  a.q = (const __hip_bfloat16*)q;
-  a.k = (const __hip_bfloat16*)k;
-  a.v = (const __hip_bfloat16*)v;
+  a.q = (const hst*)q;
+  a.k = (const hst*)k;
+  a.v = (const hst*)v;
   a.ldq = ldq;
   a.ldk = ldk;
   a.ldv = ldv;
@@ -959,7 +956,7 @@ static int attn_allow_lds(const void* fn, bool& done) {
 }
 
 template <bool kDrop, bool kIdx32, bool kSplit>
-static int launch_fwd(dim3 grid, size_t lds, hipStream_t st, const AttnArgs& a, __hip_bfloat16* o, int64_t ldo,
+static int launch_fwd(dim3 grid, size_t lds, hipStream_t st, const AttnArgs& a, hst* o, int64_t ldo,
                       float* lse, uint32_t* mask) {
   static bool done = false;
   const int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_fwd_kernel<kDrop, kIdx32, kSplit>), done);
@@ -973,8 +970,8 @@ static int launch_fwd(dim3 grid, size_t lds, hipStream_t st, const AttnArgs& a, 
 
 template <bool kDrop>
 static int launch_bwd(dim3 grid, size_t lds_dq, size_t lds_kv, hipStream_t st, const AttnArgs& a,
-                      const AttnBwdArgs& g, const __hip_bfloat16* o, int64_t ldo, __hip_bfloat16* dq,
-                      __hip_bfloat16* dk, __hip_bfloat16* dv, int64_t ldg, float* dgate) {
+                      const AttnBwdArgs& g, const hst* o, int64_t ldo, hst* dq,
+                      hst* dk, hst* dv, int64_t ldg, float* dgate) {
   static bool done_dq = false, done_kv = false;
   int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<kDrop>), done_dq);
   if (rc != RDX_OK) return rc;
@@ -1000,7 +997,7 @@ extern "C" int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t l
   const dim3 grid((nt + AT_WAVES - 1) / AT_WAVES, H, B);
   const size_t lds = 2 * (size_t)nt * AT_TILE_BYTES + rel_bytes(T);
   hipStream_t st = as_stream(stream);
-  __hip_bfloat16* ob = (__hip_bfloat16*)o;
+  hst* ob = (hst*)o;
   // key-split kernel while the unsplit grid is at most 2 workgroups per CU (one wave per SIMD each)
   const bool split = (int64_t)grid.x * grid.y * grid.z <= 512;
   if (!a.thr)
@@ -1030,15 +1027,15 @@ extern "C" int rdx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
   RDX_REQUIRE(p_drop >= 0.f && p_drop < 1.f && (p_drop == 0.f || seed_dev));
   if (head_dim != AT_DH || T > AT_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
   const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, rel_bias, seed_dev, salt, p_drop, scale, B, T, H);
-  const AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
+  const AttnBwdArgs g{(const hst*)dout, lddo, lse, D};
   const int nt = (T + AT_TILE - 1) / AT_TILE;
   const dim3 grid((nt + AT_WAVES - 1) / AT_WAVES, H, B);
   const size_t lds_dq = 2 * (size_t)nt * AT_TILE_BYTES + rel_bytes(T);
   const size_t lds_kv = 2 * (size_t)nt * AT_TILE_BYTES + 3 * (size_t)nt * AT_TILE * sizeof(float) + rel_bytes(T);
-  return a.thr ? launch_bwd<true>(grid, lds_dq, lds_kv, as_stream(stream), a, g, (const __hip_bfloat16*)o, ldo,
-                                  (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg, dgate)
-               : launch_bwd<false>(grid, lds_dq, lds_kv, as_stream(stream), a, g, (const __hip_bfloat16*)o, ldo,
-                                   (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg, dgate);
+  return a.thr ? launch_bwd<true>(grid, lds_dq, lds_kv, as_stream(stream), a, g, (const hst*)o, ldo,
+                                  (hst*)dq, (hst*)dk, (hst*)dv, ldg, dgate)
+               : launch_bwd<false>(grid, lds_dq, lds_kv, as_stream(stream), a, g, (const hst*)o, ldo,
+                                   (hst*)dq, (hst*)dk, (hst*)dv, ldg, dgate);
 }
 
 template <bool kDrop, bool kSplit>
@@ -1049,7 +1046,7 @@ static int launch_bwd_fused(dim3 grid, dim3 block, size_t lds, hipStream_t st, c
   const int rc = attn_allow_lds(reinterpret_cast<const void*>(&attn_bwd_fused_kernel<kDrop, kSplit>), done);
   if (rc != RDX_OK) return rc;
   hipLaunchKernelGGL((attn_bwd_fused_kernel<kDrop, kSplit>), grid, block, lds, st, a, g, mask,
-                     (const __hip_bfloat16*)o, ldo, (__hip_bfloat16*)dq, (__hip_bfloat16*)dk, (__hip_bfloat16*)dv, ldg,
+                     (const hst*)o, ldo, (hst*)dq, (hst*)dk, (hst*)dv, ldg,
                      dgate, ws, counters);
   return RDX_OK;
 }
@@ -1067,7 +1064,7 @@ extern "C" int rdx_attn_bwd_fused(const void* q, int64_t ldq, const void* k, int
   RDX_REQUIRE((int64_t)B * H <= 0x7fffffff);
   if (head_dim != AT_DH || T > AT_FUSED_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
   const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, rel_bias, nullptr, 0, p_drop, scale, B, T, H);
-  const AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
+  const AttnBwdArgs g{(const hst*)dout, lddo, lse, D};
   const int nt = (T + AT_TILE - 1) / AT_TILE, tp = nt * AT_TILE;
   const size_t lds = FB_LDS;   // fixed map (immediate-offset LDS addressing)
   const dim3 grid((unsigned)(B * H)), block(nt * 64);
@@ -1100,7 +1097,7 @@ extern "C" int rdx_attn_bwd_fused_split(const void* q, int64_t ldq, const void* 
   RDX_REQUIRE(((int64_t)B * H) % 8 == 0 && (int64_t)B * H * 2 <= 0x7fffffff);   // the block -> part map
   if (head_dim != AT_DH || T > AT_FUSED_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
   const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, rel_bias, nullptr, 0, p_drop, scale, B, T, H);
-  const AttnBwdArgs g{(const __hip_bfloat16*)dout, lddo, lse, D};
+  const AttnBwdArgs g{(const hst*)dout, lddo, lse, D};
   const int nt = (T + AT_TILE - 1) / AT_TILE;
   const dim3 grid((unsigned)(2 * B * H)), block(nt * 64);
   hipStream_t st = as_stream(stream);

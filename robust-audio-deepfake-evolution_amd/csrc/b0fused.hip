@@ -22,7 +22,6 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bxbf16x8;
 typedef __attribute__((ext_vector_type(16))) float bxf32x16;
 
 constexpr float BX_SELU_ALPHA = 1.6732632423543772848170429916717f;
@@ -40,17 +39,16 @@ constexpr int BX_LDS = 192 * 64 + 3 * BX_IMG + 4 * BX_XW * 4 + 128 * BX_SP * 4 +
 __device__ __forceinline__ float bx_selu(float u) {
   return BX_SELU_SCALE * (u > 0.f ? u : BX_SELU_ALPHA * (__expf(u) - 1.0f));
 }
-__device__ __forceinline__ float bx_bf16(float x) { return __bfloat162float(__float2bfloat16(x)); }
 __device__ __forceinline__ uint32_t bx_pack2(float a, float b) {
-  return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(a)) | ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(b)) << 16);
+  return (uint32_t)hbits_of(f2h(a)) | ((uint32_t)hbits_of(f2h(b)) << 16);
 }
 // [row][32] bf16 image: 8-row x 32-channel subtiles of 512 B, the 16-byte chunk XOR-swizzled by (row >> 2) & 3
 // (csrc/sconv.hip sc_img<32>)
 __device__ __forceinline__ int bx_img(int row, int ch) {
   return 512 * (row >> 3) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
-__device__ __forceinline__ float bx_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bx_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float bx_lo(uint32_t u) { return hlo(u); }
+__device__ __forceinline__ float bx_hi(uint32_t u) { return hhi(u); }
 
 // Two channels at once on the packed fp32 VALU (v_pk_fma / v_pk_mul / v_pk_add: per component the same IEEE
 // operations, so the results keep the scalar code's bits): conv1's pre-activation c (the unfused kernel's FMA
@@ -68,13 +66,13 @@ __device__ __forceinline__ bxf2 bx_conv1_pair(const float (&v0)[3], const float 
 }
 
 struct BxFwdArgs {
-  const __hip_bfloat16* x;   // [N, H, W] (the one input channel)
+  const hst* x;   // [N, H, W] (the one input channel)
   const float* w1;           // [32][6] conv1 weights as autocast rounds them (bf16 values), tap kh * 3 + kw
   const float* wd;           // [32][3] conv_downsample weights (bf16 values)
   const float* bn;           // [4][32]: conv1 bias, running mean, invstd * gamma, beta
-  const __hip_bfloat16* w2;  // [6][32 co][32 ci] conv2 weights, tap-major
+  const hst* w2;  // [6][32 co][32 ci] conv2 weights, tap-major
   const float* bias;         // [32] conv2.bias + conv_downsample.bias
-  __hip_bfloat16* y;         // [N, H, Wo, 32] pooled output (NHWC)
+  hst* y;         // [N, H, Wo, 32] pooled output (NHWC)
   uint8_t* arg;              // [N, H, Wo, 32] window argmax (0..2)
   int N, H, W, Wo, rows_per;
 };
@@ -130,7 +128,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
     sg[k] = a.bn[2 * BX_C + co];
     sh[k] = a.bn[3 * BX_C + co];
   }
-  const __hip_bfloat16* xn_base = a.x + (int64_t)n * H * W;
+  const hst* xn_base = a.x + (int64_t)n * H * W;
   // x[row][q0 - 2 + tid] as raw bf16 bits from a clamped (always valid) address: no branch around the load, so
   // its wait falls where the value is stored (x_val), after the row's MFMAs
   auto x_raw = [&](int row) -> uint32_t {
@@ -141,7 +139,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   };
   auto x_val = [&](int row, uint32_t raw) -> float {   // zero outside the image
     const int q = q0 - 2 + tid;
-    return (row >= 0 && row < H && q >= 0 && q < W) ? __uint_as_float(raw << 16) : 0.f;
+    return (row >= 0 && row < H && q >= 0 && q < W) ? hlo(raw) : 0.f;
   };
   auto xslot = [&](int row) -> float* { return xr + (row & 3) * BX_XW; };
   auto oslot = [&](int row) -> char* { return os + (row % 3) * BX_IMG; };
@@ -166,7 +164,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
           acc = fmaf(v1[0], t1[k + e][3], acc);
           acc = fmaf(v1[1], t1[k + e][4], acc);
           acc = fmaf(v1[2], t1[k + e][5], acc);
-          const float cv = bx_bf16(acc);
+          const float cv = hround(acc);
           yv[e] = bx_selu(fmaf((cv + cb[k + e]) - mu[k + e], sg[k + e], sh[k + e]));
         }
         o[k >> 1] = (q >= 0 && q < W) ? bx_pack2(yv[0], yv[1]) : 0u;
@@ -203,9 +201,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
       for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const bxbf16x8 xf = *reinterpret_cast<const bxbf16x8*>(xk + bx_img(pw + kw, 2 * s + hh));
-          const bxbf16x8 wf = *reinterpret_cast<const bxbf16x8*>(ws + bx_img((kh * 3 + kw) * BX_C + r, 2 * s + hh));
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf, acc, 0, 0, 0);   // Y^T: rows co, columns positions
+          const hx8 xf = *reinterpret_cast<const hx8*>(xk + bx_img(pw + kw, 2 * s + hh));
+          const hx8 wf = *reinterpret_cast<const hx8*>(ws + bx_img((kh * 3 + kw) * BX_C + r, 2 * s + hh));
+          acc = mfma32x32x16(wf, xf, acc);   // Y^T: rows co, columns positions
         }
     }
     BXF_STAMP(0);
@@ -220,9 +218,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = 8 * g + 4 * hh + e;
-          const float av = bx_bf16(acc[4 * g + e]);
+          const float av = hround(acc[4 * g + e]);
           const float4 pr = prec[co];
-          const float iv = bx_bf16(fmaf(x0, pr.x, fmaf(x1, pr.y, x2 * pr.z)));
+          const float iv = hround(fmaf(x0, pr.x, fmaf(x1, pr.y, x2 * pr.z)));
           o[e] = av + iv + pr.w;
         }
         *reinterpret_cast<float4*>(ss + pw * BX_SP + 8 * g + 4 * hh) = make_float4(o[0], o[1], o[2], o[3]);
@@ -289,7 +287,7 @@ extern "C" int rdx_b0x_fwd(const void* x, const float* w1, const float* wd, cons
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  BxFwdArgs a{(const __hip_bfloat16*)x, w1, wd, bn, (const __hip_bfloat16*)w2, bias, (__hip_bfloat16*)y, arg,
+  BxFwdArgs a{(const hst*)x, w1, wd, bn, (const hst*)w2, bias, (hst*)y, arg,
               N, H, W, Wo, rows_per};
   hipLaunchKernelGGL(b0x_fwd_kernel, dim3((unsigned)strips, (unsigned)N, (unsigned)nz), dim3(BX_T), BX_LDS,
                      as_stream(stream), a);
@@ -339,18 +337,16 @@ constexpr int BXB_LDS = 192 * 64 + 3 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 
 constexpr int BXB_BLOCKS = 512;
 static_assert(2 * BXB_LDS <= 160 * 1024, "two workgroups per CU");
 
-typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 bxbf16x4v;
-typedef __attribute__((address_space(3))) bxbf16x4v lds_bxbf16x4v;
 
 // MFMA operand running down a column of a bx_img image (K = positions), csrc/sconv.hip sc_read_tr<32>
-__device__ __forceinline__ bxbf16x8 bx_read_tr(const char* img, int r0, int s, int lane) {
+__device__ __forceinline__ hx8 bx_read_tr(const char* img, int r0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = r0 + 16 * s + 4 * (g >> 1) + (i >> 2);
   const int col = 16 * (g & 1) + 4 * (i & 3);
   const int sub = 2 * (col & 7);
-  const bxbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + bx_img(row, col >> 3) + sub));
-  const bxbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + bx_img(row + 8, col >> 3) + sub));
-  bxbf16x8 r;
+  const hx4v lo = ds_tr4((img + bx_img(row, col >> 3) + sub));
+  const hx4v hi = ds_tr4((img + bx_img(row + 8, col >> 3) + sub));
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = lo[j];
@@ -367,10 +363,10 @@ __device__ __forceinline__ int2 bx_tr_off(int r0, int lane) {
   const int sub = 2 * (col & 7);
   return make_int2(bx_img(row, col >> 3) + sub, bx_img(row + 8, col >> 3) + sub);
 }
-__device__ __forceinline__ bxbf16x8 bx_read_tr_at(const char* img, int2 off, int s) {
-  const bxbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + off.x + 1024 * s));
-  const bxbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bxbf16x4v*)(img + off.y + 1024 * s));
-  bxbf16x8 r;
+__device__ __forceinline__ hx8 bx_read_tr_at(const char* img, int2 off, int s) {
+  const hx4v lo = ds_tr4((img + off.x + 1024 * s));
+  const hx4v hi = ds_tr4((img + off.y + 1024 * s));
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = lo[j];
@@ -379,13 +375,13 @@ __device__ __forceinline__ bxbf16x8 bx_read_tr_at(const char* img, int2 off, int
   return r;
 }
 struct BxBwdArgs {
-  const __hip_bfloat16* x;    // [N, H, W]
-  const __hip_bfloat16* dp;   // [N, H, Wo, 32] pooled-output gradient
+  const hst* x;    // [N, H, W]
+  const hst* dp;   // [N, H, Wo, 32] pooled-output gradient
   const uint8_t* arg;         // [N, H, Wo, 32]
   const float* w1;            // [32][6]
   const float* wd;            // [32][3]
   const float* bn;            // [5][32]: conv1 bias, mean, invstd * gamma, beta, invstd
-  const __hip_bfloat16* w2f;  // [6][32 ci][32 co] conv2 weights flipped in both axes, transposed (input gradient)
+  const hst* w2f;  // [6][32 ci][32 co] conv2 weights flipped in both axes, transposed (input gradient)
   float* dx;                  // [N, H, W]
   float* part;                // [gridDim.x][BXB_NPART]: d w2 [6][32 co][32 ci], d w1 [32][6], d wd [32][3],
                               //   d bias [32], BN sums [3][32]
@@ -485,7 +481,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
   for (int64_t u = blockIdx.x; u < (int64_t)a.strips * a.N; u += gridDim.x) {
     const int strip = (int)(u % a.strips), n = (int)(u / a.strips);
     const int q0 = strip * BX_P;
-    const __hip_bfloat16* xn = a.x + (int64_t)n * H * W;
+    const hst* xn = a.x + (int64_t)n * H * W;
     // x row `row` at position q0 - 4 + tid: raw bf16 bits from a clamped (always valid) address, so the load
     // carries no branch and its wait falls where the row is stored (put_x), a phase or more later
     auto x_raw = [&](int row) -> uint32_t {
@@ -501,7 +497,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
       const int q = q0 - 4 + tid;
       const uint32_t b = (row >= 0 && row < H && q >= 0 && q < W) ? raw : 0u;
       if (tid < BXB_XW) {
-        xslot(row)[tid] = __uint_as_float(b << 16);
+        xslot(row)[tid] = hlo(b);
         char* xsr = xsslot(row);
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
@@ -591,9 +587,9 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
           for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-              const bxbf16x8 xf = *reinterpret_cast<const bxbf16x8*>(dk + bx_img(pw + kw, 2 * s + hh));
-              const bxbf16x8 wf = *reinterpret_cast<const bxbf16x8*>(wsf + (kh * 3 + kw) * 2048 + (s ? wo1 : wo0));
-              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf, acc, 0, 0, 0);
+              const hx8 xf = *reinterpret_cast<const hx8*>(dk + bx_img(pw + kw, 2 * s + hh));
+              const hx8 wf = *reinterpret_cast<const hx8*>(wsf + (kh * 3 + kw) * 2048 + (s ? wo1 : wo0));
+              acc = mfma32x32x16(wf, xf, acc);
             }
         }
         char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
@@ -611,14 +607,14 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         const int s1 = 4 * (wv & 1);
 #pragma unroll 2
         for (int s = 0; s < 8; ++s) {
-          bxbf16x8 av = bx_read_tr_at(dsi, off_ds, s);
+          hx8 av = bx_read_tr_at(dsi, off_ds, s);
           if (s == 7 && tail_lane) {
-            av[6] = (__bf16)0.0f;
-            av[7] = (__bf16)0.0f;
+            av[6] = (hel)0.0f;
+            av[7] = (hel)0.0f;
           }
-          acc2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr_at(oi0, offb0, s), acc2[0], 0, 0, 0);
+          acc2[0] = mfma32x32x16(av, bx_read_tr_at(oi0, offb0, s), acc2[0]);
           if (s >= s1 && s < s1 + 4)
-            acc2[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bx_read_tr_at(oi1, offb1, s), acc2[1], 0, 0, 0);
+            acc2[1] = mfma32x32x16(av, bx_read_tr_at(oi1, offb1, s), acc2[1]);
         }
       }
       __syncthreads();
@@ -711,10 +707,10 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
             for (int s = 0; s < 6; ++s) {
               const int img = s >> 1;
               const char* src = img == 0 ? dcA : (img == 1 ? dcB : dsP);
-              const bxbf16x8 bv =
-                  *reinterpret_cast<const bxbf16x8*>(src + bx_img(kp + (img == 2 ? 3 : 2), 2 * (s & 1) + hh));
-              const bxbf16x8 wa = *reinterpret_cast<const bxbf16x8*>(wdx + (r < 3 ? (s * 6 + hh * 3 + r) * 16 : 576));
-              o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, bv, o, 0, 0, 0);
+              const hx8 bv =
+                  *reinterpret_cast<const hx8*>(src + bx_img(kp + (img == 2 ? 3 : 2), 2 * (s & 1) + hh));
+              const hx8 wa = *reinterpret_cast<const hx8*>(wdx + (r < 3 ? (s * 6 + hh * 3 + r) * 16 : 576));
+              o = mfma32x32x16(wa, bv, o);
             }
             if (hh == 0) {   // D[m][n]: element i of lane n < 32 holds m = i for i < 3
               ob[kp + 2] = o[0];
@@ -729,19 +725,19 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) {
             const int s = 2 * wv + ss;
-            bxbf16x8 ac = bx_read_tr_at(dcA, off_dc, s), as = bx_read_tr_at(dsC, off_ds, s);
+            hx8 ac = bx_read_tr_at(dcA, off_dc, s), as = bx_read_tr_at(dsC, off_ds, s);
             if (s == 7 && tail_lane) {
-              ac[6] = ac[7] = as[6] = as[7] = (__bf16)0.0f;
+              ac[6] = ac[7] = as[6] = as[7] = (hel)0.0f;
             }
             const int kb = 2 * (16 * s + 4 * hh);
             const uint2 p1a = *reinterpret_cast<const uint2*>(xb1 + kb), p1b = *reinterpret_cast<const uint2*>(xb1 + kb + 16);
             const uint2 p2a = *reinterpret_cast<const uint2*>(xb2 + kb), p2b = *reinterpret_cast<const uint2*>(xb2 + kb + 16);
-            const uint32_t one2 = 0x3f803f80u;   // bf16 1.0 pair: the bias column
+            const uint32_t one2 = hpack2(1.f, 1.f);   // 1.0 pair: the bias column
             const uint4 w1v = r < 6 ? make_uint4(p1a.x, p1a.y, p1b.x, p1b.y) : make_uint4(0u, 0u, 0u, 0u);
             const uint4 w2v = (r >= 8 && r < 11) ? make_uint4(p2a.x, p2a.y, p2b.x, p2b.y)
                                                  : (r == 11 ? make_uint4(one2, one2, one2, one2) : make_uint4(0u, 0u, 0u, 0u));
-            accw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac, __builtin_bit_cast(bxbf16x8, w1v), accw, 0, 0, 0);
-            accw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as, __builtin_bit_cast(bxbf16x8, w2v), accw, 0, 0, 0);
+            accw = mfma32x32x16(ac, __builtin_bit_cast(hx8, w1v), accw);
+            accw = mfma32x32x16(as, __builtin_bit_cast(hx8, w2v), accw);
           }
         }
         // the next row's ds into the slot of row hp - 2 (read for the last time in phase B), its successor's fetch
@@ -820,7 +816,7 @@ extern "C" int rdx_b0x_bwd(const void* x, const void* dp, const uint8_t* arg, co
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  BxBwdArgs a{(const __hip_bfloat16*)x, (const __hip_bfloat16*)dp, arg, w1, wd, bn, (const __hip_bfloat16*)w2f,
+  BxBwdArgs a{(const hst*)x, (const hst*)dp, arg, w1, wd, bn, (const hst*)w2f,
               dx, part, N, H, W, W / 3, W / 3 / BX_J + 1};
   hipLaunchKernelGGL(b0x_bwd_kernel, dim3((unsigned)rdx_b0x_bwd_nblk(N, W)), dim3(BX_T), BXB_LDS, as_stream(stream),
                      a);

@@ -598,7 +598,7 @@ using namespace rdx;
       using T = float;                                              \
       __VA_ARGS__;                                                  \
     } else if ((dtype) == RDX_BF16) {                               \
-      using T = __hip_bfloat16;                                     \
+      using T = hst;                                     \
       __VA_ARGS__;                                                  \
     } else {                                                        \
       return RDX_EINVAL;                                            \
@@ -673,7 +673,7 @@ extern "C" int rdx_selective_scan_fwd(int dtype, const void* u, const void* delt
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_fwd_seg_kernel<float, 4>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e == hipSuccess)
-          e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_fwd_seg_kernel<__hip_bfloat16, 4>),
+          e = hipFuncSetAttribute(reinterpret_cast<const void*>(&scan_fwd_seg_kernel<hst, 4>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return (int)e;
         attr_set = true;
@@ -744,7 +744,7 @@ extern "C" int rdx_selective_scan_bwd(int dtype, const void* u, const void* delt
     return launch_scan_bwd_any<float>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride, du,
                                   ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D, dirs, as_stream(stream));
   if (dtype == RDX_BF16)
-    return launch_scan_bwd_any<__hip_bfloat16>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride,
+    return launch_scan_bwd_any<hst>(u, delta, A_log, Bm, Cm, ldbc, Dp, dt_bias, ckpt, dy, dy_dir_stride,
                                            du, ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D, dirs,
                                            as_stream(stream));
   return RDX_EINVAL;

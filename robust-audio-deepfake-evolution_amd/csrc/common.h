@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <stdint.h>
 #include "../../include/radhip.h"
 
@@ -20,17 +21,68 @@
 
 namespace rdx {
 
+// ---- The 16-bit storage type of this build ----------------------------------------------------------------------
+// libradhip.so keeps activations and GEMM / conv operands in bf16; libradhip_f16.so is the same sources built with
+// -DRDX_F16 and keeps them in IEEE fp16, the reference's autocast dtype (src/main.py:28,1049). On gfx950 both MFMA
+// forms (v_mfma_f32_{32x32x16,16x16x32}_{bf16,f16}) take the same cycles. Kernels reach the storage type only
+// through the names below: hst (the element), hel (the MFMA vector element), hx8 / hx4v (operand vectors),
+// h2f / f2h / hround (conversion, round to nearest even), hlo / hhi (the value of the low / high half-word of a
+// packed pair), hbits / hpack2 (the rounded 16-bit pattern of a float, two of them packed), the MFMA wrappers and
+// the transposed LDS read. All arithmetic stays fp32.
+#ifdef RDX_F16
+typedef __half hst;
+typedef _Float16 hel;
+#else
+typedef __hip_bfloat16 hst;
+typedef __bf16 hel;
+#endif
+typedef __attribute__((ext_vector_type(8))) hel hx8;
+typedef __attribute__((__vector_size__(4 * sizeof(hel)))) hel hx4v;
+typedef __attribute__((__vector_size__(4 * sizeof(short)))) short rdx_s4v;
+typedef __attribute__((address_space(3))) rdx_s4v rdx_lds_s4v;
+typedef __attribute__((ext_vector_type(16))) float rdx_f32x16;
+typedef __attribute__((ext_vector_type(4))) float rdx_f32x4;
+
+#ifdef RDX_F16
+__device__ __forceinline__ float h2f(hst x) { return __half2float(x); }
+__device__ __forceinline__ hst f2h(float x) { return __float2half(x); }
+__device__ __forceinline__ uint32_t hbits_of(hst x) { return (uint32_t)__half_as_ushort(x); }
+__device__ __forceinline__ float hlo(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu)); }
+__device__ __forceinline__ float hhi(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); }
+__device__ __forceinline__ rdx_f32x16 mfma32x32x16(hx8 a, hx8 b, rdx_f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ rdx_f32x4 mfma16x16x32(hx8 a, hx8 b, rdx_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+#else
+__device__ __forceinline__ float h2f(hst x) { return __bfloat162float(x); }
+__device__ __forceinline__ hst f2h(float x) { return __float2bfloat16(x); }
+__device__ __forceinline__ uint32_t hbits_of(hst x) { return (uint32_t)__bfloat16_as_ushort(x); }
+__device__ __forceinline__ float hlo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hhi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ rdx_f32x16 mfma32x32x16(hx8 a, hx8 b, rdx_f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ rdx_f32x4 mfma16x16x32(hx8 a, hx8 b, rdx_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+#endif
+__device__ __forceinline__ float hround(float x) { return h2f(f2h(x)); }
+__device__ __forceinline__ uint32_t hbits(float x) { return hbits_of(f2h(x)); }
+__device__ __forceinline__ uint32_t hpack2(float lo, float hi) { return hbits(lo) | (hbits(hi) << 16); }
+// ds_read_b64_tr_b16 from an LDS address (4 16-bit elements of the lane's transposed column)
+__device__ __forceinline__ hx4v ds_tr4(const void* lds) {
+  return __builtin_bit_cast(hx4v, __builtin_amdgcn_ds_read_tr16_b64_v4i16((rdx_lds_s4v*)(lds)));
+}
+
 // Storage-type adapters: all arithmetic is fp32.
 template <typename T> __device__ __forceinline__ float ld(const T* p, int64_t i);
 template <> __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }
-template <> __device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p, int64_t i) {
-  return __bfloat162float(p[i]);
-}
+template <> __device__ __forceinline__ float ld<hst>(const hst* p, int64_t i) { return h2f(p[i]); }
 template <typename T> __device__ __forceinline__ void st(T* p, int64_t i, float v);
 template <> __device__ __forceinline__ void st<float>(float* p, int64_t i, float v) { p[i] = v; }
-template <> __device__ __forceinline__ void st<__hip_bfloat16>(__hip_bfloat16* p, int64_t i, float v) {
-  p[i] = __float2bfloat16(v);
-}
+template <> __device__ __forceinline__ void st<hst>(hst* p, int64_t i, float v) { p[i] = f2h(v); }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }

@@ -22,7 +22,6 @@ namespace rdx {
 constexpr int FE_C = 512;            // conv_dim of every layer
 constexpr int FE_TOK = 16;           // output tokens per 256-thread block (4 per wave)
 
-__device__ __forceinline__ float fe_bf16(float x) { return __bfloat162float(__float2bfloat16(x)); }
 __device__ __forceinline__ float fe_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
 // LayerNorm over the 512 channels held 8 per lane by one wave, then GELU.
@@ -48,11 +47,11 @@ __device__ __forceinline__ void fe_ln_gelu(float v[8], const float* __restrict__
 }
 
 __device__ __forceinline__ uint32_t fe_pack2(float a, float b) {
-  __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  hst x = f2h(a), y = f2h(b);
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
 }
 
-__device__ __forceinline__ void fe_store8(__hip_bfloat16* p, const float v[8]) {
+__device__ __forceinline__ void fe_store8(hst* p, const float v[8]) {
   *reinterpret_cast<uint4*>(p) = make_uint4(fe_pack2(v[0], v[1]), fe_pack2(v[2], v[3]), fe_pack2(v[4], v[5]),
                                             fe_pack2(v[6], v[7]));
 }
@@ -63,7 +62,7 @@ template <int K>
 __global__ __launch_bounds__(256) void fe_conv0_kernel(const float* __restrict__ x, int64_t L, const float* __restrict__ w,
                                                        const float* __restrict__ bias, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, float eps, int stride,
-                                                       __hip_bfloat16* __restrict__ out, int64_t T0) {
+                                                       hst* __restrict__ out, int64_t T0) {
   extern __shared__ float s_win[];
   const int b = blockIdx.y;
   const int64_t t_base = (int64_t)blockIdx.x * FE_TOK;
@@ -71,7 +70,7 @@ __global__ __launch_bounds__(256) void fe_conv0_kernel(const float* __restrict__
   const float* xb = x + (int64_t)b * L;
   for (int i = threadIdx.x; i < nwin; i += 256) {
     const int64_t g = t_base * stride + i;
-    s_win[i] = g < L ? fe_bf16(xb[g]) : 0.f;
+    s_win[i] = g < L ? hround(xb[g]) : 0.f;
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c0 = lane * 8;
@@ -100,28 +99,28 @@ __global__ __launch_bounds__(256) void fe_conv0_kernel(const float* __restrict__
       for (int e = 0; e < 8; ++e) v[e] = fmaf(wr[e][k], xv, v[e]);
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fe_bf16(v[e] + bs[e]);
+    for (int e = 0; e < 8; ++e) v[e] = hround(v[e] + bs[e]);
     fe_ln_gelu(v, gamma, beta, c0, eps);
     fe_store8(out + ((int64_t)b * T0 + t) * FE_C + c0, v);
   }
 }
 
 // ---- LayerNorm(512) + GELU of rows [R, 512] bf16 (in place, or fp32 into out32)
-__global__ __launch_bounds__(256) void fe_ln_gelu_kernel(__hip_bfloat16* __restrict__ io, int64_t R,
+__global__ __launch_bounds__(256) void fe_ln_gelu_kernel(hst* __restrict__ io, int64_t R,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          float eps, float* __restrict__ out32) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
   const int c0 = lane * 8;
-  __hip_bfloat16* p = io + row * FE_C + c0;
+  hst* p = io + row * FE_C + c0;
   const uint4 u = *reinterpret_cast<const uint4*>(p);
   const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
   float v[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w4[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+    v[2 * i] = hlo(w4[i]);
+    v[2 * i + 1] = hhi(w4[i]);
   }
   fe_ln_gelu(v, gamma, beta, c0, eps);
   if (out32) {
@@ -148,7 +147,7 @@ extern "C" int rdx_fe_conv0(const float* x, int64_t batch, int64_t len, const fl
   dim3 grid((unsigned)((T0 + FE_TOK - 1) / FE_TOK), (unsigned)batch);
   const size_t smem = sizeof(float) * ((FE_TOK - 1) * stride + ksize);
   hipLaunchKernelGGL(fe_conv0_kernel<10>, grid, dim3(256), smem, as_stream(stream), x, len, w, bias, gamma, beta, eps,
-                     stride, (__hip_bfloat16*)out, T0);
+                     stride, (hst*)out, T0);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -158,7 +157,7 @@ extern "C" int rdx_fe_ln_gelu(void* io, int64_t rows, const float* gamma, const 
   RDX_REQUIRE(io && gamma && beta && rows > 0 && ((uintptr_t)io & 15) == 0);
   RDX_REQUIRE(((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0 && (!out32 || ((uintptr_t)out32 & 15) == 0));
   hipLaunchKernelGGL(fe_ln_gelu_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, as_stream(stream),
-                     (__hip_bfloat16*)io, rows, gamma, beta, eps, out32);
+                     (hst*)io, rows, gamma, beta, eps, out32);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

@@ -23,7 +23,6 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 gbf16x8;
 typedef __attribute__((ext_vector_type(16))) float gf32x16;
 
 constexpr int GM = 128, GN = 128, GK = 64;
@@ -32,32 +31,31 @@ constexpr int G_TILE = GM * GK * 2;  // one operand tile: 16 KB
 
 __device__ __forceinline__ int g_slot(int row, int ch) { return row * 128 + 16 * (ch ^ ((row >> 1) & 7)); }
 
-__device__ __forceinline__ gf32x16 g_mfma(gbf16x8 a, gbf16x8 b, gf32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ gf32x16 g_mfma(hx8 a, hx8 b, gf32x16 c) {
+  return mfma32x32x16(a, b, c);
 }
 
 __device__ __forceinline__ float g_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float g_gelu_grad(float x) {
   return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
-__device__ __forceinline__ float g_bf16_round(float x) { return __bfloat162float(__float2bfloat16(x)); }
 __device__ __forceinline__ uint32_t g_pack2(float a, float b) {
-  __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  hst x = f2h(a), y = f2h(b);
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
 }
 
 struct GemmArgs {
-  const __hip_bfloat16* A;
+  const hst* A;
   int64_t lda;
-  const __hip_bfloat16* B;
+  const hst* B;
   int64_t ldb;
   void* C;
   int64_t ldc;
   int M, N, K;
-  const __hip_bfloat16* bias;  // [N] or null
+  const hst* bias;  // [N] or null
   const void* aux;             // GELU_BWD: u bf16 [M, ldaux]; RESID_DROP: h fp32 [M, ldaux]
   int64_t ldaux;
-  __hip_bfloat16* aux_out;     // BIAS_GELU: gelu(u) bf16 [M, ldao]
+  hst* aux_out;     // BIAS_GELU: gelu(u) bf16 [M, ldao]
   int64_t ldao;
   const int64_t* seed_dev;     // RESID_DROP dropout (element index m * N + n, csrc/wavlm_layer.hip hash)
   int salt;
@@ -86,25 +84,25 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
     }
   }
   const int m0 = mt * GM, n0 = ntile * GN;
-  const __hip_bfloat16* __restrict__ Ab = g.A + (int64_t)blockIdx.y * g.sA;
+  const hst* __restrict__ Ab = g.A + (int64_t)blockIdx.y * g.sA;
   const int64_t mrow0 = (int64_t)blockIdx.y * g.crow;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
   const int M = g.M, N = g.N, K = g.K;
   const int nk = (K + GK - 1) / GK;
 
-  gbf16x8 ra[4], rb[4];
+  hx8 ra[4], rb[4];
   auto gload = [&](int kt) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int id = tid + G_THREADS * j, row = id >> 3, ch = id & 7;
       const int k = kt * GK + 8 * ch;
       const int am = m0 + row, bn = n0 + row;
-      gbf16x8 z;
+      hx8 z;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
-      ra[j] = (am < M && k < K) ? *reinterpret_cast<const gbf16x8*>(Ab + (int64_t)am * g.lda + k) : z;
-      rb[j] = (bn < N && k < K) ? *reinterpret_cast<const gbf16x8*>(g.B + (int64_t)bn * g.ldb + k) : z;
+      for (int e = 0; e < 8; ++e) z[e] = (hel)0.f;
+      ra[j] = (am < M && k < K) ? *reinterpret_cast<const hx8*>(Ab + (int64_t)am * g.lda + k) : z;
+      rb[j] = (bn < N && k < K) ? *reinterpret_cast<const hx8*>(g.B + (int64_t)bn * g.ldb + k) : z;
     }
   };
   auto swrite = [&](int buf) {
@@ -112,8 +110,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int id = tid + G_THREADS * j, row = id >> 3, ch = id & 7;
-      *reinterpret_cast<gbf16x8*>(base + g_slot(row, ch)) = ra[j];
-      *reinterpret_cast<gbf16x8*>(base + G_TILE + g_slot(row, ch)) = rb[j];
+      *reinterpret_cast<hx8*>(base + g_slot(row, ch)) = ra[j];
+      *reinterpret_cast<hx8*>(base + G_TILE + g_slot(row, ch)) = rb[j];
     }
   };
 
@@ -134,12 +132,12 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
     const char* Bs = As + G_TILE;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      gbf16x8 af[2], bfr[2];
+      hx8 af[2], bfr[2];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) af[mi] = *reinterpret_cast<const gbf16x8*>(As + g_slot(wm * 64 + mi * 32 + r, 2 * s + h));
+      for (int mi = 0; mi < 2; ++mi) af[mi] = *reinterpret_cast<const hx8*>(As + g_slot(wm * 64 + mi * 32 + r, 2 * s + h));
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni)
-        bfr[ni] = *reinterpret_cast<const gbf16x8*>(Bs + g_slot(wn * 64 + ni * 32 + r, 2 * s + h));
+        bfr[ni] = *reinterpret_cast<const hx8*>(Bs + g_slot(wn * 64 + ni * 32 + r, 2 * s + h));
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -167,31 +165,31 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
         for (int e = 0; e < 4; ++e) v[e] = acc[mi][ni][4 * c + e];
         if (EPI != RDX_EPI_GELU_BWD && g.bias) {
           const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
-          v[0] += __uint_as_float(bb.x << 16);
-          v[1] += __uint_as_float(bb.x & 0xffff0000u);
-          v[2] += __uint_as_float(bb.y << 16);
-          v[3] += __uint_as_float(bb.y & 0xffff0000u);
+          v[0] += hlo(bb.x);
+          v[1] += hhi(bb.x);
+          v[2] += hlo(bb.y);
+          v[3] += hhi(bb.y);
         }
         if (EPI == RDX_EPI_BIAS) {
-          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + mg * g.ldc + n) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<hst*>(g.C) + mg * g.ldc + n) =
               make_uint2(g_pack2(v[0], v[1]), g_pack2(v[2], v[3]));
         } else if (EPI == RDX_EPI_BIAS_GELU) {
           float u[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) u[e] = g_bf16_round(v[e]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + mg * g.ldc + n) =
+          for (int e = 0; e < 4; ++e) u[e] = hround(v[e]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<hst*>(g.C) + mg * g.ldc + n) =
               make_uint2(g_pack2(u[0], u[1]), g_pack2(u[2], u[3]));
           *reinterpret_cast<uint2*>(g.aux_out + mg * g.ldao + n) =
               make_uint2(g_pack2(g_gelu(u[0]), g_gelu(u[1])), g_pack2(g_gelu(u[2]), g_gelu(u[3])));
         } else if (EPI == RDX_EPI_GELU_BWD) {
-          const uint2 uu = *reinterpret_cast<const uint2*>(reinterpret_cast<const __hip_bfloat16*>(g.aux) +
+          const uint2 uu = *reinterpret_cast<const uint2*>(reinterpret_cast<const hst*>(g.aux) +
                                                            mg * g.ldaux + n);
-          const float u[4] = {__uint_as_float(uu.x << 16), __uint_as_float(uu.x & 0xffff0000u),
-                              __uint_as_float(uu.y << 16), __uint_as_float(uu.y & 0xffff0000u)};
+          const float u[4] = {hlo(uu.x), hhi(uu.x),
+                              hlo(uu.y), hhi(uu.y)};
           float d[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) d[e] = g_bf16_round(v[e]) * g_gelu_grad(u[e]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<__hip_bfloat16*>(g.C) + mg * g.ldc + n) =
+          for (int e = 0; e < 4; ++e) d[e] = hround(v[e]) * g_gelu_grad(u[e]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<hst*>(g.C) + mg * g.ldc + n) =
               make_uint2(g_pack2(d[0], d[1]), g_pack2(d[2], d[3]));
         } else {  // RDX_EPI_RESID_DROP
           const float4 hv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(g.aux) +
@@ -200,7 +198,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void gemm_nt_kernel(GemmArgs g) {
           float o[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float fo = g_bf16_round(v[e]);
+            const float fo = hround(v[e]);
             const float ms = g.thr ? (drop_keep(seed, (uint64_t)m * N + n + e, g.thr) ? g.inv_keep : 0.f) : 1.f;
             o[e] = hx[e] + fo * ms;
           }
@@ -242,19 +240,19 @@ extern "C" int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t 
   }
   RDX_REQUIRE(ldc % 4 == 0 || epilogue == RDX_EPI_BIAS);
   GemmArgs g;
-  g.A = (const __hip_bfloat16*)A;
+  g.A = (const hst*)A;
   g.lda = lda;
-  g.B = (const __hip_bfloat16*)B;
+  g.B = (const hst*)B;
   g.ldb = ldb;
   g.C = C;
   g.ldc = ldc;
   g.M = M;
   g.N = N;
   g.K = K;
-  g.bias = (const __hip_bfloat16*)bias;
+  g.bias = (const hst*)bias;
   g.aux = aux;
   g.ldaux = ldaux;
-  g.aux_out = (__hip_bfloat16*)aux_out;
+  g.aux_out = (hst*)aux_out;
   g.ldao = ldao;
   g.seed_dev = seed_dev;
   g.salt = salt;
@@ -287,16 +285,16 @@ extern "C" int rdx_gemm_bf16_strided(const void* A, int64_t lda, int64_t sA, con
   RDX_REQUIRE(N % 4 == 0 && ldc >= N && ldc % 4 == 0 && crow >= 0 && (batch == 1 || crow >= M));
   RDX_REQUIRE(!bias || ((uintptr_t)bias & 7) == 0);
   GemmArgs g;
-  g.A = (const __hip_bfloat16*)A;
+  g.A = (const hst*)A;
   g.lda = lda;
-  g.B = (const __hip_bfloat16*)B;
+  g.B = (const hst*)B;
   g.ldb = ldb;
   g.C = C;
   g.ldc = ldc;
   g.M = M;
   g.N = N;
   g.K = K;
-  g.bias = (const __hip_bfloat16*)bias;
+  g.bias = (const hst*)bias;
   g.aux = nullptr;
   g.ldaux = 0;
   g.aux_out = nullptr;

@@ -31,15 +31,15 @@ template <> struct Vec4<float> {
     *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
   }
 };
-template <> struct Vec4<__hip_bfloat16> {
-  static __device__ __forceinline__ void load(const __hip_bfloat16* p, int64_t i, float v[4]) {
+template <> struct Vec4<hst> {
+  static __device__ __forceinline__ void load(const hst* p, int64_t i, float v[4]) {
     uint2 q = *reinterpret_cast<const uint2*>(p + i);
-    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    v[0] = hlo(q.x); v[1] = hhi(q.x);
+    v[2] = hlo(q.y); v[3] = hhi(q.y);
   }
-  static __device__ __forceinline__ void store(__hip_bfloat16* p, int64_t i, const float v[4]) {
-    __hip_bfloat16 b0 = __float2bfloat16(v[0]), b1 = __float2bfloat16(v[1]);
-    __hip_bfloat16 b2 = __float2bfloat16(v[2]), b3 = __float2bfloat16(v[3]);
+  static __device__ __forceinline__ void store(hst* p, int64_t i, const float v[4]) {
+    hst b0 = f2h(v[0]), b1 = f2h(v[1]);
+    hst b2 = f2h(v[2]), b3 = f2h(v[3]);
     uint2 q;
     q.x = (uint32_t)(*reinterpret_cast<uint16_t*>(&b0)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&b1)) << 16);
     q.y = (uint32_t)(*reinterpret_cast<uint16_t*>(&b2)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&b3)) << 16);
@@ -137,7 +137,7 @@ using namespace rdx;
       using T = float;                                              \
       __VA_ARGS__;                                                  \
     } else if ((dtype) == RDX_BF16) {                               \
-      using T = __hip_bfloat16;                                     \
+      using T = hst;                                     \
       __VA_ARGS__;                                                  \
     } else {                                                        \
       return RDX_EINVAL;                                            \

@@ -90,8 +90,8 @@ extern "C" int rdx_focal_mixup_fwd(const void* logits, int logits_bf16, int ld_,
   if (C > FL_MAXC) return RDX_EUNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if (logits_bf16)
-    hipLaunchKernelGGL(focal_mixup_kernel<__hip_bfloat16>, dim3(1), dim3(FL_THREADS), 0, s,
-                       (const __hip_bfloat16*)logits, ld_, B, C, ya, yb, lam, rows_per_lam, alpha, gamma, mode, scale,
+    hipLaunchKernelGGL(focal_mixup_kernel<hst>, dim3(1), dim3(FL_THREADS), 0, s,
+                       (const hst*)logits, ld_, B, C, ya, yb, lam, rows_per_lam, alpha, gamma, mode, scale,
                        loss, dlogits);
   else
     hipLaunchKernelGGL(focal_mixup_kernel<float>, dim3(1), dim3(FL_THREADS), 0, s, (const float*)logits, ld_, B, C, ya,
@@ -106,8 +106,8 @@ extern "C" int rdx_focal_mixup_bwd(const float* grad, const float* dlogits, void
   hipStream_t s = as_stream(stream);
   const int blocks = (n + FL_THREADS - 1) / FL_THREADS < 64 ? (n + FL_THREADS - 1) / FL_THREADS : 64;
   if (out_bf16)
-    hipLaunchKernelGGL(focal_scale_kernel<__hip_bfloat16>, dim3(blocks), dim3(FL_THREADS), 0, s, grad, dlogits,
-                       (__hip_bfloat16*)out, n);
+    hipLaunchKernelGGL(focal_scale_kernel<hst>, dim3(blocks), dim3(FL_THREADS), 0, s, grad, dlogits,
+                       (hst*)out, n);
   else
     hipLaunchKernelGGL(focal_scale_kernel<float>, dim3(blocks), dim3(FL_THREADS), 0, s, grad, dlogits, (float*)out, n);
   RDX_LAUNCH_CHECK();

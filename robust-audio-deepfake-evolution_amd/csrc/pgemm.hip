@@ -23,7 +23,6 @@
 namespace rdx {
 namespace pg {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 
@@ -54,22 +53,22 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  hst x = f2h(a), y = f2h(b);
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
 }
 
 struct Args {
-  const __hip_bfloat16* A;
+  const hst* A;
   int64_t lda;
-  const __hip_bfloat16* B;
+  const hst* B;
   int64_t ldb;
-  __hip_bfloat16* C;
+  hst* C;
   int64_t ldc;
   int M, N, K;
-  const __hip_bfloat16* bias;
-  const __hip_bfloat16* aux;
+  const hst* bias;
+  const hst* aux;
   int64_t ldaux;
-  __hip_bfloat16* aux_out;
+  hst* aux_out;
   int64_t ldao;
   int tiles_m, tiles_n, group_m;
   int wide;
@@ -195,24 +194,24 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
 
   const int fr = lane & 15, fq = lane >> 4;
   // fragment reads of stage kt: A rows of phase p (FMP fragments x KK), all B columns (FN x KK)
-  auto read_a = [&](int kt, int p, bf16x8 (&af)[KK][FMP]) {
+  auto read_a = [&](int kt, int p, hx8 (&af)[KK][FMP]) {
     const char* As = lds + (kt % NST) * STAGE;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
       for (int i = 0; i < FMP; ++i) {
         const int row = wm * WTM + (p * FMP + i) * 16 + fr;
-        af[kk][i] = *reinterpret_cast<const bf16x8*>(As + row * ROWB + 16 * swz<BKT>(row, kk * 4 + fq));
+        af[kk][i] = *reinterpret_cast<const hx8*>(As + row * ROWB + 16 * swz<BKT>(row, kk * 4 + fq));
       }
   };
-  auto read_b = [&](int kt, bf16x8 (&bf)[KK][FN]) {
+  auto read_b = [&](int kt, hx8 (&bf)[KK][FN]) {
     const char* Bs = lds + (kt % NST) * STAGE + IMG_A;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * WTN + j * 16 + fr;
-        bf[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + row * ROWB + 16 * swz<BKT>(row, kk * 4 + fq));
+        bf[kk][j] = *reinterpret_cast<const hx8*>(Bs + row * ROWB + 16 * swz<BKT>(row, kk * 4 + fq));
       }
   };
 
@@ -222,7 +221,7 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto mfma_phase = [&](int p, const bf16x8 (&af)[KK][FMP], const bf16x8 (&bf)[KK][FN]) {
+  auto mfma_phase = [&](int p, const hx8 (&af)[KK][FMP], const hx8 (&bf)[KK][FN]) {
     if (ABL == 2) {                   // diagnostic: fragments read, no MFMA
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
@@ -240,8 +239,7 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
       for (int i = 0; i < FMP; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[p * FMP + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk][j], af[kk][i], acc[p * FMP + i][j], 0,
-                                                                        0, 0);
+          acc[p * FMP + i][j] = mfma16x16x32(bf[kk][j], af[kk][i], acc[p * FMP + i][j]);
     if (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
@@ -254,13 +252,13 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
   __builtin_amdgcn_sched_barrier(0);
   if (PROF) ts1 = __builtin_amdgcn_s_memtime();
 
-  bf16x8 a0[KK][FMP], a1[KK][FMP], b0[KK][FN], b1[KK][FN];
+  hx8 a0[KK][FMP], a1[KK][FMP], b0[KK][FN], b1[KK][FN];
   read_b(0, b0);
   read_a(0, 0, a0);
 
   // one K step with B fragments bc (this step) / bn (next step); the fences keep each phase's reads issued
   // before its MFMAs (the scheduler would otherwise sink them next to the barrier's lgkmcnt(0))
-  auto step = [&](int kt, bf16x8 (&bc)[KK][FN], bf16x8 (&bn)[KK][FN]) {
+  auto step = [&](int kt, hx8 (&bc)[KK][FN], hx8 (&bn)[KK][FN]) {
 #pragma unroll
     for (int p = 0; p < NPH - 1; ++p) {
       if (p & 1) {
@@ -310,10 +308,10 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (EPI != RDX_EPI_GELU_BWD && g.bias && n0 + c < N) {
         const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n0 + c);
-        v[0] += __uint_as_float(bb.x << 16);
-        v[1] += __uint_as_float(bb.x & 0xffff0000u);
-        v[2] += __uint_as_float(bb.y << 16);
-        v[3] += __uint_as_float(bb.y & 0xffff0000u);
+        v[0] += hlo(bb.x);
+        v[1] += hhi(bb.x);
+        v[2] += hlo(bb.y);
+        v[3] += hhi(bb.y);
       }
       *reinterpret_cast<uint2*>(img + r * PITCH + c * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
     }
@@ -327,13 +325,13 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
     if (m >= M || n >= N) continue;
     const bool full = n + 8 <= N;
     const bool wide = full && g.wide;
-    auto ld8 = [&](const __hip_bfloat16* src) -> uint4 {
+    auto ld8 = [&](const hst* src) -> uint4 {
       if (wide) return *reinterpret_cast<const uint4*>(src);
       const uint2 lo = *reinterpret_cast<const uint2*>(src);
       const uint2 hi = full ? *reinterpret_cast<const uint2*>(src + 4) : make_uint2(0u, 0u);
       return make_uint4(lo.x, lo.y, hi.x, hi.y);
     };
-    auto st8 = [&](__hip_bfloat16* dst, uint4 v) {
+    auto st8 = [&](hst* dst, uint4 v) {
       if (wide) { *reinterpret_cast<uint4*>(dst) = v; return; }
       *reinterpret_cast<uint2*>(dst) = make_uint2(v.x, v.y);
       if (full) *reinterpret_cast<uint2*>(dst + 4) = make_uint2(v.z, v.w);
@@ -345,8 +343,8 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
       uint32_t o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float a0v = __uint_as_float(qw[e] << 16), a1v = __uint_as_float(qw[e] & 0xffff0000u);
-        const float u0 = __uint_as_float(uw[e] << 16), u1 = __uint_as_float(uw[e] & 0xffff0000u);
+        const float a0v = hlo(qw[e]), a1v = hhi(qw[e]);
+        const float u0 = hlo(uw[e]), u1 = hhi(uw[e]);
         o[e] = pack2(a0v * gelu_grad(u0), a1v * gelu_grad(u1));
       }
       q = make_uint4(o[0], o[1], o[2], o[3]);
@@ -357,7 +355,7 @@ __global__ __launch_bounds__(512, 1) void pgemm_kernel(Args g) {
       uint32_t o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        o[e] = pack2(gelu(__uint_as_float(qw[e] << 16)), gelu(__uint_as_float(qw[e] & 0xffff0000u)));
+        o[e] = pack2(gelu(hlo(qw[e])), gelu(hhi(qw[e])));
       st8(g.aux_out + (int64_t)m * g.ldao + n, make_uint4(o[0], o[1], o[2], o[3]));
     }
   }
@@ -459,19 +457,19 @@ static int pgemm_entry(const void* A, int64_t lda, const void* B, int64_t ldb, v
   RDX_REQUIRE(tile >= 0 && tile < 200 && (pg::geometry(tile, &bm, &bn) || prof));
   RDX_REQUIRE(group_m >= 0 || prof);
   pg::Args g;
-  g.A = (const __hip_bfloat16*)A;
+  g.A = (const hst*)A;
   g.lda = lda;
-  g.B = (const __hip_bfloat16*)B;
+  g.B = (const hst*)B;
   g.ldb = ldb;
-  g.C = (__hip_bfloat16*)C;
+  g.C = (hst*)C;
   g.ldc = ldc;
   g.M = M;
   g.N = N;
   g.K = K;
-  g.bias = (const __hip_bfloat16*)bias;
-  g.aux = (const __hip_bfloat16*)aux;
+  g.bias = (const hst*)bias;
+  g.aux = (const hst*)aux;
   g.ldaux = ldaux;
-  g.aux_out = (__hip_bfloat16*)aux_out;
+  g.aux_out = (hst*)aux_out;
   g.ldao = ldao;
   g.tiles_m = g.tiles_n = 0;
   g.group_m = group_m;

@@ -22,7 +22,6 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 pc_bf16x8;
 typedef __attribute__((ext_vector_type(16))) float pc_f32x16;
 
 constexpr int PC_G = 16;                    // groups
@@ -39,64 +38,64 @@ __device__ __forceinline__ float pc_gelu_d(float u) {
 }
 
 // B fragments of tap k: [nt * 4 + s] = Wk[k][nt * 32 + n][16 s + 8 hh .. + 7] for lane (n, hh)
-__device__ __forceinline__ void pc_load_b(pc_bf16x8* dst, const __hip_bfloat16* wg, int k, int n, int hh) {
+__device__ __forceinline__ void pc_load_b(hx8* dst, const hst* wg, int k, int n, int hh) {
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       dst[nt * 4 + s] =
-          *reinterpret_cast<const pc_bf16x8*>(wg + ((int64_t)k * PC_C + nt * 32 + n) * PC_C + 16 * s + 8 * hh);
+          *reinterpret_cast<const hx8*>(wg + ((int64_t)k * PC_C + nt * 32 + n) * PC_C + 16 * s + 8 * hh);
 }
 
 // one tap: acc[nt] += A (32 window rows from arow, 64 channels) x B (the tap's 64 x 32 slice nt)
-__device__ __forceinline__ void pc_tap(pc_f32x16* acc, const __bf16* arow, const pc_bf16x8* bf) {
+__device__ __forceinline__ void pc_tap(pc_f32x16* acc, const hel* arow, const hx8* bf) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const pc_bf16x8 af = *reinterpret_cast<const pc_bf16x8*>(arow + 16 * s);
-    acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[s], acc[0], 0, 0, 0);
-    acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[4 + s], acc[1], 0, 0, 0);
+    const hx8 af = *reinterpret_cast<const hx8*>(arow + 16 * s);
+    acc[0] = mfma32x32x16(af, bf[s], acc[0]);
+    acc[1] = mfma32x32x16(af, bf[4 + s], acc[1]);
   }
 }
 
 template <bool kBwd>
-__global__ __launch_bounds__(256) void posconv_kernel(const __hip_bfloat16* __restrict__ in,   // fwd h, bwd dy
-                                                      const __hip_bfloat16* __restrict__ usave,  // bwd: u
-                                                      const __hip_bfloat16* __restrict__ wk,     // [G][K][64][64]
+__global__ __launch_bounds__(256) void posconv_kernel(const hst* __restrict__ in,   // fwd h, bwd dy
+                                                      const hst* __restrict__ usave,  // bwd: u
+                                                      const hst* __restrict__ wk,     // [G][K][64][64]
                                                       const float* __restrict__ bias,            // fwd: [E]
-                                                      __hip_bfloat16* __restrict__ out,          // fwd y, bwd dh
-                                                      __hip_bfloat16* __restrict__ uout,         // fwd: u
+                                                      hst* __restrict__ out,          // fwd y, bwd dh
+                                                      hst* __restrict__ uout,         // fwd: u
                                                       int T, int off) {
-  __shared__ __attribute__((aligned(16))) __bf16 win[PC_WIN][PC_LDW];
+  __shared__ __attribute__((aligned(16))) hel win[PC_WIN][PC_LDW];
   const int t0 = blockIdx.x * PC_ROWS, g = blockIdx.y, b = blockIdx.z;
   const int64_t base = (int64_t)b * T * PC_E + g * PC_C;
   for (int i = threadIdx.x; i < PC_WIN * (PC_C / 8); i += 256) {
     const int wr = i >> 3, c8 = (i & 7) * 8;
     const int tr = t0 - off + wr;
-    pc_bf16x8 v;
+    hx8 v;
     if (tr >= 0 && tr < T) {
       const int64_t o = base + (int64_t)tr * PC_E + c8;
       if (kBwd) {
-        const pc_bf16x8 d = *reinterpret_cast<const pc_bf16x8*>(in + o);
-        const pc_bf16x8 u = *reinterpret_cast<const pc_bf16x8*>(usave + o);
+        const hx8 d = *reinterpret_cast<const hx8*>(in + o);
+        const hx8 u = *reinterpret_cast<const hx8*>(usave + o);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)d[j] * pc_gelu_d((float)u[j]));
+        for (int j = 0; j < 8; ++j) v[j] = (hel)((float)d[j] * pc_gelu_d((float)u[j]));
       } else {
-        v = *reinterpret_cast<const pc_bf16x8*>(in + o);
+        v = *reinterpret_cast<const hx8*>(in + o);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      for (int j = 0; j < 8; ++j) v[j] = (hel)0.f;
     }
-    *reinterpret_cast<pc_bf16x8*>(&win[wr][c8]) = v;
+    *reinterpret_cast<hx8*>(&win[wr][c8]) = v;
   }
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   if (t0 + 32 * w >= T) return;  // no barrier follows
-  const __hip_bfloat16* wg = wk + (int64_t)g * PC_K * PC_C * PC_C;
+  const hst* wg = wk + (int64_t)g * PC_K * PC_C * PC_C;
   pc_f32x16 acc[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[0][i] = acc[1][i] = 0.f;
-  pc_bf16x8 b0[8], b1[8];
+  hx8 b0[8], b1[8];
   pc_load_b(b0, wg, 0, r, hh);
   for (int k = 0; k < PC_K; k += 2) {
     pc_load_b(b1, wg, k + 1, r, hh);
@@ -115,11 +114,11 @@ __global__ __launch_bounds__(256) void posconv_kernel(const __hip_bfloat16* __re
       if (t < T) {
         const int64_t o = base + (int64_t)t * PC_E + n;
         if (kBwd) {
-          out[o] = __float2bfloat16(acc[nt][i]);
+          out[o] = f2h(acc[nt][i]);
         } else {
-          const __hip_bfloat16 ub = __float2bfloat16(acc[nt][i] + bs);
+          const hst ub = f2h(acc[nt][i] + bs);
           uout[o] = ub;
-          out[o] = __float2bfloat16(pc_gelu(__bfloat162float(ub)));
+          out[o] = f2h(pc_gelu(h2f(ub)));
         }
       }
     }
@@ -136,18 +135,18 @@ constexpr int PC2_WIN = PC2_ROWS + PC_K - 1;
 constexpr int PC2_WIMG = PC_C * PC_LDW;   // one tap's weight image (bf16 elements)
 constexpr int PC2_LDS = (PC2_WIN * PC_LDW + 2 * PC2_WIMG) * 2;
 template <bool kBwd>
-__global__ __launch_bounds__(256, 2) void posconv2_kernel(const __hip_bfloat16* __restrict__ in,
-                                                          const __hip_bfloat16* __restrict__ usave,
-                                                          const __hip_bfloat16* __restrict__ wk,
+__global__ __launch_bounds__(256, 2) void posconv2_kernel(const hst* __restrict__ in,
+                                                          const hst* __restrict__ usave,
+                                                          const hst* __restrict__ wk,
                                                           const float* __restrict__ bias,
-                                                          __hip_bfloat16* __restrict__ out,
-                                                          __hip_bfloat16* __restrict__ uout, int T, int off) {
+                                                          hst* __restrict__ out,
+                                                          hst* __restrict__ uout, int T, int off) {
   extern __shared__ __attribute__((aligned(16))) char pc2_lds[];
-  __bf16 (*win)[PC_LDW] = reinterpret_cast<__bf16 (*)[PC_LDW]>(pc2_lds);
-  __bf16* wimg = reinterpret_cast<__bf16*>(pc2_lds) + PC2_WIN * PC_LDW;   // [2][64 n][PC_LDW]
+  hel (*win)[PC_LDW] = reinterpret_cast<hel (*)[PC_LDW]>(pc2_lds);
+  hel* wimg = reinterpret_cast<hel*>(pc2_lds) + PC2_WIN * PC_LDW;   // [2][64 n][PC_LDW]
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int64_t base = (int64_t)b * T * PC_E + g * PC_C;
-  const __hip_bfloat16* wg = wk + (int64_t)g * PC_K * PC_C * PC_C;
+  const hst* wg = wk + (int64_t)g * PC_K * PC_C * PC_C;
   // tap k's [64 n][64 c] slice: 512 16-byte chunks, chunks tid and tid + 256 of this thread
   const int wn0 = tid >> 3, wc0 = (tid & 7) * 8;   // chunk tid + 256: row wn0 + 32
   auto wload = [&](int k, int j) -> uint4 {
@@ -161,22 +160,22 @@ __global__ __launch_bounds__(256, 2) void posconv2_kernel(const __hip_bfloat16* 
   for (int i = tid; i < PC2_WIN * (PC_C / 8); i += 256) {
     const int wr = i >> 3, c8 = (i & 7) * 8;
     const int tr = wr - off;
-    pc_bf16x8 v;
+    hx8 v;
     if (tr >= 0 && tr < T) {
       const int64_t o = base + (int64_t)tr * PC_E + c8;
       if (kBwd) {
-        const pc_bf16x8 d = *reinterpret_cast<const pc_bf16x8*>(in + o);
-        const pc_bf16x8 u = *reinterpret_cast<const pc_bf16x8*>(usave + o);
+        const hx8 d = *reinterpret_cast<const hx8*>(in + o);
+        const hx8 u = *reinterpret_cast<const hx8*>(usave + o);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)d[j] * pc_gelu_d((float)u[j]));
+        for (int j = 0; j < 8; ++j) v[j] = (hel)((float)d[j] * pc_gelu_d((float)u[j]));
       } else {
-        v = *reinterpret_cast<const pc_bf16x8*>(in + o);
+        v = *reinterpret_cast<const hx8*>(in + o);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      for (int j = 0; j < 8; ++j) v[j] = (hel)0.f;
     }
-    *reinterpret_cast<pc_bf16x8*>(&win[wr][c8]) = v;
+    *reinterpret_cast<hx8*>(&win[wr][c8]) = v;
   }
   wstore(0, va0, va1);
   __syncthreads();
@@ -188,13 +187,13 @@ __global__ __launch_bounds__(256, 2) void posconv2_kernel(const __hip_bfloat16* 
   for (int i = 0; i < 16; ++i) acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
   // tap kk from image buf: the B fragments [nt * 4 + s] = W[kk][nt * 32 + r][16 s + 8 hh .. + 7]
   auto tap = [&](int kk, int buf) {
-    pc_bf16x8 bf[8];
+    hx8 bf[8];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
         bf[nt * 4 + s2] =
-            *reinterpret_cast<const pc_bf16x8*>(wimg + buf * PC2_WIMG + (nt * 32 + r) * PC_LDW + 16 * s2 + 8 * hh);
+            *reinterpret_cast<const hx8*>(wimg + buf * PC2_WIMG + (nt * 32 + r) * PC_LDW + 16 * s2 + 8 * hh);
     if (one) pc_tap(acc[0], &win[r0 + r + kk][8 * hh], bf);
     if (two) pc_tap(acc[1], &win[r0 + 32 + r + kk][8 * hh], bf);
   };
@@ -225,11 +224,11 @@ __global__ __launch_bounds__(256, 2) void posconv2_kernel(const __hip_bfloat16* 
         if (t < T) {
           const int64_t o = base + (int64_t)t * PC_E + n;
           if (kBwd) {
-            out[o] = __float2bfloat16(acc[mt][nt][i]);
+            out[o] = f2h(acc[mt][nt][i]);
           } else {
-            const __hip_bfloat16 ub = __float2bfloat16(acc[mt][nt][i] + bs);
+            const hst ub = f2h(acc[mt][nt][i] + bs);
             uout[o] = ub;
-            out[o] = __float2bfloat16(pc_gelu(__bfloat162float(ub)));
+            out[o] = f2h(pc_gelu(h2f(ub)));
           }
         }
       }
@@ -255,12 +254,12 @@ static int pc2_launch(bool bwd, const void* in, const void* u, const void* wk, c
   }
   dim3 grid(PC_G, B);
   if (bwd)
-    hipLaunchKernelGGL(posconv2_kernel<true>, grid, dim3(256), smem, st, (const __hip_bfloat16*)in,
-                       (const __hip_bfloat16*)u, (const __hip_bfloat16*)wk, nullptr, (__hip_bfloat16*)out, nullptr, T,
+    hipLaunchKernelGGL(posconv2_kernel<true>, grid, dim3(256), smem, st, (const hst*)in,
+                       (const hst*)u, (const hst*)wk, nullptr, (hst*)out, nullptr, T,
                        off);
   else
-    hipLaunchKernelGGL(posconv2_kernel<false>, grid, dim3(256), smem, st, (const __hip_bfloat16*)in, nullptr,
-                       (const __hip_bfloat16*)wk, bias, (__hip_bfloat16*)out, (__hip_bfloat16*)uout, T, off);
+    hipLaunchKernelGGL(posconv2_kernel<false>, grid, dim3(256), smem, st, (const hst*)in, nullptr,
+                       (const hst*)wk, bias, (hst*)out, (hst*)uout, T, off);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -272,8 +271,8 @@ extern "C" int rdx_posconv_fwd(const void* h, const void* wk, const float* bias,
   RDX_REQUIRE(pc_ok(h) && pc_ok(wk) && bias && pc_ok(y) && pc_ok(u) && B > 0 && T > 0 && B <= 65535);
   if (T <= PC2_ROWS) return pc2_launch(false, h, nullptr, wk, bias, y, u, B, T, PC_K / 2, as_stream(stream));
   dim3 grid((T + PC_ROWS - 1) / PC_ROWS, PC_G, B);
-  hipLaunchKernelGGL(posconv_kernel<false>, grid, dim3(256), 0, as_stream(stream), (const __hip_bfloat16*)h, nullptr,
-                     (const __hip_bfloat16*)wk, bias, (__hip_bfloat16*)y, (__hip_bfloat16*)u, T, PC_K / 2);
+  hipLaunchKernelGGL(posconv_kernel<false>, grid, dim3(256), 0, as_stream(stream), (const hst*)h, nullptr,
+                     (const hst*)wk, bias, (hst*)y, (hst*)u, T, PC_K / 2);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -282,8 +281,8 @@ extern "C" int rdx_posconv_bwd(const void* dy, const void* u, const void* wkt, v
   RDX_REQUIRE(pc_ok(dy) && pc_ok(u) && pc_ok(wkt) && pc_ok(dh) && B > 0 && T > 0 && B <= 65535);
   if (T <= PC2_ROWS) return pc2_launch(true, dy, u, wkt, nullptr, dh, nullptr, B, T, PC_K / 2 - 1, as_stream(stream));
   dim3 grid((T + PC_ROWS - 1) / PC_ROWS, PC_G, B);
-  hipLaunchKernelGGL(posconv_kernel<true>, grid, dim3(256), 0, as_stream(stream), (const __hip_bfloat16*)dy,
-                     (const __hip_bfloat16*)u, (const __hip_bfloat16*)wkt, nullptr, (__hip_bfloat16*)dh, nullptr, T,
+  hipLaunchKernelGGL(posconv_kernel<true>, grid, dim3(256), 0, as_stream(stream), (const hst*)dy,
+                     (const hst*)u, (const hst*)wkt, nullptr, (hst*)dh, nullptr, T,
                      PC_K / 2 - 1);
   RDX_LAUNCH_CHECK();
   return RDX_OK;

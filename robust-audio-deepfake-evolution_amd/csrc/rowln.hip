@@ -24,12 +24,12 @@ constexpr int RL_ROWS_PER_WAVE = RL_RPW;
 template <typename T>
 __device__ __forceinline__ float rl_ld(const T* p, int64_t i) {
   if constexpr (std::is_same<T, float>::value) return p[i];
-  else return __bfloat162float(p[i]);
+  else return h2f(p[i]);
 }
 template <typename T>
 __device__ __forceinline__ void rl_st(T* p, int64_t i, float v) {
   if constexpr (std::is_same<T, float>::value) p[i] = v;
-  else p[i] = __float2bfloat16(v);
+  else p[i] = f2h(v);
 }
 
 template <typename TI, typename TO>
@@ -167,9 +167,9 @@ extern "C" int rdx_row_ln_fwd(int dtype_x, const void* x, const float* gamma, co
   hipLaunchKernelGGL((row_ln_fwd_kernel<TI, TO>), grid, block, 0, st, (const TI*)x, gamma, beta, eps, (TO*)y, \
                      mean, rstd, M, C)
   if (dtype_x == RDX_F32 && dtype_y == RDX_F32) RL_FWD(float, float);
-  else if (dtype_x == RDX_F32) RL_FWD(float, __hip_bfloat16);
-  else if (dtype_y == RDX_F32) RL_FWD(__hip_bfloat16, float);
-  else RL_FWD(__hip_bfloat16, __hip_bfloat16);
+  else if (dtype_x == RDX_F32) RL_FWD(float, hst);
+  else if (dtype_y == RDX_F32) RL_FWD(hst, float);
+  else RL_FWD(hst, hst);
 #undef RL_FWD
   RDX_LAUNCH_CHECK();
   return RDX_OK;
@@ -194,9 +194,9 @@ extern "C" int rdx_row_ln_bwd(int dtype_dy, const void* dy, int dtype_x, const v
                          mean, rstd, gamma, (TX*)dx, dgamma, dbeta, M, C);                                    \
   } while (0)
   if (dtype_dy == RDX_F32 && dtype_x == RDX_F32) RL_BWD(float, float);
-  else if (dtype_dy == RDX_F32) RL_BWD(float, __hip_bfloat16);
-  else if (dtype_x == RDX_F32) RL_BWD(__hip_bfloat16, float);
-  else RL_BWD(__hip_bfloat16, __hip_bfloat16);
+  else if (dtype_dy == RDX_F32) RL_BWD(float, hst);
+  else if (dtype_x == RDX_F32) RL_BWD(hst, float);
+  else RL_BWD(hst, hst);
 #undef RL_BWD
   RDX_LAUNCH_CHECK();
   return RDX_OK;

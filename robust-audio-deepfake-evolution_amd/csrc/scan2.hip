@@ -364,7 +364,7 @@ extern "C" int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const 
   const dim3 grid((D + s2::CH - 1) / s2::CH, rdx_scan2_chunks(L), dirs * B);
   hipStream_t st = as_stream(stream);
   if (dtype == RDX_BF16) {
-    using T = __hip_bfloat16;
+    using T = hst;
     hipLaunchKernelGGL(s2::fwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, ldbc, dt_bias, hloc, P, B, L, D);
     RDX_LAUNCH_CHECK();
@@ -398,7 +398,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
   const dim3 grid((D + s2::CH - 1) / s2::CH, rdx_scan2_chunks(L), dirs * B);
   hipStream_t st = as_stream(stream);
   if (dtype == RDX_BF16) {
-    using T = __hip_bfloat16;
+    using T = hst;
     hipLaunchKernelGGL(s2::bwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)delta, A_log, (const T*)Cm,
                        ldbc, dt_bias, dy, dy_dir_stride, gloc, B, L, D);
     RDX_LAUNCH_CHECK();

@@ -27,21 +27,19 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 sbf16x8;
 typedef __attribute__((ext_vector_type(16))) float sf32x16;
 
 constexpr int SC_T = 256;        // threads
 constexpr int SC_P = 128;        // output positions per strip
 constexpr int SC_PW = SC_P + 2;  // staged input positions (halo 1 each side)
 
-__device__ __forceinline__ sf32x16 sc_mfma(sbf16x8 a, sbf16x8 b, sf32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ sf32x16 sc_mfma(hx8 a, hx8 b, sf32x16 c) {
+  return mfma32x32x16(a, b, c);
 }
 __device__ __forceinline__ uint32_t sc_pack2(float a, float b) {
-  __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  hst x = f2h(a), y = f2h(b);
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
 }
-__device__ __forceinline__ float sc_bf16(float x) { return __bfloat162float(__float2bfloat16(x)); }
 __device__ __forceinline__ float sc_selu(float u) {  // as sincnet.hip selu_fast (bf16-rounded output)
   return 1.0507009873554805f * (u > 0.f ? u : 1.6732632423543772f * (__expf(u) - 1.0f));
 }
@@ -55,15 +53,15 @@ __device__ __forceinline__ int sc_off(int row, int ch) {
 }
 
 struct SConvArgs {
-  const __hip_bfloat16* x;  // [N, H, W, CI]
-  const __hip_bfloat16* w;  // [KH*3][CO][CI] (tap-major, prepared on the host)
-  __hip_bfloat16* y;        // [N, Ho, W, CO]
-  __hip_bfloat16* y2;       // optional: selu(bn(y + cb)) [N, Ho, W, CO]
+  const hst* x;  // [N, H, W, CI]
+  const hst* w;  // [KH*3][CO][CI] (tap-major, prepared on the host)
+  hst* y;        // [N, Ho, W, CO]
+  hst* y2;       // optional: selu(bn(y + cb)) [N, Ho, W, CO]
   const float* bn;          // [4][CO]: conv bias cb, running mean, invstd * gamma, beta (frozen BN); the
                             //   backward epilogue reads a fifth row, invstd
-  const __hip_bfloat16* c;  // backward epilogue: the saved pre-activation [N, Ho, W, CO]
+  const hst* c;  // backward epilogue: the saved pre-activation [N, Ho, W, CO]
   float* sums;              // backward epilogue: [3][CO] d conv_bias | d gamma | d beta (fp32 atomics)
-  const __hip_bfloat16* res;  // optional [N, Ho, W, CO]: y = bf16(bf16(conv) + res) (a residual branch's gradient)
+  const hst* res;  // optional [N, Ho, W, CO]: y = bf16(bf16(conv) + res) (a residual branch's gradient)
   int N, H, W, Ho, ph;
   int rows_per;             // output rows per workgroup (grid.z chunks of the Ho rows)
 };
@@ -72,7 +70,7 @@ struct SConvArgs {
 // (ho + kh) % (KH + 1), and the row the next output row adds is loaded into registers while the current
 // row's MFMAs run, then written to the slot the current row no longer needs (one barrier per row).
 template <int CI>
-__device__ __forceinline__ void sc_load_row(uint4* regs, const __hip_bfloat16* x, int n, int hi, int H, int W, int p0) {
+__device__ __forceinline__ void sc_load_row(uint4* regs, const hst* x, int n, int hi, int H, int W, int p0) {
   constexpr int XCH = CI / 8, NV = (SC_PW * XCH + SC_T - 1) / SC_T;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -107,7 +105,7 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   // the epilogue's per-channel BN parameters (up to 5 x CO fp32) in LDS: read per output element, they were
   // global loads ordered behind the previous group's stores (y may alias bn / c for the compiler)
   float* sbn = reinterpret_cast<float*>(xs + NSLOT * SLOT);
-  const __hip_bfloat16* __restrict__ cpre_src = a.c;
+  const hst* __restrict__ cpre_src = a.c;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n = blockIdx.y, p0 = blockIdx.x * SC_P;
   const int ho0 = blockIdx.z * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
@@ -187,11 +185,11 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
       for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
         for (int s = 0; s < CI / 16; ++s) {
-          const sbf16x8 xf = *reinterpret_cast<const sbf16x8*>(xk + sc_off<CI>(pw + kw, 2 * s + h));
+          const hx8 xf = *reinterpret_cast<const hx8*>(xk + sc_off<CI>(pw + kw, 2 * s + h));
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
             const int rowc = (kh * 3 + kw) * CO + t * 32 + r;
-            const sbf16x8 wf = *reinterpret_cast<const sbf16x8*>(ws + sc_off<CI>(rowc, 2 * s + h));
+            const hx8 wf = *reinterpret_cast<const hx8*>(ws + sc_off<CI>(rowc, 2 * s + h));
             acc[t] = sc_mfma(wf, xf, acc[t]);  // Y^T tile: rows co, columns positions
           }
         }
@@ -209,8 +207,8 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
           for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
           if constexpr (kBnBwd) {
             const uint2 cc = cpre[t][g];
-            const float cv[4] = {__uint_as_float(cc.x << 16), __uint_as_float(cc.x & 0xffff0000u),
-                                 __uint_as_float(cc.y << 16), __uint_as_float(cc.y & 0xffff0000u)};
+            const float cv[4] = {hlo(cc.x), hhi(cc.x),
+                                 hlo(cc.y), hhi(cc.y)};
             const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
             const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
             const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
@@ -226,7 +224,7 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
               const float xhat = zc * pis[e];
               const float u = fmaf(zc, psg[e], pbb[e]);
               const float sd = u > 0.f ? 1.0507009873554805f : 1.0507009873554805f * 1.6732632423543772f * __expf(u);
-              const float du = sc_bf16(v[e]) * sd;
+              const float du = hround(v[e]) * sd;
               dz[e] = du * psg[e];
               bsum[0][t][g][e] += dz[e];
               bsum[1][t][g][e] = fmaf(du, xhat, bsum[1][t][g][e]);
@@ -237,10 +235,10 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
           }
           if (a.res) {   // the sum autograd would form: the bf16 convolution output plus the residual gradient
             const uint2 rr = rres[kBnBwd ? 0 : t][g];
-            v[0] = sc_bf16(v[0]) + __uint_as_float(rr.x << 16);
-            v[1] = sc_bf16(v[1]) + __uint_as_float(rr.x & 0xffff0000u);
-            v[2] = sc_bf16(v[2]) + __uint_as_float(rr.y << 16);
-            v[3] = sc_bf16(v[3]) + __uint_as_float(rr.y & 0xffff0000u);
+            v[0] = hround(v[0]) + hlo(rr.x);
+            v[1] = hround(v[1]) + hhi(rr.x);
+            v[2] = hround(v[2]) + hlo(rr.y);
+            v[3] = hround(v[3]) + hhi(rr.y);
           }
           *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]));
           if (a.y2) {
@@ -253,7 +251,7 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
             float u[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e)  // the arithmetic of bnselu_fwd_kernel on the bf16 conv output
-              u[e] = sc_selu(fmaf((sc_bf16(v[e]) + pcb[e]) - pmu[e], psg[e], pbb[e]));
+              u[e] = sc_selu(fmaf((hround(v[e]) + pcb[e]) - pmu[e], psg[e], pbb[e]));
             *reinterpret_cast<uint2*>(a.y2 + obase + co) = make_uint2(sc_pack2(u[0], u[1]), sc_pack2(u[2], u[3]));
           }
         }
@@ -296,16 +294,14 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
 
 // ---------------------------------------------------------------------------- weight gradient ------
 struct SWgradArgs {
-  const __hip_bfloat16* x;   // [N, H, W, CI]
-  const __hip_bfloat16* dy;  // [N, Ho, W, CO]
+  const hst* x;   // [N, H, W, CI]
+  const hst* dy;  // [N, Ho, W, CO]
   float* part;               // [gridDim.x][KH*3][CO][CI]
   int N, H, W, Ho, ph;
   int64_t units;             // N * strips * nz
   int strips, nz, rows_per;  // 128-position strips, row chunks, rows per chunk
 };
 
-typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 sbf16x4v;
-typedef __attribute__((address_space(3))) sbf16x4v lds_sbf16x4v;
 
 // Row-major [pos][C] image in LDS as 8-row x 32-channel subtiles of 512 B, the 16-byte chunk XOR-swizzled by
 // (row >> 2) & 3: conflict-free for the hardware-transposed ds_read_b64_tr_b16 reads below.
@@ -317,14 +313,14 @@ __device__ __forceinline__ int sc_img(int row, int ch) {
 // [c0 + (lane & 31)], two ds_read_b64_tr_b16. Both operands of the weight-gradient MFMA use this same
 // permuted position order, so the reduction over positions is unaffected.
 template <int C>
-__device__ __forceinline__ sbf16x8 sc_read_tr(const char* img, int r0, int c0, int s, int lane) {
+__device__ __forceinline__ hx8 sc_read_tr(const char* img, int r0, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = r0 + 16 * s + 4 * (g >> 1) + (i >> 2);
   const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
   const int sub = 2 * (col & 7);
-  const sbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_sbf16x4v*)(img + sc_img<C>(row, col >> 3) + sub));
-  const sbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_sbf16x4v*)(img + sc_img<C>(row + 8, col >> 3) + sub));
-  sbf16x8 r;
+  const hx4v lo = ds_tr4((img + sc_img<C>(row, col >> 3) + sub));
+  const hx4v hi = ds_tr4((img + sc_img<C>(row + 8, col >> 3) + sub));
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = lo[j];
@@ -541,10 +537,10 @@ extern "C" int rdx_sconv_fwd(const void* x, const void* w, void* y, void* y2, co
   RDX_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && (kh == 1 || kh == 2) && ph >= 0 && ph <= kh);
   RDX_REQUIRE(al(x) && al(w) && al(y) && (!y2 || (al(y2) && bn)));
   SConvArgs a;
-  a.x = (const __hip_bfloat16*)x;
-  a.w = (const __hip_bfloat16*)w;
-  a.y = (__hip_bfloat16*)y;
-  a.y2 = (__hip_bfloat16*)y2;
+  a.x = (const hst*)x;
+  a.w = (const hst*)w;
+  a.y = (hst*)y;
+  a.y2 = (hst*)y2;
   a.bn = bn;
   a.c = nullptr;
   a.sums = nullptr;
@@ -568,14 +564,14 @@ extern "C" int rdx_sconv_fwd_res(const void* x, const void* w, void* y, const vo
   RDX_REQUIRE(x && w && y && res && N > 0 && H > 0 && W > 0 && (kh == 1 || kh == 2) && ph >= 0 && ph <= kh);
   RDX_REQUIRE(al(x) && al(w) && al(y) && al(res));
   SConvArgs a;
-  a.x = (const __hip_bfloat16*)x;
-  a.w = (const __hip_bfloat16*)w;
-  a.y = (__hip_bfloat16*)y;
+  a.x = (const hst*)x;
+  a.w = (const hst*)w;
+  a.y = (hst*)y;
   a.y2 = nullptr;
   a.bn = nullptr;
   a.c = nullptr;
   a.sums = nullptr;
-  a.res = (const __hip_bfloat16*)res;
+  a.res = (const hst*)res;
   a.N = N;
   a.H = H;
   a.W = W;
@@ -598,12 +594,12 @@ extern "C" int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void*
   RDX_REQUIRE(al(dy) && al(w) && al(c) && al(dc) && N <= 65535);
   if (!((ci == 32 && co == 32) || (ci == 64 && co == 64)) || kh != 2) return RDX_EUNSUPPORTED;
   SConvArgs a;
-  a.x = (const __hip_bfloat16*)dy;
-  a.w = (const __hip_bfloat16*)w;
-  a.y = (__hip_bfloat16*)dc;
+  a.x = (const hst*)dy;
+  a.w = (const hst*)w;
+  a.y = (hst*)dc;
   a.y2 = nullptr;
   a.bn = bn;
-  a.c = (const __hip_bfloat16*)c;
+  a.c = (const hst*)c;
   a.sums = sums;
   a.res = nullptr;
   a.N = N;
@@ -641,8 +637,8 @@ extern "C" int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* 
   RDX_REQUIRE(x && dy && dw && part && N > 0 && H > 0 && W > 0 && (kh == 1 || kh == 2) && ph >= 0 && ph <= kh);
   RDX_REQUIRE(al(x) && al(dy));
   SWgradArgs a;
-  a.x = (const __hip_bfloat16*)x;
-  a.dy = (const __hip_bfloat16*)dy;
+  a.x = (const hst*)x;
+  a.dy = (const hst*)dy;
   a.part = part;
   a.N = N;
   a.H = H;

@@ -24,23 +24,23 @@ constexpr int SN_THREADS = 256;
 constexpr int SN_VEC = 8;
 
 template <typename T> struct Vec8;
-template <> struct Vec8<__hip_bfloat16> {
+template <> struct Vec8<hst> {
   using raw = uint4;  // 8 x bf16
-  static __device__ __forceinline__ void load(const __hip_bfloat16* p, float* v) {
+  static __device__ __forceinline__ void load(const hst* p, float* v) {
     uint4 r = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(w[i] << 16);
-      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      v[2 * i] = hlo(w[i]);
+      v[2 * i + 1] = hhi(w[i]);
     }
   }
-  static __device__ __forceinline__ void store(__hip_bfloat16* p, const float* v) {
+  static __device__ __forceinline__ void store(hst* p, const float* v) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t lo = __bfloat16_as_ushort(__float2bfloat16(v[2 * i]));
-      const uint32_t hi = __bfloat16_as_ushort(__float2bfloat16(v[2 * i + 1]));
+      const uint32_t lo = hbits_of(f2h(v[2 * i]));
+      const uint32_t hi = hbits_of(f2h(v[2 * i + 1]));
       w[i] = lo | (hi << 16);
     }
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -266,15 +266,15 @@ constexpr int B0_CPL = 4;                         // channels per lane
 constexpr int B0_LPC = B0_C / B0_CPL;             // lanes per column
 constexpr int B0_STRIP = SN_THREADS / B0_LPC;     // columns per unit
 
-__device__ __forceinline__ uint2 b0_tap(const __hip_bfloat16* __restrict__ row, int wo, int W, int cg) {
+__device__ __forceinline__ uint2 b0_tap(const hst* __restrict__ row, int wo, int W, int cg) {
   const int wc = wo < 0 ? 0 : (wo >= W ? W - 1 : wo);
   const uint2 v = *reinterpret_cast<const uint2*>(row + (int64_t)wc * B0_C + B0_CPL * cg);
   const bool ok = wo >= 0 && wo < W;
   return ok ? v : make_uint2(0u, 0u);
 }
 
-__device__ __forceinline__ float b0_lo(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float b0_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float b0_lo(unsigned u) { return hlo(u); }
+__device__ __forceinline__ float b0_hi(unsigned u) { return hhi(u); }
 
 // pdx += sum_k v[k] wt[k][t];  acc[k][t] += xq v[k]
 __device__ __forceinline__ void b0_fma(const uint2 v, int t, float xq, const float (&wt)[B0_CPL][B0_TAPS],
@@ -290,9 +290,9 @@ __device__ __forceinline__ void b0_fma(const uint2 v, int t, float xq, const flo
   }
 }
 
-__global__ __launch_bounds__(SN_THREADS) void b0_bwd_kernel(const __hip_bfloat16* __restrict__ x,
-                                                            const __hip_bfloat16* __restrict__ dc,
-                                                            const __hip_bfloat16* __restrict__ di,
+__global__ __launch_bounds__(SN_THREADS) void b0_bwd_kernel(const hst* __restrict__ x,
+                                                            const hst* __restrict__ dc,
+                                                            const hst* __restrict__ di,
                                                             const float* __restrict__ w1, const float* __restrict__ wd,
                                                             float* __restrict__ dx, float* __restrict__ part, int N,
                                                             int H, int W) {
@@ -317,21 +317,21 @@ __global__ __launch_bounds__(SN_THREADS) void b0_bwd_kernel(const __hip_bfloat16
     const int w = (u - n * strips) * B0_STRIP + threadIdx.x / B0_LPC;
     const bool live = w < W;
     const int wl = live ? w : W - 1;  // dead lanes load a valid column and contribute nothing
-    const __hip_bfloat16* dcn = dc + (int64_t)n * (H + 1) * W * B0_C;
-    const __hip_bfloat16* din = di + (int64_t)n * H * W * B0_C;
+    const hst* dcn = dc + (int64_t)n * (H + 1) * W * B0_C;
+    const hst* din = di + (int64_t)n * H * W * B0_C;
     const int64_t xrow0 = (int64_t)n * H * W;
     uint2 cur[3];  // conv1 output row h: the kh = 1 taps of input row h
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) cur[kw] = b0_tap(dcn, wl + 1 - kw, W, cg);
     for (int h = 0; h < H; ++h) {
       uint2 nxt[3], dv[3];
-      const __hip_bfloat16* rn = dcn + (int64_t)(h + 1) * W * B0_C;
-      const __hip_bfloat16* ri = din + (int64_t)h * W * B0_C;
+      const hst* rn = dcn + (int64_t)(h + 1) * W * B0_C;
+      const hst* ri = din + (int64_t)h * W * B0_C;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) nxt[kw] = b0_tap(rn, wl + 1 - kw, W, cg);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) dv[kw] = b0_tap(ri, wl + 1 - kw, W, cg);
-      const float xq = live ? __bfloat162float(x[xrow0 + (int64_t)h * W + wl]) : 0.f;
+      const float xq = live ? h2f(x[xrow0 + (int64_t)h * W + wl]) : 0.f;
       float pdx = 0.f;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
@@ -374,7 +374,7 @@ using namespace rdx;
       using T = float;                                              \
       __VA_ARGS__;                                                  \
     } else if ((dtype) == RDX_BF16) {                               \
-      using T = __hip_bfloat16;                                     \
+      using T = hst;                                     \
       __VA_ARGS__;                                                  \
     } else {                                                        \
       return RDX_EINVAL;                                            \
@@ -448,13 +448,13 @@ extern "C" int rdx_res_tail_bwd(int dtype, const void* dy, const uint8_t* argmax
 // y = selu(bn(c + cb)) and, for h < H, idn (the bottom row of conv1's window is the downsample's window).
 // Replaces two MIOpen convolutions (each with its own output-zeroing pass) and the separate BN + SELU pass.
 constexpr int B0F_RUN = 8;
-__device__ __forceinline__ float b0_x(const __hip_bfloat16* x, int n, int r, int cc, int H, int W) {
-  return (r >= 0 && r < H && cc >= 0 && cc < W) ? __bfloat162float(x[((int64_t)n * H + r) * W + cc]) : 0.f;
+__device__ __forceinline__ float b0_x(const hst* x, int n, int r, int cc, int H, int W) {
+  return (r >= 0 && r < H && cc >= 0 && cc < W) ? h2f(x[((int64_t)n * H + r) * W + cc]) : 0.f;
 }
 __global__ __launch_bounds__(SN_THREADS) void b0_fwd_kernel(
-    const __hip_bfloat16* __restrict__ x, const float* __restrict__ w1, const float* __restrict__ wd,
-    const float* __restrict__ bn, __hip_bfloat16* __restrict__ c, __hip_bfloat16* __restrict__ y,
-    __hip_bfloat16* __restrict__ idn, int N, int H, int W) {
+    const hst* __restrict__ x, const float* __restrict__ w1, const float* __restrict__ wd,
+    const float* __restrict__ bn, hst* __restrict__ c, hst* __restrict__ y,
+    hst* __restrict__ idn, int N, int H, int W) {
   const int g = threadIdx.x & 3;
   float t1[SN_VEC][6], td[SN_VEC][3], cb[SN_VEC], mu[SN_VEC], sc[SN_VEC], sh[SN_VEC];
 #pragma unroll
@@ -496,13 +496,13 @@ __global__ __launch_bounds__(SN_THREADS) void b0_fwd_kernel(
       acc = fmaf(v1[0], t1[k][3], acc);
       acc = fmaf(v1[1], t1[k][4], acc);
       acc = fmaf(v1[2], t1[k][5], acc);
-      cv[k] = __bfloat162float(__float2bfloat16(acc));
+      cv[k] = h2f(f2h(acc));
       yv[k] = selu_fast(fmaf((cv[k] + cb[k]) - mu[k], sc[k], sh[k]));
       iv[k] = fmaf(v1[0], td[k][0], fmaf(v1[1], td[k][1], v1[2] * td[k][2]));
     }
-    Vec8<__hip_bfloat16>::store(c + (pbase + w) * B0_C + g * SN_VEC, cv);
-    Vec8<__hip_bfloat16>::store(y + (pbase + w) * B0_C + g * SN_VEC, yv);
-    if (h < H) Vec8<__hip_bfloat16>::store(idn + (ibase + w) * B0_C + g * SN_VEC, iv);
+    Vec8<hst>::store(c + (pbase + w) * B0_C + g * SN_VEC, cv);
+    Vec8<hst>::store(y + (pbase + w) * B0_C + g * SN_VEC, yv);
+    if (h < H) Vec8<hst>::store(idn + (ibase + w) * B0_C + g * SN_VEC, iv);
     v0[0] = v0[1]; v0[1] = v0[2]; v0[2] = b0_x(x, n, h - 1, w + 2, H, W);
     v1[0] = v1[1]; v1[1] = v1[2]; v1[2] = b0_x(x, n, h, w + 2, H, W);
   }
@@ -515,8 +515,8 @@ extern "C" int rdx_sincnet_b0_fwd(const void* x, const float* w1, const float* w
   const int64_t nruns = (int64_t)N * (H + 1) * ((W + B0F_RUN - 1) / B0F_RUN);
   RDX_REQUIRE(nruns * 4 < ((int64_t)1 << 31));
   hipLaunchKernelGGL(b0_fwd_kernel, dim3((unsigned)((nruns + SN_THREADS / 4 - 1) / (SN_THREADS / 4))), dim3(SN_THREADS),
-                     0, as_stream(stream), (const __hip_bfloat16*)x, w1, wd, bn, (__hip_bfloat16*)c, (__hip_bfloat16*)y,
-                     (__hip_bfloat16*)idn, N, H, W);
+                     0, as_stream(stream), (const hst*)x, w1, wd, bn, (hst*)c, (hst*)y,
+                     (hst*)idn, N, H, W);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -534,7 +534,7 @@ extern "C" int rdx_sincnet_b0_bwd(const void* x, const void* dc, const void* di,
   if (C != B0_C) return RDX_EUNSUPPORTED;
   const int64_t npix = (int64_t)N * H * W;
   hipLaunchKernelGGL(b0_bwd_kernel, dim3(rdx_sincnet_b0_nblk(npix)), dim3(SN_THREADS), 0, as_stream(stream),
-                     (const __hip_bfloat16*)x, (const __hip_bfloat16*)dc, (const __hip_bfloat16*)di, w1, wd, dx, part,
+                     (const hst*)x, (const hst*)dc, (const hst*)di, w1, wd, dx, part,
                      N, H, W);
   RDX_LAUNCH_CHECK();
   return RDX_OK;

@@ -47,7 +47,7 @@ __device__ __forceinline__ void store16(float* p, const float* v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
 }
-__device__ __forceinline__ void load16_bf(const __hip_bfloat16* p, float* v) {
+__device__ __forceinline__ void load16_bf(const hst* p, float* v) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -55,8 +55,8 @@ __device__ __forceinline__ void load16_bf(const __hip_bfloat16* p, float* v) {
     uint32_t w[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      v[8 * i + 2 * j] = __uint_as_float(w[j] << 16);
-      v[8 * i + 2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      v[8 * i + 2 * j] = hlo(w[j]);
+      v[8 * i + 2 * j + 1] = hhi(w[j]);
     }
   }
 }
@@ -64,7 +64,7 @@ __device__ __forceinline__ void load16_bf(const __hip_bfloat16* p, float* v) {
 struct Bf16x16 {
   uint4 q[2];
 };
-__device__ __forceinline__ Bf16x16 load16_bf_raw(const __hip_bfloat16* p) {
+__device__ __forceinline__ Bf16x16 load16_bf_raw(const hst* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
   return Bf16x16{{q[0], q[1]}};
 }
@@ -74,26 +74,21 @@ __device__ __forceinline__ void unpack16_bf(const Bf16x16& t, float* v) {
     uint32_t w[4] = {t.q[i].x, t.q[i].y, t.q[i].z, t.q[i].w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      v[8 * i + 2 * j] = __uint_as_float(w[j] << 16);
-      v[8 * i + 2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      v[8 * i + 2 * j] = hlo(w[j]);
+      v[8 * i + 2 * j + 1] = hhi(w[j]);
     }
   }
 }
-__device__ __forceinline__ uint32_t bf16_bits(float f) {
-  __hip_bfloat16 b = __float2bfloat16(f);
-  return (uint32_t)(*reinterpret_cast<uint16_t*>(&b));
-}
-__device__ __forceinline__ void store16_bf(__hip_bfloat16* p, const float* v) {
+__device__ __forceinline__ void store16_bf(hst* p, const float* v) {
   uint4* q = reinterpret_cast<uint4*>(p);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = bf16_bits(v[8 * i + 2 * j]) | (bf16_bits(v[8 * i + 2 * j + 1]) << 16);
+    for (int j = 0; j < 4; ++j) w[j] = hbits(v[8 * i + 2 * j]) | (hbits(v[8 * i + 2 * j + 1]) << 16);
     q[i] = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
-__device__ __forceinline__ float bf16_round(float f) { return __bfloat162float(__float2bfloat16(f)); }
 
 // mean / rstd of a row held as 16 values per lane (two-pass, biased variance like torch)
 __device__ __forceinline__ void row_stats(const float* v, float eps, float& mean, float& rstd) {
@@ -181,7 +176,7 @@ struct Ln1Args {
   const float* Aq;  // [r, E] lora_A (q), null without LoRA
   const float* Av;  // [r, E] lora_A (v)
   Drop dq, dv;      // LoRA dropouts (q, v)
-  __hip_bfloat16* x1;  // [M, ldx]: LN1 output in [0, E), LoRA down-projection in [E, E + 2r)
+  hst* x1;  // [M, ldx]: LN1 output in [0, E), LoRA down-projection in [E, E + 2r)
   int64_t ldx;
   float* gate;  // [M, H]
   float* mean;
@@ -190,7 +185,7 @@ struct Ln1Args {
   // optional residual prologue (the previous layer's last step): h = h2 + drop(delta) is computed here and
   // written to hout (h is then unused)
   const float* h2;
-  const __hip_bfloat16* delta;
+  const hst* delta;
   Drop dres;
   float* hout;
 };
@@ -204,23 +199,23 @@ struct Ln1Args {
 constexpr int WL_LN1_ROWS = WL_LN1_ROWS_DEF;
 constexpr int WL_LN1_THREADS = WL_LN1_ROWS * RDX_WAVE;
 
-__device__ __forceinline__ void stage_lora_a(__hip_bfloat16* sA, const float* Aq, const float* Av) {
+__device__ __forceinline__ void stage_lora_a(hst* sA, const float* Aq, const float* Av) {
   // WL_R2 * WL_E floats over WL_LN1_THREADS threads, 4 float4 per pass
   constexpr int kN = WL_R2 * WL_E / 4;
   for (int i = threadIdx.x; i < kN; i += WL_LN1_THREADS) {
     const int k = (4 * i) / WL_E, e = (4 * i) % WL_E;
     const float* src = k < WL_R2 / 2 ? Aq + (int64_t)k * WL_E + e : Av + (int64_t)(k - WL_R2 / 2) * WL_E + e;
     const float4 t = *reinterpret_cast<const float4*>(src);
-    const uint32_t w0 = bf16_bits(t.x) | (bf16_bits(t.y) << 16), w1 = bf16_bits(t.z) | (bf16_bits(t.w) << 16);
+    const uint32_t w0 = hbits(t.x) | (hbits(t.y) << 16), w1 = hbits(t.z) | (hbits(t.w) << 16);
     *reinterpret_cast<uint2*>(sA + 4 * i) = make_uint2(w0, w1);
   }
 }
 // 16 consecutive bf16 of an LDS row as fp32
-__device__ __forceinline__ void lds16_bf(const __hip_bfloat16* p, float* v) { load16_bf(p, v); }
+__device__ __forceinline__ void lds16_bf(const hst* p, float* v) { load16_bf(p, v); }
 
 template <bool kLora>
 __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
-  __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[kLora ? WL_R2 * WL_E : 8];
+  __shared__ __attribute__((aligned(16))) hst sA[kLora ? WL_R2 * WL_E : 8];
   __shared__ __attribute__((aligned(16))) float swg[8 * 64];
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * WL_LN1_ROWS + (threadIdx.x >> 6);
@@ -251,7 +246,7 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
     float mean, rstd;
     row_stats(v, a.eps, mean, rstd);
 #pragma unroll
-    for (int i = 0; i < WL_VPL; ++i) v[i] = bf16_round((v[i] - mean) * rstd * gm[i] + bt[i]);
+    for (int i = 0; i < WL_VPL; ++i) v[i] = hround((v[i] - mean) * rstd * gm[i] + bt[i]);
     store16_bf(a.x1 + m * a.ldx + e0, v);
     if (lane == 0) {
       a.mean[m] = mean;
@@ -289,20 +284,20 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
       acc[k] = s;
     }
     float tot = wave_sum16(acc, lane);
-    if ((lane & 3) == 0) a.x1[m * a.ldx + WL_E + sum16_index(lane)] = __float2bfloat16(tot);
+    if ((lane & 3) == 0) a.x1[m * a.ldx + WL_E + sum16_index(lane)] = f2h(tot);
   }
 }
 
 // h2 = h + drop(delta) (fp32, stored), x = LN(h2) (bf16), mean / rstd saved
 struct AddLnArgs {
   const float* h;
-  const __hip_bfloat16* delta;
+  const hst* delta;
   Drop d;
   float* h2;
   const float* gamma;
   const float* beta;
   float eps;
-  __hip_bfloat16* x;
+  hst* x;
   float* mean;
   float* rstd;
   int64_t M;
@@ -337,7 +332,7 @@ __global__ __launch_bounds__(256) void wl_add_ln_fwd_kernel(AddLnArgs a) {
 
 // out = h + drop(delta) over n = M * E elements (8 per thread)
 __global__ __launch_bounds__(256) void wl_residual_kernel(const float* __restrict__ h,
-                                                          const __hip_bfloat16* __restrict__ delta, Drop d,
+                                                          const hst* __restrict__ delta, Drop d,
                                                           float* __restrict__ out, int64_t n) {
   const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (i0 >= n) return;
@@ -348,7 +343,7 @@ __global__ __launch_bounds__(256) void wl_residual_kernel(const float* __restric
   uint32_t w[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    float dv = __uint_as_float((j & 1) ? (w[j >> 1] & 0xffff0000u) : (w[j >> 1] << 16));
+    float dv = (j & 1) ? hhi(w[j >> 1]) : hlo(w[j >> 1]);
     x[j] += dv * (d.thr ? drop_scale(d, seed, (uint64_t)(i0 + j)) : 1.0f);
   }
   reinterpret_cast<float4*>(out + i0)[0] = make_float4(x[0], x[1], x[2], x[3]);
@@ -357,7 +352,7 @@ __global__ __launch_bounds__(256) void wl_residual_kernel(const float* __restric
 
 // grad of drop(): out = drop_mask * g (fp32 in, bf16 out), n elements (8 per thread)
 __global__ __launch_bounds__(256) void wl_dropout_bwd_kernel(const float* __restrict__ g, Drop d,
-                                                             __hip_bfloat16* __restrict__ out, int64_t n) {
+                                                             hst* __restrict__ out, int64_t n) {
   const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (i0 >= n) return;
   const uint64_t seed = d.thr ? attn_seed(d.seed_dev, d.salt) : 0;
@@ -368,7 +363,7 @@ __global__ __launch_bounds__(256) void wl_dropout_bwd_kernel(const float* __rest
   for (int j = 0; j < 4; ++j) {
     float s0 = d.thr ? drop_scale(d, seed, (uint64_t)(i0 + 2 * j)) : 1.0f;
     float s1 = d.thr ? drop_scale(d, seed, (uint64_t)(i0 + 2 * j + 1)) : 1.0f;
-    w[j] = bf16_bits(x[2 * j] * s0) | (bf16_bits(x[2 * j + 1] * s1) << 16);
+    w[j] = hbits(x[2 * j] * s0) | (hbits(x[2 * j + 1] * s1) << 16);
   }
   *reinterpret_cast<uint4*>(out + i0) = make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -380,9 +375,9 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
 
 // y = gelu(u) (mode 0) or du = dy * gelu'(u) (mode 1); bf16, 8 elements per thread
 template <int kMode>
-__global__ __launch_bounds__(256) void wl_gelu_kernel(const __hip_bfloat16* __restrict__ u,
-                                                      const __hip_bfloat16* __restrict__ dy,
-                                                      __hip_bfloat16* __restrict__ out, int64_t n) {
+__global__ __launch_bounds__(256) void wl_gelu_kernel(const hst* __restrict__ u,
+                                                      const hst* __restrict__ dy,
+                                                      hst* __restrict__ out, int64_t n) {
   const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (i0 >= n) return;
   uint4 t = *reinterpret_cast<const uint4*>(u + i0);
@@ -394,16 +389,16 @@ __global__ __launch_bounds__(256) void wl_gelu_kernel(const __hip_bfloat16* __re
   uint32_t o[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float x0 = __uint_as_float(w[j] << 16), x1 = __uint_as_float(w[j] & 0xffff0000u);
+    float x0 = hlo(w[j]), x1 = hhi(w[j]);
     float y0, y1;
     if (kMode == 0) {
       y0 = gelu_erf(x0);
       y1 = gelu_erf(x1);
     } else {
-      y0 = __uint_as_float(gw[j] << 16) * gelu_erf_grad(x0);
-      y1 = __uint_as_float(gw[j] & 0xffff0000u) * gelu_erf_grad(x1);
+      y0 = hlo(gw[j]) * gelu_erf_grad(x0);
+      y1 = hhi(gw[j]) * gelu_erf_grad(x1);
     }
-    o[j] = bf16_bits(y0) | (bf16_bits(y1) << 16);
+    o[j] = hbits(y0) | (hbits(y1) << 16);
   }
   *reinterpret_cast<uint4*>(out + i0) = make_uint4(o[0], o[1], o[2], o[3]);
 }
@@ -411,7 +406,7 @@ __global__ __launch_bounds__(256) void wl_gelu_kernel(const __hip_bfloat16* __re
 // LN backward with residual: dh = dres + rstd * (g - mean(g) - xhat * mean(g xhat)), g = dx * gamma.
 // Optionally also ddrop = drop_mask * dh (bf16): the gradient into the dropout that fed h.
 struct LnBwdArgs {
-  const __hip_bfloat16* dx;  // [M, ldd] (first E columns used)
+  const hst* dx;  // [M, ldd] (first E columns used)
   int64_t ldd;
   const float* h;  // LN input [M, E]
   const float* mean;
@@ -420,7 +415,7 @@ struct LnBwdArgs {
   const float* dres;  // [M, E] or null
   float* dh;          // [M, E]
   Drop d;
-  __hip_bfloat16* ddrop;  // [M, E] or null
+  hst* ddrop;  // [M, E] or null
   int64_t M;
 };
 
@@ -469,7 +464,7 @@ __global__ __launch_bounds__(256) void wl_ln_bwd_kernel(LnBwdArgs a) {
 // LN1 backward: dx1 = dX1[:, :E] + gate backward + LoRA-A backward; dh = dres + LN1_bwd(dx1).
 // Also writes the dropped LN output of each adapter (xd[0] q, xd[1] v) for the dA GEMMs.
 struct Ln1BwdArgs {
-  const __hip_bfloat16* dx1;  // [M, ldx] = d [x1 | a] from the qkv GEMM backward
+  const hst* dx1;  // [M, ldx] = d [x1 | a] from the qkv GEMM backward
   int64_t ldx;
   const float* dgate;  // [M, H]
   const float* h;
@@ -483,7 +478,7 @@ struct Ln1BwdArgs {
   Drop dq, dv;
   const float* dres;  // [M, E]
   float* dh;
-  __hip_bfloat16* xd;  // [2, M, E] or null
+  hst* xd;  // [2, M, E] or null
   int64_t M;
   // optional: the gradient this layer's INPUT receives as a hidden state of the layer-weighted sum,
   // sw[0] * sg (sw a device scalar: softmax(w)_l), added into dh
@@ -491,12 +486,12 @@ struct Ln1BwdArgs {
   const float* sw;
   // optional: ddrop = drop_prev(dh) bf16, the gradient of the previous layer's dropped FFN output
   Drop dprev;
-  __hip_bfloat16* ddrop;
+  hst* ddrop;
 };
 
 template <bool kLora>
 __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[kLora ? WL_R2 * WL_E : 8];
+  __shared__ __attribute__((aligned(16))) hst sA[kLora ? WL_R2 * WL_E : 8];
   __shared__ __attribute__((aligned(16))) float swg[8 * 64];
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * WL_LN1_ROWS + (threadIdx.x >> 6);
@@ -525,7 +520,7 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a
   if (!live) return;  // after the only barrier
   unpack16_bf(dxr, dx);
 #pragma unroll
-  for (int i = 0; i < WL_VPL; ++i) x1[i] = bf16_round((x[i] - mean) * rstd * gm[i] + x1[i]);
+  for (int i = 0; i < WL_VPL; ++i) x1[i] = hround((x[i] - mean) * rstd * gm[i] + x1[i]);
   // gate: gate = ga (gb c - 1) + 2
   float z[8];
   gate_z(a.g, swg, x1, lane, z);
@@ -611,11 +606,11 @@ constexpr int WL_LG_COLS = 128;
 constexpr int WL_LG_PAD = WL_LG_COLS + 1;  // LDS row stride (floats): the dB read walks k
 
 struct LoraGradArgs {
-  const __hip_bfloat16* dqkv;  // [M, ldq]: dq at column 0, dv at column 2E
+  const hst* dqkv;  // [M, ldq]: dq at column 0, dv at column 2E
   int64_t ldq;
-  const __hip_bfloat16* x1;    // [M, ldx]: x1 in [0, E), a in [E, E + 2r)
+  const hst* x1;    // [M, ldx]: x1 in [0, E), a in [E, E + 2r)
   int64_t ldx;
-  const __hip_bfloat16* dx1;   // [M, ldd]: d a in [E, E + 2r)
+  const hst* dx1;   // [M, ldd]: d a in [E, E + 2r)
   int64_t ldd;
   Drop dq, dv;
   float scale;
@@ -623,9 +618,9 @@ struct LoraGradArgs {
   int64_t M;
 };
 
-__device__ __forceinline__ float2 bf16x2_at(const __hip_bfloat16* p) {
+__device__ __forceinline__ float2 hx2_at(const hst* p) {
   const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
-  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+  return make_float2(hlo(u), hhi(u));
 }
 
 template <int RPW>
@@ -652,17 +647,17 @@ __global__ __launch_bounds__(256, 2) void wl_lora_grad_kernel(LoraGradArgs a, in
       const int64_t m = m0 + rr;
       float v = 0.f;
       if (m < a.M)
-        v = c < WL_R2 ? __bfloat162float(a.x1[m * a.ldx + WL_E + c])
-                      : __bfloat162float(a.dx1[m * a.ldd + WL_E + c - WL_R2]);
+        v = c < WL_R2 ? h2f(a.x1[m * a.ldx + WL_E + c])
+                      : h2f(a.dx1[m * a.ldd + WL_E + c - WL_R2]);
       srow[rr][c] = v;
     }
     float2 gq[RPW], gv[RPW], xx[RPW];
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int64_t m = min(m0 + w * RPW + j, a.M - 1);
-      gq[j] = bf16x2_at(a.dqkv + m * a.ldq + e);
-      gv[j] = bf16x2_at(a.dqkv + m * a.ldq + 2 * WL_E + e);
-      xx[j] = bf16x2_at(a.x1 + m * a.ldx + e);
+      gq[j] = hx2_at(a.dqkv + m * a.ldq + e);
+      gv[j] = hx2_at(a.dqkv + m * a.ldq + 2 * WL_E + e);
+      xx[j] = hx2_at(a.x1 + m * a.ldx + e);
     }
     __syncthreads();  // srow staged (the other buffer is still read by nobody: one barrier per chunk)
 #pragma unroll
@@ -723,7 +718,7 @@ __global__ __launch_bounds__(256, 2) void wl_lora_grad_kernel(LoraGradArgs a, in
 // Wext[:, E:E+2r] <- s * B (q rows 0..E-1 columns E..E+r-1, v rows 2E..3E-1 columns E+r..E+2r-1);
 // one launch for every layer. Other rows of those columns stay zero.
 __global__ __launch_bounds__(256) void wl_lora_pack_kernel(int nl, const float* const* bq, const float* const* bv,
-                                                           __hip_bfloat16* const* wext, int64_t ldw, int r,
+                                                           hst* const* wext, int64_t ldw, int r,
                                                            float scale) {
   const int l = blockIdx.y;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over 2 * E * r
@@ -734,7 +729,7 @@ __global__ __launch_bounds__(256) void wl_lora_pack_kernel(int nl, const float* 
   const int k = (int)(rem % r);
   const float* b = which ? bv[l] : bq[l];  // lora_B weight [E, r]
   const int64_t wrow = which ? 2 * WL_E + row : row;
-  wext[l][wrow * ldw + WL_E + which * r + k] = __float2bfloat16(scale * b[row * r + k]);
+  wext[l][wrow * ldw + WL_E + which * r + k] = f2h(scale * b[row * r + k]);
 }
 
 }  // namespace rdx
@@ -775,7 +770,7 @@ int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float 
   RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
   RDX_REQUIRE(ldx % 8 == 0);
   Ln1Args a{h, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
-            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M,
+            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<hst*>(x1), ldx, gate, mean, rstd, M,
             nullptr, nullptr, mk_drop(nullptr, 0, 0.f), nullptr};
   return ln1_fwd_launch(a, lora, stream);
 }
@@ -790,8 +785,8 @@ int rdx_wl_res_ln1_fwd(const float* h2, const void* delta, int salt_res, float p
   RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
   RDX_REQUIRE(ldx % 8 == 0);
   Ln1Args a{nullptr, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
-            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<__hip_bfloat16*>(x1), ldx, gate, mean, rstd, M,
-            h2, reinterpret_cast<const __hip_bfloat16*>(delta), mk_drop(seed_dev, salt_res, p_res), hout};
+            mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<hst*>(x1), ldx, gate, mean, rstd, M,
+            h2, reinterpret_cast<const hst*>(delta), mk_drop(seed_dev, salt_res, p_res), hout};
   return ln1_fwd_launch(a, lora, stream);
 }
 
@@ -799,8 +794,8 @@ int rdx_wl_add_ln_fwd(const float* h, const void* delta, const int64_t* seed_dev
                       const float* gamma, const float* beta, float eps, void* x, float* mean, float* rstd, int64_t M,
                       int E, void* stream) {
   RDX_REQUIRE(h && delta && h2 && gamma && beta && x && mean && rstd && M > 0 && E == WL_E);
-  AddLnArgs a{h, reinterpret_cast<const __hip_bfloat16*>(delta), mk_drop(seed_dev, salt, p), h2, gamma, beta, eps,
-              reinterpret_cast<__hip_bfloat16*>(x), mean, rstd, M};
+  AddLnArgs a{h, reinterpret_cast<const hst*>(delta), mk_drop(seed_dev, salt, p), h2, gamma, beta, eps,
+              reinterpret_cast<hst*>(x), mean, rstd, M};
   hipLaunchKernelGGL(wl_add_ln_fwd_kernel, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return 0;
@@ -810,7 +805,7 @@ int rdx_wl_residual(const float* h, const void* delta, const int64_t* seed_dev, 
                     int64_t n, void* stream) {
   RDX_REQUIRE(h && delta && out && n > 0 && n % 8 == 0);
   hipLaunchKernelGGL(wl_residual_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, as_stream(stream), h,
-                     reinterpret_cast<const __hip_bfloat16*>(delta), mk_drop(seed_dev, salt, p), out, n);
+                     reinterpret_cast<const hst*>(delta), mk_drop(seed_dev, salt, p), out, n);
   RDX_LAUNCH_CHECK();
   return 0;
 }
@@ -819,16 +814,16 @@ int rdx_wl_dropout_bwd(const float* g, const int64_t* seed_dev, int salt, float 
                        void* stream) {
   RDX_REQUIRE(g && out && n > 0 && n % 8 == 0);
   hipLaunchKernelGGL(wl_dropout_bwd_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, as_stream(stream), g,
-                     mk_drop(seed_dev, salt, p), reinterpret_cast<__hip_bfloat16*>(out), n);
+                     mk_drop(seed_dev, salt, p), reinterpret_cast<hst*>(out), n);
   RDX_LAUNCH_CHECK();
   return 0;
 }
 
 int rdx_wl_gelu(int mode, const void* u, const void* dy, void* out, int64_t n, void* stream) {
   RDX_REQUIRE(u && out && n > 0 && n % 8 == 0 && (mode == 0 || (mode == 1 && dy)));
-  const auto* U = reinterpret_cast<const __hip_bfloat16*>(u);
-  const auto* DY = reinterpret_cast<const __hip_bfloat16*>(dy);
-  auto* O = reinterpret_cast<__hip_bfloat16*>(out);
+  const auto* U = reinterpret_cast<const hst*>(u);
+  const auto* DY = reinterpret_cast<const hst*>(dy);
+  auto* O = reinterpret_cast<hst*>(out);
   const dim3 grid((unsigned)((n / 8 + 255) / 256));
   if (mode == 0)
     hipLaunchKernelGGL(wl_gelu_kernel<0>, grid, dim3(256), 0, as_stream(stream), U, DY, O, n);
@@ -842,8 +837,8 @@ int rdx_wl_ln_bwd(const void* dx, int64_t ldd, const float* h, const float* mean
                   const float* gamma, const float* dres, float* dh, const int64_t* seed_dev, int salt, float p,
                   void* ddrop, int64_t M, int E, void* stream) {
   RDX_REQUIRE(dx && h && mean && rstd && gamma && dh && M > 0 && E == WL_E && ldd >= E && ldd % 8 == 0);
-  LnBwdArgs a{reinterpret_cast<const __hip_bfloat16*>(dx), ldd, h, mean, rstd, gamma, dres, dh,
-              mk_drop(seed_dev, salt, p), reinterpret_cast<__hip_bfloat16*>(ddrop), M};
+  LnBwdArgs a{reinterpret_cast<const hst*>(dx), ldd, h, mean, rstd, gamma, dres, dh,
+              mk_drop(seed_dev, salt, p), reinterpret_cast<hst*>(ddrop), M};
   hipLaunchKernelGGL(wl_ln_bwd_kernel, dim3(blocks_rows(M)), dim3(256), 0, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return 0;
@@ -859,10 +854,10 @@ int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const fl
   RDX_REQUIRE((state_grad == nullptr) == (state_weight == nullptr));
   const bool lora = lora_aq != nullptr;
   RDX_REQUIRE(E == WL_E && ldx % 8 == 0 && (!lora || (2 * r == WL_R2 && lora_av && ldx >= E + 2 * r)));
-  Ln1BwdArgs a{reinterpret_cast<const __hip_bfloat16*>(dx1), ldx, dgate, h, mean, rstd, gamma, beta,
+  Ln1BwdArgs a{reinterpret_cast<const hst*>(dx1), ldx, dgate, h, mean, rstd, gamma, beta,
                GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
-               dres, dh, reinterpret_cast<__hip_bfloat16*>(xd), M, state_grad, state_weight,
-               mk_drop(seed_dev, salt_prev, p_prev), reinterpret_cast<__hip_bfloat16*>(ddrop_prev)};
+               dres, dh, reinterpret_cast<hst*>(xd), M, state_grad, state_weight,
+               mk_drop(seed_dev, salt_prev, p_prev), reinterpret_cast<hst*>(ddrop_prev)};
   if (lora)
     hipLaunchKernelGGL(wl_ln1_bwd_kernel<true>, dim3(blocks_ln1(M)), dim3(WL_LN1_THREADS), 0, as_stream(stream), a);
   else
@@ -886,8 +881,8 @@ int rdx_wl_lora_grad(const void* dqkv, int64_t ldq, const void* x1, int64_t ldx,
   RDX_REQUIRE(dqkv && x1 && dx1 && daq && dbq && dav && dbv && M > 0 && E == WL_E && 2 * r == WL_R2);
   RDX_REQUIRE(ldq >= 3 * (int64_t)E && ldx >= E + 2 * r && ldd >= E + 2 * r);
   RDX_REQUIRE(ldq % 2 == 0 && ldx % 2 == 0 && ((uintptr_t)dqkv & 3) == 0 && ((uintptr_t)x1 & 3) == 0);
-  LoraGradArgs a{reinterpret_cast<const __hip_bfloat16*>(dqkv), ldq, reinterpret_cast<const __hip_bfloat16*>(x1), ldx,
-                 reinterpret_cast<const __hip_bfloat16*>(dx1), ldd, mk_drop(seed_dev, salt_q, p_lora),
+  LoraGradArgs a{reinterpret_cast<const hst*>(dqkv), ldq, reinterpret_cast<const hst*>(x1), ldx,
+                 reinterpret_cast<const hst*>(dx1), ldd, mk_drop(seed_dev, salt_q, p_lora),
                  mk_drop(seed_dev, salt_v, p_lora), scale, daq, dbq, dav, dbv, M};
   // 32-row chunks; a block walks nch of them so the 4096 fp32 atomics it ends with are amortised over
   // >= 64 rows once M allows (atomics run at ~1.3 TB/s of added bytes chip-wide), keeping >= 400 blocks.
@@ -904,7 +899,7 @@ int rdx_wl_lora_pack(int nl, const float* const* bq, const float* const* bv, voi
   RDX_REQUIRE(nl > 0 && bq && bv && wext && E == WL_E && r > 0 && ldw >= E + 2 * r);
   const int64_t n = 2 * (int64_t)E * r;
   hipLaunchKernelGGL(wl_lora_pack_kernel, dim3((unsigned)((n + 255) / 256), nl), dim3(256), 0, as_stream(stream), nl,
-                     bq, bv, reinterpret_cast<__hip_bfloat16* const*>(wext), ldw, r, scale);
+                     bq, bv, reinterpret_cast<hst* const*>(wext), ldw, r, scale);
   RDX_LAUNCH_CHECK();
   return 0;
 }

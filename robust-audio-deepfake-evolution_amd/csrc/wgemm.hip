@@ -27,7 +27,6 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 wbf16x8;
 typedef __attribute__((ext_vector_type(4))) float wf32x4;
 typedef __attribute__((ext_vector_type(4))) int wi32x4;
 
@@ -52,24 +51,23 @@ __device__ __forceinline__ float wg_gelu(float x) { return 0.5f * x * (1.0f + er
 __device__ __forceinline__ float wg_gelu_grad(float x) {
   return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
-__device__ __forceinline__ float wg_bf16(float x) { return __bfloat162float(__float2bfloat16(x)); }
 __device__ __forceinline__ uint32_t wg_pack2(float a, float b) {
-  __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+  hst x = f2h(a), y = f2h(b);
   return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
 }
 
 struct WgArgs {
-  const __hip_bfloat16* A;
+  const hst* A;
   int64_t lda;
-  const __hip_bfloat16* B;
+  const hst* B;
   int64_t ldb;
-  __hip_bfloat16* C;
+  hst* C;
   int64_t ldc;
   int M, N, K;
-  const __hip_bfloat16* bias;  // [N] or null
-  const __hip_bfloat16* aux;   // GELU_BWD: u [M, ldaux]
+  const hst* bias;  // [N] or null
+  const hst* aux;   // GELU_BWD: u [M, ldaux]
   int64_t ldaux;
-  __hip_bfloat16* aux_out;     // BIAS_GELU: gelu(u) [M, ldao]
+  hst* aux_out;     // BIAS_GELU: gelu(u) [M, ldao]
   int64_t ldao;
   int tiles_m, tiles_n;
   int splits;                  // split-K factor (1: none); split s covers k-steps [s*nk/S, (s+1)*nk/S)
@@ -168,16 +166,16 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = kk * 4 + fq;
-      wbf16x8 af[FM], bf[FN];
+      hx8 af[FM], bf[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * WTM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const wbf16x8*>(As + row * 128 + 16 * wg_swz(row, ch));
+        af[i] = *reinterpret_cast<const hx8*>(As + row * 128 + 16 * wg_swz(row, ch));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * WTN + j * 16 + fr;
-        bf[j] = *reinterpret_cast<const wbf16x8*>(Bs + row * 128 + 16 * wg_swz(row, ch));
+        bf[j] = *reinterpret_cast<const hx8*>(Bs + row * 128 + 16 * wg_swz(row, ch));
       }
       if (ABL == 2) {                // timing probe: fragments read, no MFMA
 #pragma unroll
@@ -189,7 +187,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16x16x32(bf[j], af[i], acc[i][j]);
       }
     }
   }
@@ -270,10 +268,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (EPI != RDX_EPI_GELU_BWD && g.bias && n0 + c < N) {
           const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n0 + c);
-          v[0] += __uint_as_float(bb.x << 16);
-          v[1] += __uint_as_float(bb.x & 0xffff0000u);
-          v[2] += __uint_as_float(bb.y << 16);
-          v[3] += __uint_as_float(bb.y & 0xffff0000u);
+          v[0] += hlo(bb.x);
+          v[1] += hhi(bb.x);
+          v[2] += hlo(bb.y);
+          v[3] += hhi(bb.y);
         }
         *reinterpret_cast<uint2*>(img + r * PITCH + c * 2) = make_uint2(wg_pack2(v[0], v[1]), wg_pack2(v[2], v[3]));
       }
@@ -288,13 +286,13 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
       const bool full = n + 8 <= N;   // else 4 columns (N % 4 == 0)
       const bool wide = full && g.wide;
       // 8 columns as one 16-byte access, or two 8-byte halves (the second only when full)
-      auto ld8 = [&](const __hip_bfloat16* src) -> uint4 {
+      auto ld8 = [&](const hst* src) -> uint4 {
         if (wide) return *reinterpret_cast<const uint4*>(src);
         const uint2 lo = *reinterpret_cast<const uint2*>(src);
         const uint2 hi = full ? *reinterpret_cast<const uint2*>(src + 4) : make_uint2(0u, 0u);
         return make_uint4(lo.x, lo.y, hi.x, hi.y);
       };
-      auto st8 = [&](__hip_bfloat16* dst, uint4 v) {
+      auto st8 = [&](hst* dst, uint4 v) {
         if (wide) { *reinterpret_cast<uint4*>(dst) = v; return; }
         *reinterpret_cast<uint2*>(dst) = make_uint2(v.x, v.y);
         if (full) *reinterpret_cast<uint2*>(dst + 4) = make_uint2(v.z, v.w);
@@ -306,8 +304,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
         uint32_t o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a0 = __uint_as_float(qw[e] << 16), a1 = __uint_as_float(qw[e] & 0xffff0000u);
-          const float u0 = __uint_as_float(uw[e] << 16), u1 = __uint_as_float(uw[e] & 0xffff0000u);
+          const float a0 = hlo(qw[e]), a1 = hhi(qw[e]);
+          const float u0 = hlo(uw[e]), u1 = hhi(uw[e]);
           o[e] = wg_pack2(a0 * wg_gelu_grad(u0), a1 * wg_gelu_grad(u1));
         }
         q = make_uint4(o[0], o[1], o[2], o[3]);
@@ -318,7 +316,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
         uint32_t o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          o[e] = wg_pack2(wg_gelu(__uint_as_float(qw[e] << 16)), wg_gelu(__uint_as_float(qw[e] & 0xffff0000u)));
+          o[e] = wg_pack2(wg_gelu(hlo(qw[e])), wg_gelu(hhi(qw[e])));
         st8(g.aux_out + (int64_t)m * g.ldao + n, make_uint4(o[0], o[1], o[2], o[3]));
       }
     }
@@ -335,28 +333,28 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void wgemm_kernel(WgArgs g) {
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (EPI != RDX_EPI_GELU_BWD && g.bias) {
         const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
-        v[0] += __uint_as_float(bb.x << 16);
-        v[1] += __uint_as_float(bb.x & 0xffff0000u);
-        v[2] += __uint_as_float(bb.y << 16);
-        v[3] += __uint_as_float(bb.y & 0xffff0000u);
+        v[0] += hlo(bb.x);
+        v[1] += hhi(bb.x);
+        v[2] += hlo(bb.y);
+        v[3] += hhi(bb.y);
       }
-      __hip_bfloat16* cp = g.C + (int64_t)m * g.ldc + n;
+      hst* cp = g.C + (int64_t)m * g.ldc + n;
       if (EPI == RDX_EPI_BIAS) {
         *reinterpret_cast<uint2*>(cp) = make_uint2(wg_pack2(v[0], v[1]), wg_pack2(v[2], v[3]));
       } else if (EPI == RDX_EPI_BIAS_GELU) {
         float u[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = wg_bf16(v[e]);
+        for (int e = 0; e < 4; ++e) u[e] = hround(v[e]);
         *reinterpret_cast<uint2*>(cp) = make_uint2(wg_pack2(u[0], u[1]), wg_pack2(u[2], u[3]));
         *reinterpret_cast<uint2*>(g.aux_out + (int64_t)m * g.ldao + n) =
             make_uint2(wg_pack2(wg_gelu(u[0]), wg_gelu(u[1])), wg_pack2(wg_gelu(u[2]), wg_gelu(u[3])));
       } else {  // RDX_EPI_GELU_BWD
         const uint2 uu = *reinterpret_cast<const uint2*>(g.aux + (int64_t)m * g.ldaux + n);
-        const float u[4] = {__uint_as_float(uu.x << 16), __uint_as_float(uu.x & 0xffff0000u),
-                            __uint_as_float(uu.y << 16), __uint_as_float(uu.y & 0xffff0000u)};
+        const float u[4] = {hlo(uu.x), hhi(uu.x),
+                            hlo(uu.y), hhi(uu.y)};
         float d[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[e] = wg_bf16(v[e]) * wg_gelu_grad(u[e]);
+        for (int e = 0; e < 4; ++e) d[e] = hround(v[e]) * wg_gelu_grad(u[e]);
         *reinterpret_cast<uint2*>(cp) = make_uint2(wg_pack2(d[0], d[1]), wg_pack2(d[2], d[3]));
       }
     }
@@ -487,19 +485,19 @@ extern "C" int rdx_wgemm_bf16_ex(const void* A, int64_t lda, const void* B, int6
     RDX_REQUIRE(need > 0 && ws && al(ws, 16) && ws_bytes >= need && counters && n_counters >= nc);
   }
   WgArgs g;
-  g.A = (const __hip_bfloat16*)A;
+  g.A = (const hst*)A;
   g.lda = lda;
-  g.B = (const __hip_bfloat16*)B;
+  g.B = (const hst*)B;
   g.ldb = ldb;
-  g.C = (__hip_bfloat16*)C;
+  g.C = (hst*)C;
   g.ldc = ldc;
   g.M = M;
   g.N = N;
   g.K = K;
-  g.bias = (const __hip_bfloat16*)bias;
-  g.aux = (const __hip_bfloat16*)aux;
+  g.bias = (const hst*)bias;
+  g.aux = (const hst*)aux;
   g.ldaux = ldaux;
-  g.aux_out = (__hip_bfloat16*)aux_out;
+  g.aux_out = (hst*)aux_out;
   g.ldao = ldao;
   g.tiles_m = g.tiles_n = 0;
   g.splits = splits;

@@ -12,10 +12,7 @@
 
 namespace rdx {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 wrbf16x8;
 typedef __attribute__((ext_vector_type(16))) float wrf32x16;
-typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 wrbf16x4v;
-typedef __attribute__((address_space(3))) wrbf16x4v lds_wrbf16x4v;
 
 constexpr int WR_T = 256;
 constexpr int WR_MAXMC = 256;   // token rows per chunk (multiple of 16)
@@ -25,14 +22,14 @@ __device__ __forceinline__ int wr_img(int row, int ch) {
   return 1024 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 // element j = IMG[16 s + 8 (j >> 2) + 4 h + (j & 3)][c0 + (lane & 31)]
-__device__ __forceinline__ wrbf16x8 wr_read_tr(const char* img, int c0, int s, int lane) {
+__device__ __forceinline__ hx8 wr_read_tr(const char* img, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = 16 * s + 4 * (g >> 1) + (i >> 2);
   const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
   const int sub = 2 * (col & 7);
-  const wrbf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_wrbf16x4v*)(img + wr_img(row, col >> 3) + sub));
-  const wrbf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_wrbf16x4v*)(img + wr_img(row + 8, col >> 3) + sub));
-  wrbf16x8 r;
+  const hx4v lo = ds_tr4((img + wr_img(row, col >> 3) + sub));
+  const hx4v hi = ds_tr4((img + wr_img(row + 8, col >> 3) + sub));
+  hx8 r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     r[j] = lo[j];
@@ -44,7 +41,7 @@ __device__ __forceinline__ wrbf16x8 wr_read_tr(const char* img, int c0, int s, i
 // rows [m0, m0 + mc) x columns [c0, c0 + 64) of a [M][ld] bf16 matrix into an image (zeros outside): every
 // load of the thread is issued before the first LDS store, so their latencies overlap
 constexpr int WR_ITEMS = WR_MAXMC * 8 / WR_T;   // 16-byte items per thread, at most
-__device__ __forceinline__ void wr_gather(uint4 (&v)[WR_ITEMS], const __hip_bfloat16* __restrict__ src, int64_t ld,
+__device__ __forceinline__ void wr_gather(uint4 (&v)[WR_ITEMS], const hst* __restrict__ src, int64_t ld,
                                           int M, int C, int m0, int c0, int mc, bool vec) {
 #pragma unroll
   for (int j = 0; j < WR_ITEMS; ++j) {
@@ -53,13 +50,13 @@ __device__ __forceinline__ void wr_gather(uint4 (&v)[WR_ITEMS], const __hip_bflo
     const int m = m0 + row, c = c0 + 8 * ch;
     v[j] = make_uint4(0u, 0u, 0u, 0u);
     if (i < mc * 8 && m < M) {
-      const __hip_bfloat16* p = src + (int64_t)m * ld + c;
+      const hst* p = src + (int64_t)m * ld + c;
       if (vec && c + 8 <= C) {
         v[j] = *reinterpret_cast<const uint4*>(p);
       } else {
         uint16_t e[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) e[t] = (c + t < C) ? __bfloat16_as_ushort(p[t]) : (uint16_t)0;
+        for (int t = 0; t < 8; ++t) e[t] = (c + t < C) ? hbits_of(p[t]) : (uint16_t)0;
         v[j] = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
                           e[6] | ((uint32_t)e[7] << 16));
       }
@@ -75,8 +72,8 @@ __device__ __forceinline__ void wr_put(char* img, const uint4 (&v)[WR_ITEMS], in
 }
 
 struct WgradArgs {
-  const __hip_bfloat16* dy;   // [M][ldy], columns 0..N-1
-  const __hip_bfloat16* x;    // [M][ldx], columns 0..K-1
+  const hst* dy;   // [M][ldy], columns 0..N-1
+  const hst* x;    // [M][ldx], columns 0..K-1
   int64_t ldy, ldx;
   float* part;                // [S][N][K] partial dW per chunk
   float* partb;               // [S][N] partial db (or null)
@@ -106,8 +103,8 @@ __global__ __launch_bounds__(WR_T) void wgrad_part_kernel(WgradArgs a) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   for (int st = 0; st < mc / 16; ++st)
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr_read_tr(iy, tn * 32, st, lane), wr_read_tr(ix, tk * 32, st, lane),
-                                                  acc, 0, 0, 0);
+    acc = mfma32x32x16(wr_read_tr(iy, tn * 32, st, lane), wr_read_tr(ix, tk * 32, st, lane),
+                                                  acc);
   // D[n][k]: k = tk * 32 + (lane & 31), n = tn * 32 + (i & 3) + 8 (i >> 2) + 4 hh
   const int r = lane & 31, hh = lane >> 5;
   const int k = k0 + tk * 32 + r;
@@ -123,7 +120,7 @@ __global__ __launch_bounds__(WR_T) void wgrad_part_kernel(WgradArgs a) {
     const int ch = tid >> 3, sub = 2 * (tid & 7);
     float v = 0.f;
     for (int row = 0; row < mc; ++row)
-      v += __uint_as_float((uint32_t)(*reinterpret_cast<const uint16_t*>(iy + wr_img(row, ch) + sub)) << 16);
+      v += hlo((uint32_t)(*reinterpret_cast<const uint16_t*>(iy + wr_img(row, ch) + sub)));
     a.partb[(int64_t)s * a.N + n0 + tid] = v;
   }
 }
@@ -205,8 +202,8 @@ extern "C" int rdx_wgrad_acc(const void* dy, int64_t ldy, const void* x, int64_t
     attr = true;
   }
   WgradArgs a;
-  a.dy = (const __hip_bfloat16*)dy;
-  a.x = (const __hip_bfloat16*)x;
+  a.dy = (const hst*)dy;
+  a.x = (const hst*)x;
   a.ldy = ldy;
   a.ldx = ldx;
   a.part = ws;

@@ -1,7 +1,9 @@
-"""ctypes binding of libradhip.so (C ABI declared in include/radhip.h).
+"""ctypes binding of libradhip.so and libradhip_f16.so (C ABI declared in include/radhip.h).
 
-The library is built in-tree (csrc/Makefile -> radhip/libradhip.so). There is no CPU fallback:
-if the library is missing or a call fails, a RuntimeError is raised.
+Both are built in-tree from the same sources (csrc/Makefile -> radhip/libradhip.so with bf16 16-bit storage,
+radhip/libradhip_f16.so with fp16 storage, -DRDX_F16) and export the same entry points; radhip.ops picks the
+one matching a tensor's 16-bit dtype. There is no CPU fallback: if a library is missing or a call fails, a
+RuntimeError is raised.
 """
 import ctypes
 import os
@@ -9,6 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RADHIP_LIB", os.path.join(_HERE, "libradhip.so"))
+LIB16_PATH = os.environ.get("RADHIP_LIB16", os.path.join(_HERE, "libradhip_f16.so"))
 
 RDX_F32 = 0
 RDX_BF16 = 1
@@ -179,6 +182,7 @@ SIGNATURES = {
 
 _lock = threading.Lock()
 _lib = None
+_lib16 = None
 
 
 def header_symbols():
@@ -189,24 +193,41 @@ def header_symbols():
     return sorted(set(re.findall(r"^\s*(?:const char\*|int64_t|int)\s+(rdx_\w+)\s*\(", text, re.M)))
 
 
+def _load(path, mode):
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{os.path.basename(path)} not found at {path}: build it with `make -C csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback for the HIP path")
+    L = ctypes.CDLL(path, mode=mode)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib():
-    """Load libradhip.so once; raise loudly if it is absent."""
+    """Load libradhip.so (bf16 storage) once; raise loudly if it is absent."""
     global _lib
     if _lib is not None:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise RuntimeError(
-                    f"libradhip.so not found at {LIB_PATH}: build it with `make -C csrc` "
-                    "(or __graft_entry__.build()); there is no CPU fallback for the HIP path")
-            L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-            for name, (res, args) in SIGNATURES.items():
-                fn = getattr(L, name)
-                fn.restype = res
-                fn.argtypes = args
-            _lib = L
+            _lib = _load(LIB_PATH, ctypes.RTLD_GLOBAL)
     return _lib
+
+
+def lib16():
+    """Load libradhip_f16.so (the same entry points over fp16 storage) once, with its symbols kept local (both
+    libraries are linked -Bsymbolic); raise loudly if it is absent."""
+    global _lib16
+    if _lib16 is not None:
+        return _lib16
+    lib()
+    with _lock:
+        if _lib16 is None:
+            _lib16 = _load(LIB16_PATH, ctypes.RTLD_LOCAL)
+    return _lib16
 
 
 def check(code, what=""):

@@ -94,7 +94,7 @@ class SideLinearFn(torch.autograd.Function):
         if side is not cur:
             side.wait_stream(cur)
         with torch.cuda.stream(side):
-            if (_WGRAD and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.stride(-1) == 1
+            if (_WGRAD and dy2.dtype in ops.HALF and x2.dtype == dy2.dtype and dy2.stride(-1) == 1
                     and x2.stride(-1) == 1 and weight.grad.is_contiguous()):
                 # one split-over-tokens MFMA pass + a fixed-order reduce into .grad (csrc/wgrad.hip): hipBLASLt
                 # ran these long-K, tiny-output GEMMs on 5-27 workgroups
@@ -104,7 +104,7 @@ class SideLinearFn(torch.autograd.Function):
             else:
                 torch.ops.aten.addmm.dtype_out(weight.grad, dy2.t(), x2, torch.float32, beta=1, alpha=1,
                                                out=weight.grad)
-            if need_b and not (_WGRAD and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            if need_b and not (_WGRAD and dy2.dtype in ops.HALF and x2.dtype == dy2.dtype
                                and dy2.stride(-1) == 1 and x2.stride(-1) == 1 and weight.grad.is_contiguous()):
                 bias.grad.add_(dy2.sum(0, dtype=torch.float32))
         if side is cur:
@@ -117,7 +117,7 @@ class SideLinearFn(torch.autograd.Function):
         return dx, None, None, None
 
 
-_WGRAD = os.environ.get("RADHIP_WGRAD", "1") != "0"     # csrc/wgrad.hip for the bf16 weight gradients
+_WGRAD = os.environ.get("RADHIP_WGRAD", "1") != "0"     # csrc/wgrad.hip for the 16-bit weight gradients
 _MODE = os.environ.get("RADHIP_SIDE_LINEAR", "2")   # "2": main stream; "1": side stream; "0": F.linear
 _ON = _MODE != "0"
 
@@ -153,7 +153,7 @@ class RowLNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, eps, out_dtype):
-        from ._lib import check, lib
+        from ._lib import check
         C = x.shape[-1]
         xc = x.contiguous()
         M = xc.numel() // C
@@ -161,7 +161,7 @@ class RowLNFn(torch.autograd.Function):
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         w, b = weight.detach().float().contiguous(), bias.detach().float().contiguous()
-        check(lib().rdx_row_ln_fwd(ops._dtype_code(xc), ops._p(xc), ops._p(w), ops._p(b), float(eps),
+        check(ops._L(xc, y).rdx_row_ln_fwd(ops._dtype_code(xc), ops._p(xc), ops._p(w), ops._p(b), float(eps),
                                    ops._dtype_code(y), ops._p(y), ops._p(mean), ops._p(rstd), M, C, ops._stream(xc)),
               "row_ln_fwd")
         ctx.save_for_backward(xc, mean, rstd, w)
@@ -170,13 +170,14 @@ class RowLNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from ._lib import check, lib
+        from ._lib import check
         xc, mean, rstd, w = ctx.saved_tensors
         weight, bias = ctx.params
         C = xc.shape[-1]
         M = xc.numel() // C
         dy = dy.contiguous()
-        if dy.dtype not in (torch.float32, torch.bfloat16):
+        if dy.dtype not in (torch.float32, *ops.HALF) or (xc.dtype in ops.HALF
+                                                           and dy.dtype not in (torch.float32, xc.dtype)):
             dy = dy.float()
         dx = torch.empty_like(xc)
         direct = all(p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
@@ -185,7 +186,7 @@ class RowLNFn(torch.autograd.Function):
             dgw, dgb = weight.grad, bias.grad
         else:
             dgw, dgb = torch.zeros(C, device=xc.device), torch.zeros(C, device=xc.device)
-        check(lib().rdx_row_ln_bwd(ops._dtype_code(dy), ops._p(dy), ops._dtype_code(xc), ops._p(xc), ops._p(mean),
+        check(ops._L(dy, xc).rdx_row_ln_bwd(ops._dtype_code(dy), ops._p(dy), ops._dtype_code(xc), ops._p(xc), ops._p(mean),
                                    ops._p(rstd), ops._p(w), ops._p(dx), ops._p(dgw), ops._p(dgb), M, C,
                                    ops._stream(xc)), "row_ln_bwd")
         if direct:
@@ -197,8 +198,8 @@ class RowLayerNorm(nn.LayerNorm):
     """nn.LayerNorm (same parameters and state_dict keys) on csrc/rowln.hip for C <= 1024 on the GPU: one kernel
     each way instead of torch's layer_norm forward, its three backward kernels and the casts around them. Its
     gamma / beta gradients are accumulated in fp32 straight into .grad (like SideLinear). `to_linear`: the only
-    consumers are linears, so under bf16 autocast the output is written in bf16 — the value the linear's input
-    cast would produce from torch's fp32 output."""
+    consumers are linears, so under bf16 / fp16 autocast the output is written in that dtype — the value the
+    linear's input cast would produce from torch's fp32 output."""
 
     def __init__(self, *args, to_linear=False, **kw):
         super().__init__(*args, **kw)
@@ -210,12 +211,15 @@ class RowLayerNorm(nn.LayerNorm):
 
     def forward(self, x):
         if not (_ROWLN and x.is_cuda and len(self.normalized_shape) == 1 and x.shape[-1] <= 1024 and self.elementwise_affine
-                and self.bias is not None and x.dtype in (torch.float32, torch.bfloat16)):
+                and self.bias is not None and x.dtype in (torch.float32, *ops.HALF)):
             return super().forward(x)
         ac = torch.is_autocast_enabled("cuda")
         if ac:
-            out = torch.bfloat16 if (self.to_linear and torch.get_autocast_dtype("cuda") == torch.bfloat16) else torch.float32
+            adt = torch.get_autocast_dtype("cuda")
+            out = adt if (self.to_linear and adt in ops.HALF) else torch.float32
         else:
             out = x.dtype
+        if x.dtype in ops.HALF and out in ops.HALF and out != x.dtype:
+            return super().forward(x)
         with torch.autocast("cuda", enabled=False):
             return RowLNFn.apply(x, self.weight, self.bias, self.eps, out)

@@ -11,7 +11,31 @@ import torch
 from . import _lib
 from ._lib import check, lib, ptr_array
 
-_DT = {torch.float32: _lib.RDX_F32, torch.bfloat16: _lib.RDX_BF16}
+# 16-bit storage: bf16 on libradhip.so, fp16 on libradhip_f16.so (the same kernels built with -DRDX_F16,
+# csrc/common.h); the dtype code 1 (RDX_BF16) names the library's 16-bit storage type in both
+HALF = (torch.bfloat16, torch.float16)
+_DT = {torch.float32: _lib.RDX_F32, torch.bfloat16: _lib.RDX_BF16, torch.float16: _lib.RDX_BF16}
+
+
+def _L(*xs):
+    """The library whose 16-bit storage type is that of the tensors / dtypes xs: libradhip_f16.so for fp16,
+    libradhip.so otherwise (one call never mixes bf16 and fp16)."""
+    dts = {x if isinstance(x, torch.dtype) else x.dtype for x in xs}
+    if torch.float16 in dts:
+        if torch.bfloat16 in dts:
+            raise TypeError("radhip: one launch cannot mix bf16 and fp16 tensors")
+        return _lib.lib16()
+    return lib()
+
+
+def half_dtype():
+    """The 16-bit storage dtype of a fused op's forward: the CUDA autocast dtype (bf16 or fp16) when autocast
+    is on, else bf16. Backward passes take it from their saved tensors."""
+    if torch.is_autocast_enabled("cuda"):
+        d = torch.get_autocast_dtype("cuda")
+        if d in HALF:
+            return d
+    return torch.bfloat16
 
 # Optional live timing: when TIMING is a dict, every C-ABI launch below is bracketed by two HIP events
 # recorded on the stream it is launched on; TIMING[name] collects (start, end, work) tuples, where
@@ -135,7 +159,7 @@ def _dtype_code(t):
     try:
         return _DT[t.dtype]
     except KeyError:
-        raise TypeError(f"radhip: unsupported dtype {t.dtype} (float32 / bfloat16 only)")
+        raise TypeError(f"radhip: unsupported dtype {t.dtype} (float32 / bfloat16 / float16 only)")
 
 
 def _require_gpu(*ts):
@@ -234,7 +258,7 @@ class DWConvBidir(torch.autograd.Function):
         b = bias.contiguous().float()
         K = w.shape[1]
         u = torch.empty(dirs, B, L, D, device=x.device, dtype=x.dtype)
-        check(lib().rdx_dwconv_bidir_fwd(_dtype_code(x), _p(x), ldx, _p(w), _p(b), _p(u), B, L, D, K, dirs,
+        check(_L(x).rdx_dwconv_bidir_fwd(_dtype_code(x), _p(x), ldx, _p(w), _p(b), _p(u), B, L, D, K, dirs,
                                          _stream(x)), "dwconv_bidir_fwd")
         ctx.save_for_backward(x, w, b)
         ctx.dirs = dirs
@@ -251,7 +275,7 @@ class DWConvBidir(torch.autograd.Function):
         parts = lib().rdx_dwconv_bidir_bwd_parts(L) * B
         dw_part = torch.empty(parts, D, K, device=x.device, dtype=torch.float32)
         db_part = torch.empty(parts, D, device=x.device, dtype=torch.float32)
-        check(lib().rdx_dwconv_bidir_bwd(_dtype_code(x), _p(x), _rowview_ld(x), _p(w), _p(b), _p(du), _p(dx), D,
+        check(_L(x).rdx_dwconv_bidir_bwd(_dtype_code(x), _p(x), _rowview_ld(x), _p(w), _p(b), _p(du), _p(dx), D,
                                          _p(dw_part), _p(db_part), B, L, D, K, ctx.dirs, _stream(x)),
               "dwconv_bidir_bwd")
         return dx, dw_part.sum(0).view(ctx.wshape), db_part.sum(0), None
@@ -291,13 +315,13 @@ class SelectiveScan(torch.autograd.Function):
             P = torch.empty(nrec, device=u.device, dtype=torch.float32)
             hloc = torch.empty(nrec, device=u.device, dtype=torch.float32)
             with _timed("selective_scan_fwd", u, dirs * B * L * (D * (2 * es + 4) + 2 * N * es)):
-                check(lib().rdx_scan2_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc, _p(Dp),
+                check(_L(u).rdx_scan2_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ldbc, _p(Dp),
                                           _p(dt_bias), _p(y), _p(ck), _p(P), _p(hloc), B, L, D, N, dirs, _stream(u)),
                       "scan2_fwd")
         else:
             P = torch.empty(0, device=u.device, dtype=torch.float32)
             with _timed("selective_scan_fwd", u, dirs * B * L * (D * (2 * es + 4) + 2 * N * es)):
-                check(lib().rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
+                check(_L(u).rdx_selective_scan_fwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
                                                    ldbc, _p(Dp), _p(dt_bias), _p(y), _p(ck), B, L, D, N, dirs,
                                                    _stream(u)), "selective_scan_fwd")
         ctx.save_for_backward(u, delta, A_log, Bm, Cm, Dp, dt_bias, ck, P)
@@ -327,13 +351,13 @@ class SelectiveScan(torch.autograd.Function):
         if ctx.chunked:
             gloc = torch.empty(int(lib().rdx_scan2_rec_elems(B, L, D, N, dirs)), device=u.device, dtype=torch.float32)
             with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
-                check(lib().rdx_scan2_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ctx.ldbc,
+                check(_L(u).rdx_scan2_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ctx.ldbc,
                                           _p(Dp), _p(dt_bias), _p(ck), _p(P), _p(dy), dy_stride, _p(du), _p(ddelta),
                                           _p(dBC), _p(dA), _p(dD), _p(dbias), _p(gloc), B, L, D, N, dirs, _stream(u)),
                       "scan2_bwd")
         else:
             with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
-                check(lib().rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
+                check(_L(u).rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
                                                    ctx.ldbc, _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du),
                                                    _p(ddelta), _p(dBC), _p(dA), _p(dD), _p(dbias), B, L, D, N, dirs,
                                                    _stream(u)), "selective_scan_bwd")
@@ -352,7 +376,7 @@ class BiGate(torch.autograd.Function):
         ldz = _rowview_ld(z)
         g = torch.empty(B, L, D, device=z.device, dtype=z.dtype)
         ysum = torch.empty(B, L, D, device=z.device, dtype=torch.float32)
-        check(lib().rdx_bigate_fwd(_dtype_code(z), _p(y), dirs, _p(z), ldz, _p(g), _p(ysum), B, L, D, _stream(z)),
+        check(_L(z).rdx_bigate_fwd(_dtype_code(z), _p(y), dirs, _p(z), ldz, _p(g), _p(ysum), B, L, D, _stream(z)),
               "bigate_fwd")
         ctx.save_for_backward(z, ysum)
         ctx.dirs = dirs
@@ -365,7 +389,7 @@ class BiGate(torch.autograd.Function):
         dg = dg.contiguous().to(z.dtype)
         dy = torch.empty(B, L, D, device=z.device, dtype=torch.float32)
         dz = torch.empty(B, L, D, device=z.device, dtype=z.dtype)
-        check(lib().rdx_bigate_bwd(_dtype_code(z), _p(dg), _p(z), _rowview_ld(z), _p(ysum), _p(dy), _p(dz), D, B, L,
+        check(_L(z).rdx_bigate_bwd(_dtype_code(z), _p(dg), _p(z), _rowview_ld(z), _p(ysum), _p(dy), _p(dz), D, B, L,
                                    D, _stream(z)), "bigate_bwd")
         return dy.unsqueeze(0).expand(ctx.dirs, B, L, D), dz
 
@@ -388,7 +412,7 @@ class LayerWeightedSum(torch.autograd.Function):
         wf = w.detach().contiguous().float()
         out = torch.empty_like(hs[0])
         with _timed("layer_wsum_fwd", out, (len(hs) + 1) * out.numel() * out.element_size()):
-            check(lib().rdx_layer_wsum_fwd(_dtype_code(h0), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
+            check(_L(h0).rdx_layer_wsum_fwd(_dtype_code(h0), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
                                            _p(out), out.numel(), _stream(out)), "layer_wsum_fwd")
         ctx.save_for_backward(wf, *hs)
         ctx.deferred = deferred
@@ -406,7 +430,7 @@ class LayerWeightedSum(torch.autograd.Function):
         dots = torch.empty(nblk, len(hs), device=g.device, dtype=torch.float32)
         nwrite = sum(d is not None for d in dhs)
         with _timed("layer_wsum_bwd", g, (len(hs) + nwrite + 1) * n * g.element_size()):
-            check(lib().rdx_layer_wsum_bwd(_dtype_code(g), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
+            check(_L(g).rdx_layer_wsum_bwd(_dtype_code(g), len(hs), ptr_array([h.data_ptr() for h in hs]), _p(wf),
                                            _p(g), ptr_array([d.data_ptr() if d is not None else 0 for d in dhs]),
                                            _p(dots), n, _stream(g)), "layer_wsum_bwd")
         dots = dots.sum(0)
@@ -449,8 +473,8 @@ class MixupFocal(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, ya, yb, lam, rows_per_lam, alpha, gamma, mode, scale):
         _require_gpu(logits, ya)
-        if logits.dim() != 2 or logits.dtype not in (torch.bfloat16, torch.float32) or logits.stride(1) != 1:
-            raise ValueError("mixup focal: [B, C] bf16/fp32 logits with unit column stride required")
+        if logits.dim() != 2 or logits.dtype not in (*HALF, torch.float32) or logits.stride(1) != 1:
+            raise ValueError("mixup focal: [B, C] bf16/fp16/fp32 logits with unit column stride required")
         B, C = logits.shape
         ya = ya.contiguous()
         yb = yb.contiguous() if yb is not None else None
@@ -461,7 +485,7 @@ class MixupFocal(torch.autograd.Function):
             raise ValueError("mixup focal: lam has too few entries for the rows")
         loss = torch.empty((), device=logits.device, dtype=torch.float32)
         d32 = torch.empty(B, C, device=logits.device, dtype=torch.float32)
-        check(lib().rdx_focal_mixup_fwd(_p(logits), int(logits.dtype == torch.bfloat16), logits.stride(0), B, C, _p(ya),
+        check(_L(logits).rdx_focal_mixup_fwd(_p(logits), int(logits.dtype in HALF), logits.stride(0), B, C, _p(ya),
                                         _p(yb) if yb is not None else None, _p(lam) if lam is not None else None,
                                         int(rows_per_lam), float(alpha), float(gamma), int(mode), float(scale),
                                         _p(loss), _p(d32), _stream(logits)), "focal_mixup_fwd")
@@ -474,7 +498,7 @@ class MixupFocal(torch.autograd.Function):
         d32, = ctx.saved_tensors
         g = g.float().contiguous()
         out = torch.empty(d32.shape, device=d32.device, dtype=ctx.out_dtype)
-        check(lib().rdx_focal_mixup_bwd(_p(g), _p(d32), _p(out), int(ctx.out_dtype == torch.bfloat16), d32.numel(),
+        check(_L(ctx.out_dtype).rdx_focal_mixup_bwd(_p(g), _p(d32), _p(out), int(ctx.out_dtype in HALF), d32.numel(),
                                         _stream(d32)), "focal_mixup_bwd")
         return out, None, None, None, None, None, None, None, None
 
@@ -595,7 +619,7 @@ class BnSelu(torch.autograd.Function):
         N, C, H, W = c.shape
         f32 = [t.detach().contiguous().float() for t in (conv_bias, mean, invstd, weight, bias)]
         y = torch.empty_like(c)
-        check(lib().rdx_bnselu_fwd(_dtype_code(c), _p(c), *[_p(t) for t in f32], _p(y), N * H * W, C, _stream(c)),
+        check(_L(c).rdx_bnselu_fwd(_dtype_code(c), _p(c), *[_p(t) for t in f32], _p(y), N * H * W, C, _stream(c)),
               "bnselu_fwd")
         ctx.save_for_backward(c, *f32)
         return y
@@ -607,7 +631,7 @@ class BnSelu(torch.autograd.Function):
         dy = _nhwc(dy.to(c.dtype))
         dc = torch.empty_like(c)
         sums = torch.zeros(3, C, device=c.device, dtype=torch.float32)
-        check(lib().rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(dy), _p(cb), _p(mean), _p(invstd), _p(w), _p(b), _p(dc),
+        check(_L(c).rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(dy), _p(cb), _p(mean), _p(invstd), _p(w), _p(b), _p(dc),
                                    _p(sums), N * H * W, C, _stream(c)), "bnselu_bwd")
         return dc, sums[0], None, None, sums[1], sums[2]
 
@@ -626,7 +650,7 @@ class ResTail(torch.autograd.Function):
         y = torch.empty(N, C, H, W // 3, device=a.device, dtype=a.dtype, memory_format=torch.channels_last)
         arg = torch.empty(N, C, H, W // 3, device=a.device, dtype=torch.uint8, memory_format=torch.channels_last)
         bf = bias.detach().contiguous().float()
-        check(lib().rdx_res_tail_fwd(_dtype_code(a), _p(a), _p(identity), _p(bf), _p(y), _p(arg), N * H, W, C,
+        check(_L(a).rdx_res_tail_fwd(_dtype_code(a), _p(a), _p(identity), _p(bf), _p(y), _p(arg), N * H, W, C,
                                      _stream(a)), "res_tail_fwd")
         ctx.save_for_backward(arg)
         ctx.shape, ctx.dtype = (N, C, H, W), a.dtype
@@ -639,7 +663,7 @@ class ResTail(torch.autograd.Function):
         dy = _nhwc(dy.to(ctx.dtype))
         dx = torch.empty(N, C, H, W, device=dy.device, dtype=ctx.dtype, memory_format=torch.channels_last)
         dbias = torch.zeros(C, device=dy.device, dtype=torch.float32)
-        check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(dx), _p(dbias), N * H, W, C, _stream(dy)),
+        check(_L(dy).rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(dx), _p(dbias), N * H, W, C, _stream(dy)),
               "res_tail_bwd")
         return dx, dx, dbias
 
@@ -654,8 +678,9 @@ class Block0Convs(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, wd):
         _require_gpu(x)
-        xb = x.to(torch.bfloat16)
-        w1b, wdb = w1.to(torch.bfloat16), wd.to(torch.bfloat16)
+        hd = half_dtype()
+        xb = x.to(hd)
+        w1b, wdb = w1.to(hd), wd.to(hd)
         c = torch.nn.functional.conv2d(xb, w1b, None, 1, (1, 1))
         idn = torch.nn.functional.conv2d(xb, wdb, None, 1, (0, 1))
         ctx.save_for_backward(xb, w1b, wdb)
@@ -668,15 +693,15 @@ class Block0Convs(torch.autograd.Function):
         w1_shape, wd_shape, x_dtype = ctx.meta
         N, _, H, W = xb.shape
         C = w1_shape[0]
-        dc = _nhwc(dc.to(torch.bfloat16))
-        di = _nhwc(di.to(torch.bfloat16))
+        dc = _nhwc(dc.to(xb.dtype))
+        di = _nhwc(di.to(xb.dtype))
         xc = xb.contiguous(memory_format=torch.channels_last)      # one channel: [N, H, W] in memory
-        w1f = w1b.float().contiguous()                               # the bf16 weights the forward used
+        w1f = w1b.float().contiguous()                               # the 16-bit weights the forward used
         wdf = wdb.float().contiguous()
         dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
         part = torch.empty(lib().rdx_sincnet_b0_nblk(N * H * W), C * 9, device=xb.device, dtype=torch.float32)
         with _timed("sincnet_b0_bwd", dc, 2 * (dc.numel() + di.numel()) + 4 * dx.numel() + 2 * xc.numel()):
-            check(lib().rdx_sincnet_b0_bwd(_p(xc), _p(dc), _p(di), _p(w1f), _p(wdf), _p(dx), _p(part), N, H, W, C,
+            check(_L(xb).rdx_sincnet_b0_bwd(_p(xc), _p(dc), _p(di), _p(w1f), _p(wdf), _p(dx), _p(part), N, H, W, C,
                                            _stream(dc)), "sincnet_b0_bwd")
         dw = part.sum(0).view(C, 9)
         return dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape)
@@ -704,42 +729,43 @@ def sconv_ok(x, weight):
 SCONV_WCACHE = None
 
 
-def _sconv_w(weight):
+def _sconv_w(weight, hd):
     if SCONV_WCACHE is not None:
-        hit = SCONV_WCACHE.get(id(weight))
+        hit = SCONV_WCACHE.get((id(weight), hd))
         if hit is not None and hit[0] is weight:
             return hit[1], hit[2]
-    wf, wd = _sconv_w_prep(weight)
+    wf, wd = _sconv_w_prep(weight, hd)
     if SCONV_WCACHE is not None:
-        SCONV_WCACHE[id(weight)] = (weight, wf, wd)
+        SCONV_WCACHE[(id(weight), hd)] = (weight, wf, wd)
     return wf, wd
 
 
-def _sconv_w_prep(weight):
-    """[C_out, C_in, KH, 3] -> tap-major [KH*3][C_out][C_in] bf16 (forward) and the flipped, transposed
-    [KH*3][C_in][C_out] bf16 (input gradient = the same convolution of dY)."""
+def _sconv_w_prep(weight, hd):
+    """[C_out, C_in, KH, 3] -> tap-major [KH*3][C_out][C_in] in the 16-bit dtype hd (forward) and the flipped,
+    transposed [KH*3][C_in][C_out] (input gradient = the same convolution of dY)."""
     co, ci, kh, kw = weight.shape
-    wb = weight.detach().to(torch.bfloat16)
+    wb = weight.detach().to(hd)
     wf = wb.permute(2, 3, 0, 1).reshape(kh * kw, co, ci).contiguous()
     wd = wb.flip(2, 3).permute(2, 3, 1, 0).reshape(kh * kw, ci, co).contiguous()
     return wf, wd
 
 
 def _sconv_run(x, w_tap, ci, co, kh, ph, y2=None, bn=None, res=None):
-    """res: a bf16 [N, co, Ho, W] channels_last tensor added in the epilogue (y = bf16(bf16(conv) + res))."""
+    """x: 16-bit NHWC (bf16 or fp16: the output's dtype and the library); res: an [N, co, Ho, W] channels_last
+    tensor of x's dtype added in the epilogue (y = r(r(conv) + res), r = rounding to that dtype)."""
     N, _, H, W = x.shape
     Ho = H + 2 * ph - kh + 1
-    y = torch.empty(N, co, Ho, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+    y = torch.empty(N, co, Ho, W, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
     # algorithmic HBM bytes (the convolution is HBM-bound: ~100 FLOP per byte at these channel counts)
     nbytes = 2.0 * (N * H * W * ci + N * Ho * W * co * (2 if (y2 is not None or res is not None) else 1))
     with _timed("sconv_fwd", x, nbytes, shape=(N, H, W, ci, co, kh, ph)):
         if res is not None:
-            if res.shape != y.shape or res.dtype != torch.bfloat16 or not res.is_contiguous(memory_format=torch.channels_last):
-                raise ValueError("radhip sconv: residual must be bf16 NHWC of the output's shape")
-            check(lib().rdx_sconv_fwd_res(_p(x), _p(w_tap), _p(y), _p(res), N, H, W, ci, co, kh, ph, _stream(x)),
+            if res.shape != y.shape or res.dtype != y.dtype or not res.is_contiguous(memory_format=torch.channels_last):
+                raise ValueError("radhip sconv: residual must be NHWC of the output's shape and dtype")
+            check(_L(x).rdx_sconv_fwd_res(_p(x), _p(w_tap), _p(y), _p(res), N, H, W, ci, co, kh, ph, _stream(x)),
                   "sconv_fwd_res")
         else:
-            check(lib().rdx_sconv_fwd(_p(x), _p(w_tap), _p(y), _p(y2) if y2 is not None else None,
+            check(_L(x).rdx_sconv_fwd(_p(x), _p(w_tap), _p(y), _p(y2) if y2 is not None else None,
                                       _p(bn) if bn is not None else None, N, H, W, ci, co, kh, ph, _stream(x)),
                   "sconv_fwd")
     return y
@@ -754,7 +780,7 @@ def _sconv_backward(x, dy, wd, weight_shape, ph, need_dx):
     part = torch.empty(nblk, kh * 3 * co * ci, device=x.device, dtype=torch.float32)
     dw = torch.empty(kh * 3, co, ci, device=x.device, dtype=torch.float32)
     with _timed("sconv_wgrad", x, 2.0 * (N * H * W * ci + N * Ho * W * co), shape=(N, H, W, ci, co, kh, ph)):
-        check(lib().rdx_sconv_wgrad(_p(x), _p(dy), _p(dw), _p(part), N, H, W, ci, co, kh, ph, _stream(x)), "sconv_wgrad")
+        check(_L(x).rdx_sconv_wgrad(_p(x), _p(dy), _p(dw), _p(part), N, H, W, ci, co, kh, ph, _stream(x)), "sconv_wgrad")
     return dx, dw.view(kh, 3, co, ci).permute(2, 3, 0, 1)
 
 
@@ -766,9 +792,9 @@ class SConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, ph):
         _require_gpu(x)
-        x = _nhwc(x.to(torch.bfloat16))
+        x = _nhwc(x.to(half_dtype()))
         co, ci, kh, _ = weight.shape
-        wf, wd = _sconv_w(weight)
+        wf, wd = _sconv_w(weight, x.dtype)
         ctx.save_for_backward(x, wd)
         ctx.meta = (tuple(weight.shape), ph, weight.dtype)
         return _sconv_run(x, wf, ci, co, kh, ph)
@@ -777,7 +803,7 @@ class SConv(torch.autograd.Function):
     def backward(ctx, dy):
         x, wd = ctx.saved_tensors
         shape, ph, wdt = ctx.meta
-        dy = _nhwc(dy.to(torch.bfloat16))
+        dy = _nhwc(dy.to(x.dtype))
         dx, dw = _sconv_backward(x, dy, wd, shape, ph, ctx.needs_input_grad[0])
         return dx, dw.to(wdt), None
 
@@ -790,13 +816,13 @@ class SConvBnSelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, ph, conv_bias, mean, invstd, gamma, beta):
         _require_gpu(x)
-        x = _nhwc(x.to(torch.bfloat16))
+        x = _nhwc(x.to(half_dtype()))
         co, ci, kh, _ = weight.shape
-        wf, wd = _sconv_w(weight)
+        wf, wd = _sconv_w(weight, x.dtype)
         f32 = [t.detach().contiguous().float() for t in (conv_bias, mean, invstd, gamma, beta)]
         bn = torch.stack([f32[0], f32[1], f32[2] * f32[3], f32[4]]).contiguous()
         N, _, H, W = x.shape
-        y = torch.empty(N, co, H + 2 * ph - kh + 1, W, device=x.device, dtype=torch.bfloat16,
+        y = torch.empty(N, co, H + 2 * ph - kh + 1, W, device=x.device, dtype=x.dtype,
                         memory_format=torch.channels_last)
         c = _sconv_run(x, wf, ci, co, kh, ph, y2=y, bn=bn)
         ctx.save_for_backward(x, wd, c, *f32)
@@ -808,10 +834,10 @@ class SConvBnSelu(torch.autograd.Function):
         x, wd, c, cb, mean, invstd, w, b = ctx.saved_tensors
         shape, ph, wdt = ctx.meta
         N, C, H, W = c.shape
-        dy = _nhwc(dy.to(torch.bfloat16))
+        dy = _nhwc(dy.to(c.dtype))
         dc = torch.empty_like(c)
         sums = torch.zeros(3, C, device=c.device, dtype=torch.float32)
-        check(lib().rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(dy), _p(cb), _p(mean), _p(invstd), _p(w), _p(b), _p(dc),
+        check(_L(c).rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(dy), _p(cb), _p(mean), _p(invstd), _p(w), _p(b), _p(dc),
                                    _p(sums), N * H * W, C, _stream(c)), "bnselu_bwd")
         dx, dw = _sconv_backward(x, dc, wd, shape, ph, ctx.needs_input_grad[0])
         return dx, dw.to(wdt), None, sums[0], None, None, sums[1], sums[2]
@@ -830,12 +856,12 @@ def _conv2_grad_to_c(da, out1, c, wd2, w2_shape, bn5, f32):
         H = da.shape[2]
         nbytes = 2.0 * (N * H * W * co2 + 2 * N * Ho * W * C)
         with _timed("sconv_dgrad_bnselu", da, nbytes, shape=(N, H, W)):
-            check(lib().rdx_sconv_dgrad_bnselu(_p(da), _p(wd2), _p(c), _p(dc), _p(bn5), _p(sums), N, H, W, co2, ci2,
+            check(_L(da).rdx_sconv_dgrad_bnselu(_p(da), _p(wd2), _p(c), _p(dc), _p(bn5), _p(sums), N, H, W, co2, ci2,
                                                kh2, kh2 - 1, _stream(da)), "sconv_dgrad_bnselu")
     else:
         do1 = _sconv_run(da, wd2, co2, ci2, kh2, kh2 - 1)
         cb, mean, invstd, w, b = f32
-        check(lib().rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(do1), _p(cb), _p(mean), _p(invstd), _p(w), _p(b),
+        check(_L(c).rdx_bnselu_bwd(_dtype_code(c), _p(c), _p(do1), _p(cb), _p(mean), _p(invstd), _p(w), _p(b),
                                    _p(dc), _p(sums), N * Ho * W, C, _stream(c)), "bnselu_bwd")
     _, dw2 = _sconv_backward(out1, da, wd2, w2_shape, 0, False)
     return dc, sums, dw2
@@ -855,13 +881,13 @@ class SConvBnSeluSConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, ph1, conv_bias, mean, invstd, gamma, beta, w2):
         _require_gpu(x)
-        x = _nhwc(x.to(torch.bfloat16))
+        x = _nhwc(x.to(half_dtype()))
         co, ci, kh, _ = w1.shape
-        wf1, wd1 = _sconv_w(w1)
-        wf2, wd2 = _sconv_w(w2)
+        wf1, wd1 = _sconv_w(w1, x.dtype)
+        wf2, wd2 = _sconv_w(w2, x.dtype)
         f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
         N, _, H, W = x.shape
-        out1 = torch.empty(N, co, H + 2 * ph1 - kh + 1, W, device=x.device, dtype=torch.bfloat16,
+        out1 = torch.empty(N, co, H + 2 * ph1 - kh + 1, W, device=x.device, dtype=x.dtype,
                            memory_format=torch.channels_last)
         c = _sconv_run(x, wf1, ci, co, kh, ph1, y2=out1, bn=bn5[:4])
         co2, ci2, kh2, _ = w2.shape
@@ -874,7 +900,7 @@ class SConvBnSeluSConv(torch.autograd.Function):
     def backward(ctx, da):
         x, wd1, c, out1, wd2, bn5, *f32 = ctx.saved_tensors
         s1, ph1, w1dt, s2, w2dt = ctx.meta
-        da = _nhwc(da.to(torch.bfloat16))
+        da = _nhwc(da.to(x.dtype))
         dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
         dx, dw1 = _sconv_backward(x, dc, wd1, s1, ph1, ctx.needs_input_grad[0])
         return dx, dw1.to(w1dt), None, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt)
@@ -892,22 +918,22 @@ class ResBlockIdentity(torch.autograd.Function):
     def forward(ctx, x, w1, conv_bias, mean, invstd, gamma, beta, w2, b2):
         _require_gpu(x)
         x_dtype = x.dtype
-        x = _nhwc(x.to(torch.bfloat16))
+        x = _nhwc(x.to(half_dtype()))
         co, ci, kh, _ = w1.shape
-        wf1, wd1 = _sconv_w(w1)
-        wf2, wd2 = _sconv_w(w2)
+        wf1, wd1 = _sconv_w(w1, x.dtype)
+        wf2, wd2 = _sconv_w(w2, x.dtype)
         f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
         N, _, H, W = x.shape
-        out1 = torch.empty(N, co, H + 1, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        out1 = torch.empty(N, co, H + 1, W, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
         c = _sconv_run(x, wf1, ci, co, kh, 1, y2=out1, bn=bn5[:4])
         co2, ci2, kh2, _ = w2.shape
         a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
         if a.shape != x.shape:
             raise ValueError(f"radhip: residual shapes differ {tuple(a.shape)} vs {tuple(x.shape)}")
-        y = torch.empty(N, co2, H, W // 3, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        y = torch.empty(N, co2, H, W // 3, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
         arg = torch.empty(N, co2, H, W // 3, device=x.device, dtype=torch.uint8, memory_format=torch.channels_last)
         bf = b2.detach().contiguous().float()
-        check(lib().rdx_res_tail_fwd(_dtype_code(a), _p(a), _p(x), _p(bf), _p(y), _p(arg), N * H, W, co2, _stream(a)),
+        check(_L(a).rdx_res_tail_fwd(_dtype_code(a), _p(a), _p(x), _p(bf), _p(y), _p(arg), N * H, W, co2, _stream(a)),
               "res_tail_fwd")
         ctx.save_for_backward(x, wd1, c, out1, wd2, bn5, arg, *f32)
         ctx.meta = (tuple(w1.shape), w1.dtype, tuple(w2.shape), w2.dtype, x_dtype)
@@ -918,10 +944,10 @@ class ResBlockIdentity(torch.autograd.Function):
         x, wd1, c, out1, wd2, bn5, arg, *f32 = ctx.saved_tensors
         s1, w1dt, s2, w2dt, x_dtype = ctx.meta
         N, C, H, W = x.shape
-        dy = _nhwc(dy.to(torch.bfloat16))
-        ds = torch.empty(N, C, H, W, device=dy.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        dy = _nhwc(dy.to(x.dtype))
+        ds = torch.empty(N, C, H, W, device=dy.device, dtype=x.dtype, memory_format=torch.channels_last)
         dbias = torch.zeros(C, device=dy.device, dtype=torch.float32)
-        check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(ds), _p(dbias), N * H, W, C, _stream(dy)),
+        check(_L(dy).rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(ds), _p(dbias), N * H, W, C, _stream(dy)),
               "res_tail_bwd")
         dc, sums, dw2 = _conv2_grad_to_c(ds, out1, c, wd2, s2, bn5, f32)
         co, ci, kh, _ = s1
@@ -938,13 +964,13 @@ class BnSeluSConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, c, conv_bias, mean, invstd, gamma, beta, w2):
         _require_gpu(c)
-        c = _nhwc(c.to(torch.bfloat16))
+        c = _nhwc(c.to(half_dtype()))
         N, C, H, W = c.shape
         f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
         out1 = torch.empty_like(c)
-        check(lib().rdx_bnselu_fwd(_dtype_code(c), _p(c), *[_p(t) for t in f32], _p(out1), N * H * W, C, _stream(c)),
+        check(_L(c).rdx_bnselu_fwd(_dtype_code(c), _p(c), *[_p(t) for t in f32], _p(out1), N * H * W, C, _stream(c)),
               "bnselu_fwd")
-        wf2, wd2 = _sconv_w(w2)
+        wf2, wd2 = _sconv_w(w2, c.dtype)
         co2, ci2, kh2, _ = w2.shape
         a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
         ctx.save_for_backward(c, out1, wd2, bn5, *f32)
@@ -955,7 +981,7 @@ class BnSeluSConv(torch.autograd.Function):
     def backward(ctx, da):
         c, out1, wd2, bn5, *f32 = ctx.saved_tensors
         s2, w2dt = ctx.meta
-        da = _nhwc(da.to(torch.bfloat16))
+        da = _nhwc(da.to(c.dtype))
         dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
         return dc, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt)
 
@@ -970,19 +996,20 @@ class Block0Front(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, wd, conv_bias, mean, invstd, gamma, beta, w2):
         _require_gpu(x)
-        xb = x.to(torch.bfloat16).contiguous()                       # one channel: [N, H, W] in memory
+        hd = half_dtype()
+        xb = x.to(hd).contiguous()                                   # one channel: [N, H, W] in memory
         N, _, H, W = xb.shape
         C = w1.shape[0]
-        w1b = w1.detach().to(torch.bfloat16).float().reshape(C, 6).contiguous()   # autocast's bf16 weights
-        wdb = wd.detach().to(torch.bfloat16).float().reshape(C, 3).contiguous()
+        w1b = w1.detach().to(hd).float().reshape(C, 6).contiguous()   # autocast's 16-bit weights
+        wdb = wd.detach().to(hd).float().reshape(C, 3).contiguous()
         f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
-        c = torch.empty(N, C, H + 1, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        c = torch.empty(N, C, H + 1, W, device=x.device, dtype=hd, memory_format=torch.channels_last)
         out1 = torch.empty_like(c)
-        idn = torch.empty(N, C, H, W, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        idn = torch.empty(N, C, H, W, device=x.device, dtype=hd, memory_format=torch.channels_last)
         with _timed("sincnet_b0_fwd", x, 2.0 * (xb.numel() + 2 * c.numel() + idn.numel())):
-            check(lib().rdx_sincnet_b0_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(c), _p(out1), _p(idn), N, H, W, C,
+            check(_L(hd).rdx_sincnet_b0_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(c), _p(out1), _p(idn), N, H, W, C,
                                            _stream(x)), "sincnet_b0_fwd")
-        wf2, wd2 = _sconv_w(w2)
+        wf2, wd2 = _sconv_w(w2, hd)
         co2, ci2, kh2, _ = w2.shape
         a = _sconv_run(out1, wf2, ci2, co2, kh2, 0)
         ctx.save_for_backward(xb, w1b, wdb, c, out1, wd2, bn5, *f32)
@@ -995,15 +1022,14 @@ class Block0Front(torch.autograd.Function):
         w1_shape, wd_shape, x_dtype, s2, w2dt = ctx.meta
         N, H, W = xb.shape[0], xb.shape[2], xb.shape[3]
         C = w1_shape[0]
-        da = _nhwc(da.to(torch.bfloat16))
+        da = _nhwc(da.to(xb.dtype))
         dc, sums, dw2 = _conv2_grad_to_c(da, out1, c, wd2, s2, bn5, f32)
-        di = _nhwc(di.to(torch.bfloat16)) if di is not None else torch.zeros(N, C, H, W, device=xb.device,
-                                                                             dtype=torch.bfloat16,
-                                                                             memory_format=torch.channels_last)
+        di = _nhwc(di.to(xb.dtype)) if di is not None else torch.zeros(N, C, H, W, device=xb.device, dtype=xb.dtype,
+                                                                       memory_format=torch.channels_last)
         dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
         part = torch.empty(lib().rdx_sincnet_b0_nblk(N * H * W), C * 9, device=xb.device, dtype=torch.float32)
         with _timed("sincnet_b0_bwd", dc, 2 * (dc.numel() + di.numel()) + 4 * dx.numel() + 2 * xb.numel()):
-            check(lib().rdx_sincnet_b0_bwd(_p(xb), _p(dc), _p(di), _p(w1b), _p(wdb), _p(dx), _p(part), N, H, W, C,
+            check(_L(xb).rdx_sincnet_b0_bwd(_p(xb), _p(dc), _p(di), _p(w1b), _p(wdb), _p(dx), _p(part), N, H, W, C,
                                            _stream(dc)), "sincnet_b0_bwd")
         dw = part.sum(0).view(C, 9)
         return (dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape), sums[0], None, None, sums[1],
@@ -1021,19 +1047,20 @@ class Block0Fused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, wd, conv_bias, mean, invstd, gamma, beta, w2, b2, bd):
         _require_gpu(x)
-        xb = x.to(torch.bfloat16).contiguous()                       # one channel: [N, H, W] in memory
+        hd = half_dtype()
+        xb = x.to(hd).contiguous()                                   # one channel: [N, H, W] in memory
         N, _, H, W = xb.shape
         C = w1.shape[0]
-        w1b = w1.detach().to(torch.bfloat16).float().reshape(C, 6).contiguous()   # autocast's bf16 weights
-        wdb = wd.detach().to(torch.bfloat16).float().reshape(C, 3).contiguous()
+        w1b = w1.detach().to(hd).float().reshape(C, 6).contiguous()   # autocast's 16-bit weights
+        wdb = wd.detach().to(hd).float().reshape(C, 3).contiguous()
         f32, bn5 = _bn_rows(conv_bias, mean, invstd, gamma, beta)
-        wf2, wd2 = _sconv_w(w2)
+        wf2, wd2 = _sconv_w(w2, hd)
         bias = (b2.detach().float() + bd.detach().float()).contiguous()
-        y = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        y = torch.empty(N, C, H, W // 3, device=x.device, dtype=hd, memory_format=torch.channels_last)
         arg = torch.empty(N, C, H, W // 3, device=x.device, dtype=torch.uint8, memory_format=torch.channels_last)
         # MFMA work: conv2 (32 -> 32, 2 x 3) over N x H x W positions; HBM: x in, y + argmax out
         with _timed("b0x_fwd", x, 2.0 * N * H * W * 32 * 192):
-            check(lib().rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg), N, H, W,
+            check(_L(hd).rdx_b0x_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(wf2), _p(bias), _p(y), _p(arg), N, H, W,
                                     _stream(x)), "b0x_fwd")
         ctx.save_for_backward(xb, w1b, wdb, wd2, bn5, arg, *f32)
         ctx.meta = (tuple(w1.shape), tuple(wd.shape), x.dtype, tuple(w2.shape), w2.dtype)
@@ -1046,12 +1073,12 @@ class Block0Fused(torch.autograd.Function):
         N, H, W = xb.shape[0], xb.shape[2], xb.shape[3]
         C = w1_shape[0]
         if os.environ.get("RADHIP_B0X_BWD", "1") != "0":
-            dy = _nhwc(dy.to(torch.bfloat16))
+            dy = _nhwc(dy.to(xb.dtype))
             dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
             part = torch.empty(lib().rdx_b0x_bwd_nblk(N, W), 6560, device=xb.device, dtype=torch.float32)
             # MFMA work: conv2's input gradient and weight gradient (2 x the forward's conv2)
             with _timed("b0x_bwd", dy, 4.0 * N * H * W * 32 * 192):
-                check(lib().rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2), _p(dx), _p(part),
+                check(_L(xb).rdx_b0x_bwd(_p(xb), _p(dy), _p(arg), _p(w1b), _p(wdb), _p(bn5), _p(wd2), _p(dx), _p(part),
                                         N, H, W, _stream(dy)), "b0x_bwd")
             tot = part.sum(0)
             dw2 = tot[:6144].view(2, 3, C, C).permute(2, 3, 0, 1)
@@ -1060,21 +1087,21 @@ class Block0Fused(torch.autograd.Function):
             dbias = tot[6432:6464]
             sums = tot[6464:6560].view(3, C)
             return (dx.to(x_dtype), dw1, dwd, sums[0], None, None, sums[1], sums[2], dw2.to(w2dt), dbias, dbias)
-        c = torch.empty(N, C, H + 1, W, device=xb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        c = torch.empty(N, C, H + 1, W, device=xb.device, dtype=xb.dtype, memory_format=torch.channels_last)
         out1 = torch.empty_like(c)
-        idn = torch.empty(N, C, H, W, device=xb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
-        check(lib().rdx_sincnet_b0_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(c), _p(out1), _p(idn), N, H, W, C,
+        idn = torch.empty(N, C, H, W, device=xb.device, dtype=xb.dtype, memory_format=torch.channels_last)
+        check(_L(xb).rdx_sincnet_b0_fwd(_p(xb), _p(w1b), _p(wdb), _p(bn5), _p(c), _p(out1), _p(idn), N, H, W, C,
                                        _stream(xb)), "sincnet_b0_fwd")
-        dy = _nhwc(dy.to(torch.bfloat16))
-        ds = torch.empty(N, C, H, W, device=xb.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        dy = _nhwc(dy.to(xb.dtype))
+        ds = torch.empty(N, C, H, W, device=xb.device, dtype=xb.dtype, memory_format=torch.channels_last)
         dbias = torch.zeros(C, device=xb.device, dtype=torch.float32)
-        check(lib().rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(ds), _p(dbias), N * H, W, C, _stream(dy)),
+        check(_L(dy).rdx_res_tail_bwd(_dtype_code(dy), _p(dy), _p(arg), _p(ds), _p(dbias), N * H, W, C, _stream(dy)),
               "res_tail_bwd")
         dc, sums, dw2 = _conv2_grad_to_c(ds, out1, c, wd2, s2, bn5, f32)
         dx = torch.empty(N, 1, H, W, device=xb.device, dtype=torch.float32)
         part = torch.empty(lib().rdx_sincnet_b0_nblk(N * H * W), C * 9, device=xb.device, dtype=torch.float32)
         with _timed("sincnet_b0_bwd", dc, 2 * (dc.numel() + ds.numel()) + 4 * dx.numel() + 2 * xb.numel()):
-            check(lib().rdx_sincnet_b0_bwd(_p(xb), _p(dc), _p(ds), _p(w1b), _p(wdb), _p(dx), _p(part), N, H, W, C,
+            check(_L(xb).rdx_sincnet_b0_bwd(_p(xb), _p(dc), _p(ds), _p(w1b), _p(wdb), _p(dx), _p(part), N, H, W, C,
                                            _stream(dc)), "sincnet_b0_bwd")
         dw = part.sum(0).view(C, 9)
         return (dx.to(x_dtype), dw[:, :6].reshape(w1_shape), dw[:, 6:].reshape(wd_shape), sums[0], None, None, sums[1],
@@ -1082,13 +1109,13 @@ class Block0Fused(torch.autograd.Function):
 
 
 # ------------------------------------------------------------ WavLM positional convolution ----
-def posconv_weights(weight):
-    """Conv weight [1024, 64, 128] (weight_norm applied) -> the two bf16 operand layouts of csrc/posconv.hip:
+def posconv_weights(weight, hd=torch.bfloat16):
+    """Conv weight [1024, 64, 128] (weight_norm applied) -> the two 16-bit (hd) operand layouts of csrc/posconv.hip:
     wk [16][128][64 n][64 c] = W[g*64+n, c, k] (forward) and wkt [16][128][64 c][64 n] = W[g*64+n, c, 127-k]
     (input gradient)."""
     W = weight.detach().reshape(16, 64, 64, 128)                             # [g, n, c, k]
-    wk = W.permute(0, 3, 1, 2).contiguous().to(torch.bfloat16)
-    wkt = W.flip(-1).permute(0, 3, 2, 1).contiguous().to(torch.bfloat16)
+    wk = W.permute(0, 3, 1, 2).contiguous().to(hd)
+    wkt = W.flip(-1).permute(0, 3, 2, 1).contiguous().to(hd)
     return wk, wkt
 
 
@@ -1103,12 +1130,12 @@ class PosConv(torch.autograd.Function):
         B, T, E = h.shape
         if E != 1024:
             raise ValueError("radhip posconv: 1024 channels (16 groups of 64) required")
-        h = h.to(torch.bfloat16).contiguous()
+        h = h.to(wk.dtype).contiguous()
         bias = bias.detach().float().contiguous()
         y = torch.empty_like(h)
         u = torch.empty_like(h)
         with _timed("posconv_fwd", h, 2.0 * B * T * E * 64 * 128):
-            check(lib().rdx_posconv_fwd(_p(h), _p(wk), _p(bias), _p(y), _p(u), B, T, _stream(h)), "posconv_fwd")
+            check(_L(h).rdx_posconv_fwd(_p(h), _p(wk), _p(bias), _p(y), _p(u), B, T, _stream(h)), "posconv_fwd")
         ctx.save_for_backward(u, wkt)
         return y
 
@@ -1116,10 +1143,10 @@ class PosConv(torch.autograd.Function):
     def backward(ctx, dy):
         u, wkt = ctx.saved_tensors
         B, T, E = u.shape
-        dy = dy.to(torch.bfloat16).contiguous()
+        dy = dy.to(u.dtype).contiguous()
         dh = torch.empty_like(u)
         with _timed("posconv_bwd", dy, 2.0 * B * T * E * 64 * 128):
-            check(lib().rdx_posconv_bwd(_p(dy), _p(u), _p(wkt), _p(dh), B, T, _stream(dy)), "posconv_bwd")
+            check(_L(u).rdx_posconv_bwd(_p(dy), _p(u), _p(wkt), _p(dh), B, T, _stream(dy)), "posconv_bwd")
         return dh, None, None, None
 
 
@@ -1184,10 +1211,12 @@ def _attn_split_workspace(dev, n_floats, n_counters):
 
 
 def attn_bwd_launch(q, ldq, k, ldk, v, ldv, gate, rel, mask, seed, salt, p_drop, o, ldo, lse, do, lddo, D, dq, dk, dv,
-                    ldg, dgate, B, T, H, stream):
+                    ldg, dgate, B, T, H, stream, dtype=torch.bfloat16):
     """One gated-attention backward: the fused one-workgroup-per-(b, h) kernel when T <= 224 (dropout from
     the forward's keep mask), else the query-stationary dQ + key-stationary dK/dV kernel pair (dropout
-    re-hashed from the seed). rel: the [H, 2T - 1] relative-position bias table."""
+    re-hashed from the seed). rel: the [H, 2T - 1] relative-position bias table; dtype: the 16-bit storage of
+    q / k / v (the library)."""
+    L = _L(dtype)
     if fused_bwd_enabled(T):
         if p_drop > 0 and mask is None:
             raise RuntimeError("fused attention backward with dropout needs the forward's keep mask")
@@ -1196,16 +1225,16 @@ def attn_bwd_launch(q, ldq, k, ldk, v, ldv, gate, rel, mask, seed, salt, p_drop,
             # (fills the chip at B = 8, but measured 4.6 vs 4.2 ms of attention backward per step in the
             # bench: the combine's extra dQ traffic and the halved per-workgroup key reuse cost more)
             ws, cnt = _attn_split_workspace(gate.device, int(lib().rdx_attn_bwd_split_ws(B, H)), B * H)
-            return check(lib().rdx_attn_bwd_fused_split(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
+            return check(L.rdx_attn_bwd_fused_split(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
                                                         _p(mask) if mask is not None else None, p_drop, 0.125, o,
                                                         ldo, _p(lse), do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate),
                                                         _p(ws), ws.numel(), _p(cnt), cnt.numel(), B, T, H, 64,
                                                         stream), "attn_bwd_fused_split")
-        return check(lib().rdx_attn_bwd_fused(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
+        return check(L.rdx_attn_bwd_fused(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
                                               _p(mask) if mask is not None else None, p_drop, 0.125, o, ldo, _p(lse),
                                               do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate), B, T, H, 64, stream),
                      "attn_bwd_fused")
-    return check(lib().rdx_attn_bwd(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel), seed, salt, p_drop, 0.125, o, ldo,
+    return check(L.rdx_attn_bwd(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel), seed, salt, p_drop, 0.125, o, ldo,
                                     _p(lse), do, lddo, _p(D), dq, dk, dv, ldg, _p(dgate), B, T, H, 64, stream),
                  "attn_bwd")
 
@@ -1220,8 +1249,8 @@ class GatedAttention(torch.autograd.Function):
         _require_gpu(q, k, v, gate, pos_bias)
         B, T, E = q.shape
         H = gate.shape[2]
-        if E != H * 64 or q.dtype != torch.bfloat16 or k.dtype != q.dtype or v.dtype != q.dtype:
-            raise ValueError("radhip attention: bf16 q/k/v with 64-dim heads required")
+        if E != H * 64 or q.dtype not in HALF or k.dtype != q.dtype or v.dtype != q.dtype:
+            raise ValueError("radhip attention: bf16 / fp16 q/k/v with 64-dim heads required")
         if pos_bias.requires_grad:
             raise ValueError("radhip attention: the position bias must be frozen")
         gate = gate.contiguous().float()
@@ -1231,7 +1260,7 @@ class GatedAttention(torch.autograd.Function):
         sd = seed if seed is not None else torch.zeros(1, dtype=torch.int64, device=q.device)
         mask = attn_keep_mask(B, T, H, float(p_drop), q.device)
         with _timed("attn_fwd", q, 2.0 * 2 * B * H * T * T * 64):
-            check(lib().rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(rel),
+            check(_L(q).rdx_attn_fwd(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(gate), _p(rel),
                                      _p(sd), int(salt), float(p_drop), 0.125, _p(o), E, _p(lse),
                                      _p(mask) if mask is not None else None, B, T, H, 64, _stream(q)), "attn_fwd")
         ctx.mask = mask
@@ -1251,7 +1280,8 @@ class GatedAttention(torch.autograd.Function):
         dgate = torch.empty(B, T, H, device=q.device, dtype=torch.float32)
         with _timed("attn_bwd", q, 2.0 * 5 * B * H * T * T * 64):
             attn_bwd_launch(_p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), gate, rel, ctx.mask, _p(sd), ctx.salt,
-                            ctx.p, _p(o), E, lse, _p(do), E, D, _p(dq), _p(dk), _p(dv), E, dgate, B, T, H, _stream(q))
+                            ctx.p, _p(o), E, lse, _p(do), E, D, _p(dq), _p(dk), _p(dv), E, dgate, B, T, H, _stream(q),
+                            q.dtype)
         return dq, dk, dv, dgate, None, None, None, None
 
 
@@ -1277,7 +1307,7 @@ def dropout_mask(seed, salt, p_drop, shape):
     return keep.view(*shape)
 
 
-# --------------------------------------------------------------------------- bf16 GEMM --------
+# ------------------------------------------------------------------------ 16-bit GEMM --------
 def gemm_flops(M, N, K):
     return 2.0 * M * N * K
 
@@ -1285,21 +1315,21 @@ def gemm_flops(M, N, K):
 def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, seed=None, salt=0, p_drop=0.0,
          name="gemm"):
     """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on the hand-written MFMA kernel (csrc/gemm.hip):
-    bf16 row views a, b (unit inner stride); returns C (bf16, or fp32 for EPI_RESID_DROP)."""
+    16-bit (bf16 or fp16) row views a, b (unit inner stride); returns C (a's dtype, or fp32 for EPI_RESID_DROP)."""
     _require_gpu(a, b)
-    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
-        raise ValueError("radhip gemm: bf16 operands with unit inner stride required")
+    if a.dtype not in HALF or b.dtype != a.dtype or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip gemm: bf16 / fp16 operands of one dtype with unit inner stride required")
     M, K = a.shape
     N, K2 = b.shape
     if K != K2:
         raise ValueError(f"radhip gemm: K mismatch {K} vs {K2}")
     if out is None:
-        dt = torch.float32 if epilogue == _lib.EPI_RESID_DROP else torch.bfloat16
+        dt = torch.float32 if epilogue == _lib.EPI_RESID_DROP else a.dtype
         out = torch.empty(M, N, device=a.device, dtype=dt)
     if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
-        aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        aux_out = torch.empty(M, N, device=a.device, dtype=a.dtype)
     with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
-        check(lib().rdx_gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+        check(_L(a).rdx_gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
                                   _p(bias) if bias is not None else None, int(epilogue),
                                   _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
                                   _p(aux_out) if aux_out is not None else None,
@@ -1352,10 +1382,10 @@ def layer_gemm(pol, a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None):
 
 def wgrad_acc(dy, x, dw, db=None):
     """dw += dy^T x and db += dy.sum(0) in fp32 on csrc/wgrad.hip: dy [M, N], x [M, K] bf16 row views (unit inner
-    stride), dw fp32 [N, K] (row stride >= K, unit inner stride), db fp32 [N] or None."""
+    stride; bf16 or fp16, one dtype), dw fp32 [N, K] (row stride >= K, unit inner stride), db fp32 [N] or None."""
     _require_gpu(dy, x)
-    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or dy.stride(-1) != 1 or x.stride(-1) != 1:
-        raise ValueError("radhip wgrad_acc: bf16 operands with unit inner stride required")
+    if dy.dtype not in HALF or x.dtype != dy.dtype or dy.stride(-1) != 1 or x.stride(-1) != 1:
+        raise ValueError("radhip wgrad_acc: bf16 / fp16 operands of one dtype with unit inner stride required")
     M, N = dy.shape
     M2, K = x.shape
     if M != M2 or dw.shape != (N, K) or dw.dtype != torch.float32 or dw.stride(-1) != 1:
@@ -1364,7 +1394,7 @@ def wgrad_acc(dy, x, dw, db=None):
         raise ValueError("radhip wgrad_acc: db must be fp32 [N]")
     ws = torch.empty(int(lib().rdx_wgrad_ws_floats(M, N, K)), device=dy.device, dtype=torch.float32)
     with _timed("wgrad_acc", dy, gemm_flops(N, K, M), shape=(M, N, K)):
-        check(lib().rdx_wgrad_acc(_p(dy), dy.stride(0), _p(x), x.stride(0), M, N, K, _p(dw), dw.stride(0),
+        check(_L(dy).rdx_wgrad_acc(_p(dy), dy.stride(0), _p(x), x.stride(0), M, N, K, _p(dw), dw.stride(0),
                                   _p(db) if db is not None else None, _p(ws), ws.numel(), _stream(dy)), "wgrad_acc")
 
 
@@ -1392,19 +1422,20 @@ def _wgemm_workspace(dev, ws_bytes, n_counters):
 def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm",
           splits=1):
     """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/wgemm.hip (LDS-DMA pipelined MFMA GEMM):
-    bf16 row views a, b (unit inner stride, 16-byte aligned, K % 64 == 0); returns C, or (C, gelu(C)) for
-    EPI_BIAS_GELU. splits > 1: split-K over that many workgroups per output tile (last-arriver reduction)."""
+    16-bit (bf16 / fp16) row views a, b (unit inner stride, 16-byte aligned, K % 64 == 0); returns C, or
+    (C, gelu(C)) for EPI_BIAS_GELU. splits > 1: split-K over that many workgroups per output tile (last-arriver
+    reduction)."""
     _require_gpu(a, b)
-    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
-        raise ValueError("radhip wgemm: bf16 operands with unit inner stride required")
+    if a.dtype not in HALF or b.dtype != a.dtype or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip wgemm: bf16 / fp16 operands of one dtype with unit inner stride required")
     M, K = a.shape
     N, K2 = b.shape
     if K != K2 or K % 64:
         raise ValueError(f"radhip wgemm: K {K} vs {K2} (K % 64 == 0 required)")
     if out is None:
-        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        out = torch.empty(M, N, device=a.device, dtype=a.dtype)
     if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
-        aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        aux_out = torch.empty(M, N, device=a.device, dtype=a.dtype)
     st = _stream(a)
     ws = cnt = None
     ws_bytes = n_cnt = 0
@@ -1418,7 +1449,7 @@ def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
         ws, cnt = _wgemm_workspace(a.device, ws_bytes, n_cnt)
         ws_bytes, n_cnt = ws.numel(), cnt.numel()
     with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
-        check(lib().rdx_wgemm_bf16_ex(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+        check(_L(a).rdx_wgemm_bf16_ex(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
                                       _p(bias) if bias is not None else None, int(epilogue),
                                       _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
                                       _p(aux_out) if aux_out is not None else None,
@@ -1432,21 +1463,21 @@ def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
 def pgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=4, group_m=4,
           name="pgemm"):
     """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/pgemm.hip (8-wave deep-pipelined MFMA GEMM, one
-    workgroup per output tile): bf16 row views a, b (unit inner stride, 16-byte aligned, K % 64 == 0); returns C, or
-    (C, gelu(C)) for EPI_BIAS_GELU."""
+    workgroup per output tile): 16-bit (bf16 / fp16) row views a, b (unit inner stride, 16-byte aligned,
+    K % 64 == 0); returns C, or (C, gelu(C)) for EPI_BIAS_GELU."""
     _require_gpu(a, b)
-    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.stride(-1) != 1 or b.stride(-1) != 1:
-        raise ValueError("radhip pgemm: bf16 operands with unit inner stride required")
+    if a.dtype not in HALF or b.dtype != a.dtype or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip pgemm: bf16 / fp16 operands of one dtype with unit inner stride required")
     M, K = a.shape
     N, K2 = b.shape
     if K != K2 or K % 64:
         raise ValueError(f"radhip pgemm: K {K} vs {K2} (K % 64 == 0 required)")
     if out is None:
-        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        out = torch.empty(M, N, device=a.device, dtype=a.dtype)
     if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
-        aux_out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        aux_out = torch.empty(M, N, device=a.device, dtype=a.dtype)
     with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
-        check(lib().rdx_pgemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+        check(_L(a).rdx_pgemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
                                    _p(bias) if bias is not None else None, int(epilogue),
                                    _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
                                    _p(aux_out) if aux_out is not None else None,
@@ -1456,21 +1487,22 @@ def pgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
 
 
 # ------------------------------------------------------------------- WavLM CNN feature encoder ----
-def fe_conv_weights(layers):
-    """Per-layer device operands of the fused frozen CNN (csrc/featconv.hip) from the ConvLayer modules:
-    layer 0 (w fp32 [512, 10] and bias fp32, both bf16-rounded as autocast feeds them), layers >= 1 the
-    weight permuted to [C_out][k][C_in] = [512, K*512] bf16 and the bf16 bias; LayerNorm gamma/beta fp32."""
+def fe_conv_weights(layers, hd=torch.bfloat16):
+    """Per-layer device operands of the fused frozen CNN (csrc/featconv.hip) from the ConvLayer modules, for the
+    16-bit storage dtype hd (the autocast dtype): layer 0 (w fp32 [512, 10] and bias fp32, both rounded to hd as
+    autocast feeds them), layers >= 1 the weight permuted to [C_out][k][C_in] = [512, K*512] and the bias, in hd;
+    LayerNorm gamma/beta fp32."""
     out = []
     with torch.no_grad():
         for i, ly in enumerate(layers):
             c = ly.conv
             w = c.weight.detach()
-            b = c.bias.detach().to(torch.bfloat16) if c.bias is not None else None   # wavlm-large: conv_bias False
+            b = c.bias.detach().to(hd) if c.bias is not None else None   # wavlm-large: conv_bias False
             if i == 0:
-                wk = w.reshape(w.shape[0], -1).to(torch.bfloat16).float().contiguous()
+                wk = w.reshape(w.shape[0], -1).to(hd).float().contiguous()
                 bk = b.float().contiguous() if b is not None else torch.zeros(w.shape[0], device=w.device)
             else:
-                wk = w.permute(0, 2, 1).reshape(w.shape[0], -1).to(torch.bfloat16).contiguous()
+                wk = w.permute(0, 2, 1).reshape(w.shape[0], -1).to(hd).contiguous()
                 bk = b.contiguous() if b is not None else None
             out.append((wk, bk, ly.layer_norm.weight.detach().float().contiguous(),
                         ly.layer_norm.bias.detach().float().contiguous(), float(ly.layer_norm.eps),
@@ -1488,21 +1520,23 @@ def feature_encoder_fused(x, ops_):
     x = x.contiguous().float()
     B, L = x.shape
     w0, b0, g0, be0, eps0, k0, s0 = ops_[0]
+    hd = ops_[1][0].dtype                                   # the 16-bit storage dtype the weights were made for
+    Lb = _L(hd)
     T = (L - k0) // s0 + 1
-    h = torch.empty(B, T, 512, device=x.device, dtype=torch.bfloat16)
+    h = torch.empty(B, T, 512, device=x.device, dtype=hd)
     with _timed("fe_conv0", x, 4.0 * B * L + 2.0 * B * T * 512):            # bytes: waveform in, bf16 out
-        check(lib().rdx_fe_conv0(_p(x), B, L, _p(w0), _p(b0), _p(g0), _p(be0), eps0, k0, s0, _p(h), _stream(x)),
+        check(Lb.rdx_fe_conv0(_p(x), B, L, _p(w0), _p(b0), _p(g0), _p(be0), eps0, k0, s0, _p(h), _stream(x)),
               "fe_conv0")
     for i, (w, b, g, be, eps, k, s) in enumerate(ops_[1:], start=1):
         To = (T - k) // s + 1
-        y = torch.empty(B, To, 512, device=x.device, dtype=torch.bfloat16)
+        y = torch.empty(B, To, 512, device=x.device, dtype=hd)
         with _timed("fe_conv_gemm", x, gemm_flops(B * To, 512, k * 512), shape=(B, T, k)):
-            check(lib().rdx_gemm_bf16_strided(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To, B, To, 512,
+            check(Lb.rdx_gemm_bf16_strided(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To, B, To, 512,
                                               k * 512, _p(b) if b is not None else None, _stream(x)), "gemm_bf16_strided")
         last = i == len(ops_) - 1
         out32 = torch.empty(B, To, 512, device=x.device, dtype=torch.float32) if last else None
         with _timed("fe_ln_gelu", x, (2.0 + (4.0 if last else 2.0)) * B * To * 512, shape=(B, To)):
-            check(lib().rdx_fe_ln_gelu(_p(y), B * To, _p(g), _p(be), eps, _p(out32) if last else None, _stream(x)),
+            check(Lb.rdx_fe_ln_gelu(_p(y), B * To, _p(g), _p(be), eps, _p(out32) if last else None, _stream(x)),
                   "fe_ln_gelu")
         h, T = (out32 if last else y), To
     return h

@@ -12,12 +12,13 @@ import torch.nn as nn
 
 import torch.nn.functional as F
 
-from .ops import (Block0Convs, Block0Front, Block0Fused, BnSelu, ResBlockIdentity, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
+from .ops import (HALF, Block0Convs, Block0Front, Block0Fused, BnSelu, ResBlockIdentity, BnSeluSConv, ResTail, SConv, SConvBnSelu, SConvBnSeluSConv, sconv_ok,
                   sconv_weight_ok, sincconv_absmaxpool)
 
 
-def _bf16_autocast(x):
-    return x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+def _half_autocast(x):
+    """CUDA autocast to bf16 or fp16: the 16-bit NHWC kernels (libradhip.so / libradhip_f16.so) apply."""
+    return x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") in HALF
 
 
 def mel_edges(out_channels, sample_rate, nfft=512):
@@ -124,10 +125,10 @@ class Residual_block(nn.Module):
                 self.bn1(x)
         if self._fused_ok(x):
             # NHWC fused epilogues (csrc/sincnet.hip): conv1's bias is folded into the frozen-BN+SELU pass,
-            # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass. Under bf16 autocast the
+            # conv2 / conv_downsample biases into the add + MaxPool2d((1,3)) pass. Under bf16 / fp16 autocast the
             # 32/64-channel convolutions run on csrc/sconv.hip (conv1 with the BN+SELU in its epilogue).
             bn = self.bn2
-            bf = _bf16_autocast(x)
+            bf = _half_autocast(x)
             invstd = torch.rsqrt(bn.running_var + bn.eps)
             bnp = (self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
             w2 = self.conv2.weight

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import wavlm_fused
-from .ops import GatedAttention, PosConv, fe_conv_weights, feature_encoder_fused, posconv_weights
+from .ops import HALF, GatedAttention, PosConv, fe_conv_weights, feature_encoder_fused, half_dtype, posconv_weights
 
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
 # restated, not verifiable offline: parity unpinned for those regularisers)
@@ -183,12 +183,12 @@ class FeatureEncoder(nn.Module):
         self.cfg = cfg
 
     def _fused_ok(self, x):
-        """bf16 CUDA pass with the WavLM-Large CNN geometry and frozen weights -> csrc/featconv.hip (token-major
+        """bf16 / fp16 CUDA pass with the WavLM-Large CNN geometry and frozen weights -> csrc/featconv.hip (token-major
         conv0+LN+GELU kernel, implicit-GEMM convs, LN+GELU passes) instead of MIOpen convs plus transposes,
         casts and separate LayerNorm/GELU launches."""
         c = self.cfg
         return (x.is_cuda and x.dim() == 2 and torch.is_autocast_enabled("cuda")
-                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and len(c.conv_dim) >= 2
+                and torch.get_autocast_dtype("cuda") in HALF and len(c.conv_dim) >= 2
                 and all(d == 512 for d in c.conv_dim) and c.conv_kernel[0] == 10
                 and c.feat_extract_norm == "layer" and c.feat_extract_activation == "gelu"
                 and all(k * 512 % 8 == 0 for k in c.conv_kernel)
@@ -197,9 +197,10 @@ class FeatureEncoder(nn.Module):
 
     def forward(self, x):
         if self._fused_ok(x):
-            key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+            hd = half_dtype()
+            key = (hd,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
             if getattr(self, "_fe_key", None) != key:
-                self._fe_ops = fe_conv_weights(self.conv_layers)
+                self._fe_ops = fe_conv_weights(self.conv_layers, hd)
                 self._fe_key = key
             return feature_encoder_fused(x, self._fe_ops).transpose(1, 2)     # [B, 512, T] view, as the modules
         x = x[:, None]
@@ -246,11 +247,11 @@ class PositionalConvEmbedding(nn.Module):
         return self._w
 
     def _fused_ok(self, x):
-        """bf16 CUDA step with the WavLM-Large geometry and frozen weights -> csrc/posconv.hip (one MFMA launch
+        """bf16 / fp16 CUDA step with the WavLM-Large geometry and frozen weights -> csrc/posconv.hip (one MFMA launch
         each way instead of MIOpen's per-utterance im2col + GEMM + col2im)."""
         c = self.conv
         return (x.is_cuda and x.dim() == 3 and torch.is_autocast_enabled("cuda")
-                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and c.in_channels == 1024
+                and torch.get_autocast_dtype("cuda") in HALF and c.in_channels == 1024
                 and c.out_channels == 1024 and c.groups == 16 and c.kernel_size[0] == 128 and self.remove == 1
                 and self.act_name == "gelu" and os.environ.get("RADHIP_FUSED_POSCONV", "1") != "0"
                 and not any(p.requires_grad for p in c.parameters()))
@@ -259,9 +260,10 @@ class PositionalConvEmbedding(nn.Module):
         c = self.conv
         if self._fused_ok(x):
             w = self._weight()
-            key = (w.data_ptr(), getattr(self, "_wkey", None))
+            hd = half_dtype()
+            key = (w.data_ptr(), getattr(self, "_wkey", None), hd)
             if getattr(self, "_pc_key", None) != key:
-                self._pc = posconv_weights(w)
+                self._pc = posconv_weights(w, hd)
                 self._pc_key = key
             return PosConv.apply(x, self._pc[0], self._pc[1], c.bias)
         y = F.conv1d(x.transpose(1, 2), self._weight(), c.bias, c.stride, c.padding, c.dilation, c.groups)
@@ -338,7 +340,7 @@ class Attention(nn.Module):
         gate = g[..., 0] * (g[..., 1] * self.gru_rel_pos_const.view(1, 1, H) - 1.0) + 2.0   # [B, T, H]
         qq, kk, vv = self._qkv(h)
         dt = qq.dtype
-        if (qq.is_cuda and dt == torch.bfloat16 and kk.dtype == dt and vv.dtype == dt and Dh == 64
+        if (qq.is_cuda and dt in HALF and kk.dtype == dt and vv.dtype == dt and Dh == 64
                 and not position_bias.requires_grad):
             # fused MFMA kernel (csrc/attention.hip): bias formed in registers, dropout mask from a device
             # seed (HIP-graph replayable), output already [B, T, E] for out_proj

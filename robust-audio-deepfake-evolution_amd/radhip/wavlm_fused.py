@@ -1,4 +1,5 @@
-"""Fused WavLM encoder layer for the bf16 training/eval step (csrc/wavlm_layer.hip + attention.hip).
+"""Fused WavLM encoder layer for the 16-bit (bf16 or fp16 autocast) training/eval step (csrc/wavlm_layer.hip +
+attention.hip; fp16 runs the same kernels from libradhip_f16.so).
 
 The LoRA weight gradients (four skinny reductions over the tokens) are one kernel that accumulates
 into the fp32 .grad buffers directly (so the Function returns no gradient for those leaves).
@@ -10,7 +11,7 @@ LN1 + gate + LoRA-A, dropout + residual + LN2, GELU, and their backwards. Same m
 reference layer (HF WavLMEncoderLayerStableLayerNorm + peft LoRA q/v; DualStreamSEMamba.py:292-439,
 main.py:103-158); dropout masks come from the device-seeded counter hash (graph replayable).
 
-Used when: CUDA, bf16 autocast, stable layer norm, E = 1024 with 64-dim heads, GELU FFN, a frozen
+Used when: CUDA, bf16 or fp16 autocast, stable layer norm, E = 1024 with 64-dim heads, GELU FFN, a frozen
 base layer, and either no LoRA or LoRA r = 8 on exactly q_proj and v_proj. Anything else takes the
 module path (radhip/wavlm.py), which is what the fp32 parity tests exercise.
 RADHIP_FUSED_WAVLM=0 disables the fused layer (A/B measurement).
@@ -22,8 +23,9 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from ._lib import check, lib
-from .ops import _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, layer_gemm, rel_bias_table, wgemm_policy
+from ._lib import check
+from .ops import (HALF, _L, _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, half_dtype, layer_gemm,
+                  rel_bias_table, wgemm_policy)
 
 E_FUSED = 1024
 
@@ -62,7 +64,7 @@ def eligible(encoder, h):
     if not (enabled() and h.is_cuda and encoder.stable and cfg.hidden_size == E_FUSED
             and cfg.hidden_size // cfg.num_attention_heads == 64 and cfg.hidden_act == "gelu"):
         return False
-    if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+    if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") in HALF):
         return False
     st = encoder.__dict__.get("_fused_ok")
     if st is not None and st[0] == _trainable_signature(encoder):
@@ -92,37 +94,39 @@ def _trainable_signature(encoder):
 
 
 class _LayerCache:
-    """bf16 copies of a frozen layer's weights (rebuilt when a source tensor changes) and the
+    """16-bit (the autocast dtype) copies of a frozen layer's weights (rebuilt when a source tensor or the dtype
+    changes) and the
     [3E, E + 2r] q/k/v operand whose last 2r columns receive s * lora_B every forward."""
 
     def __init__(self):
         self.key = None
 
-    def refresh(self, layer, lora):
+    def refresh(self, layer, lora, hd):
         a, ff = layer.attention, layer.feed_forward
         from .wavlm import _base
         bq, bk, bv = _base(a.q_proj), _base(a.k_proj), _base(a.v_proj)
         src = [bq.weight, bk.weight, bv.weight, bq.bias, bk.bias, bv.bias, a.out_proj.weight, a.out_proj.bias,
                ff.intermediate_dense.weight, ff.intermediate_dense.bias, ff.output_dense.weight,
                ff.output_dense.bias]
-        key = (lora is not None,) + tuple((t.data_ptr(), t._version) for t in src)
+        key = (lora is not None, hd) + tuple((t.data_ptr(), t._version) for t in src)
         if key == self.key:
             return
         E = bq.weight.shape[0]
         r2 = 16 if lora is not None else 0
         with torch.no_grad():
-            w = torch.zeros(3 * E, E + r2, device=bq.weight.device, dtype=torch.bfloat16)
-            w[:, :E] = torch.cat([bq.weight, bk.weight, bv.weight]).to(torch.bfloat16)
+            w = torch.zeros(3 * E, E + r2, device=bq.weight.device, dtype=hd)
+            w[:, :E] = torch.cat([bq.weight, bk.weight, bv.weight]).to(hd)
             self.wext = w
-            self.bqkv = torch.cat([bq.bias, bk.bias, bv.bias]).to(torch.bfloat16)
-            self.wo = a.out_proj.weight.to(torch.bfloat16)
-            self.bo = a.out_proj.bias.to(torch.bfloat16)
-            self.w1 = ff.intermediate_dense.weight.to(torch.bfloat16)
-            self.b1 = ff.intermediate_dense.bias.to(torch.bfloat16)
-            self.w2 = ff.output_dense.weight.to(torch.bfloat16)
-            self.b2 = ff.output_dense.bias.to(torch.bfloat16)
+            self.bqkv = torch.cat([bq.bias, bk.bias, bv.bias]).to(hd)
+            self.wo = a.out_proj.weight.to(hd)
+            self.bo = a.out_proj.bias.to(hd)
+            self.w1 = ff.intermediate_dense.weight.to(hd)
+            self.b1 = ff.intermediate_dense.bias.to(hd)
+            self.w2 = ff.output_dense.weight.to(hd)
+            self.b2 = ff.output_dense.bias.to(hd)
             # transposed copies for the input-gradient GEMMs on csrc/wgemm.hip (B operand [N][K]; built lazily)
             self.woT = self.w1T = self.w2T = self.wqkvT = None
+            self.hd = hd
             self.wg = a.gru_rel_pos_linear.weight.detach().float().contiguous()
             self.bg = a.gru_rel_pos_linear.bias.detach().float().contiguous()
             self.gconst = a.gru_rel_pos_const.detach().float().reshape(-1).contiguous()
@@ -182,7 +186,9 @@ class WavLMLayerFn(torch.autograd.Function):
         sd = seed if seed is not None else None
         sdp = _p(sd) if sd is not None else None
         salt = SALT_BASE + 8 * index
-        x1 = torch.empty(M, ldx, device=dev, dtype=torch.bfloat16)
+        hd = cache.hd
+        L = _L(hd)
+        x1 = torch.empty(M, ldx, device=dev, dtype=hd)
         gate = torch.empty(M, H, device=dev, dtype=torch.float32)
         mean1 = torch.empty(M, device=dev, dtype=torch.float32)
         rstd1 = torch.empty_like(mean1)
@@ -191,13 +197,13 @@ class WavLMLayerFn(torch.autograd.Function):
             # the previous layer's residual, computed here into its output (= this layer's input) tensor
             chain.pending_res = None
             _, h2p, fop, salt_res, p_res = pend
-            check(lib().rdx_wl_res_ln1_fwd(_p(h2p), _p(fop), salt_res, float(p_res), _p(hf), _p(ln1.weight),
+            check(L.rdx_wl_res_ln1_fwd(_p(h2p), _p(fop), salt_res, float(p_res), _p(hf), _p(ln1.weight),
                                            _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
                                            _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3,
                                            salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1), _p(rstd1), M,
                                            E, st), "wl_res_ln1_fwd")
         else:
-            check(lib().rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg),
+            check(L.rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg),
                                        _p(cache.bg), _p(cache.gconst), _p(aq) if lora else None,
                                        _p(av) if lora else None, 8, sdp, salt + 3, salt + 4, float(p_lora), _p(x1),
                                        ldx, _p(gate), _p(mean1), _p(rstd1), M, E, st), "wl_ln1_fwd")
@@ -206,12 +212,12 @@ class WavLMLayerFn(torch.autograd.Function):
             qkv = layer_gemm(pol, x1, cache.wext, cache.bqkv)
         else:
             qkv = F.linear(x1, cache.wext, cache.bqkv)                      # [M, 3E] (LoRA folded in)
-        o = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        o = torch.empty(M, E, device=dev, dtype=hd)
         lse = torch.empty(B, H, T, device=dev, dtype=torch.float32)
         zseed = sd if sd is not None else torch.zeros(1, dtype=torch.int64, device=dev)
         mask = attn_keep_mask(B, T, H, float(p_attn), dev)
         with _timed("attn_fwd", hf, 2.0 * 2 * B * H * T * T * 64):
-            check(lib().rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(rel),
+            check(L.rdx_attn_fwd(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, _p(gate), _p(rel),
                                      _p(zseed), int(index), float(p_attn), 0.125, _p(o), E, _p(lse),
                                      _p(mask) if mask is not None else None, B, T, H, 64, st), "attn_fwd")
         pol = _gemm("out", M, E, E)
@@ -220,10 +226,10 @@ class WavLMLayerFn(torch.autograd.Function):
         else:
             aout = F.linear(o, cache.wo, cache.bo)
         h2 = torch.empty(M, E, device=dev, dtype=torch.float32)
-        x2 = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        x2 = torch.empty(M, E, device=dev, dtype=hd)
         mean2 = torch.empty_like(mean1)
         rstd2 = torch.empty_like(mean1)
-        check(lib().rdx_wl_add_ln_fwd(_p(hf), _p(aout), sdp, salt + 1, float(p_hidden), _p(h2), _p(ln2.weight),
+        check(L.rdx_wl_add_ln_fwd(_p(hf), _p(aout), sdp, salt + 1, float(p_hidden), _p(h2), _p(ln2.weight),
                                       _p(ln2.bias), float(ln2.eps), _p(x2), _p(mean2), _p(rstd2), M, E, st),
               "wl_add_ln_fwd")
         F4 = cache.w1.shape[0]
@@ -233,7 +239,7 @@ class WavLMLayerFn(torch.autograd.Function):
         else:
             u = F.linear(x2, cache.w1, cache.b1)
             v = torch.empty_like(u)
-            check(lib().rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
+            check(L.rdx_wl_gelu(0, _p(u), None, _p(v), u.numel(), st), "wl_gelu")
         pol = _gemm("ffn2", M, E, F4)
         if pol is not None:
             fo = layer_gemm(pol, v, cache.w2, cache.b2)
@@ -243,7 +249,7 @@ class WavLMLayerFn(torch.autograd.Function):
         if chain is not None and index < chain.n - 1:
             chain.pending_res = (out.data_ptr(), h2, fo, salt + 2, float(p_hidden))   # -> the next LN1 forward
         else:
-            check(lib().rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st),
+            check(L.rdx_wl_residual(_p(h2), _p(fo), sdp, salt + 2, float(p_hidden), _p(out), M * E, st),
                   "wl_residual")
         ctx.save_for_backward(hf, x1, qkv, o, lse, gate, h2, mean1, rstd1, mean2, rstd2, u, zseed, rel, aq, av)
         ctx.layer, ctx.cache, ctx.mask, ctx.chain = layer, cache, mask, chain
@@ -264,13 +270,15 @@ class WavLMLayerFn(torch.autograd.Function):
         salt = SALT_BASE + 8 * index
         ldx = x1.shape[1]
         g = dout.contiguous().view(M, E).float()
+        hd = x1.dtype
+        L = _L(hd)
         chain = ctx.chain
         rec = chain.dfo.pop(index, None) if chain is not None else None
         if rec is not None and rec[0] == g.data_ptr():
             dfo = rec[1]                  # written by the next layer's LN1 backward along with g
         else:
-            dfo = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
-            check(lib().rdx_wl_dropout_bwd(_p(g), sdp, salt + 2, p_hidden, _p(dfo), M * E, st), "wl_dropout_bwd")
+            dfo = torch.empty(M, E, device=dev, dtype=hd)
+            check(L.rdx_wl_dropout_bwd(_p(g), sdp, salt + 2, p_hidden, _p(dfo), M * E, st), "wl_dropout_bwd")
         F4 = u.shape[1]
         pol = _gemm("d_ffn2", M, F4, E)
         if pol is not None:                             # FFN2's input gradient with the GELU backward fused
@@ -278,16 +286,16 @@ class WavLMLayerFn(torch.autograd.Function):
         else:
             dv = torch.mm(dfo, cache.w2)
             du = torch.empty_like(u)
-            check(lib().rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
+            check(L.rdx_wl_gelu(1, _p(u), _p(dv), _p(du), u.numel(), st), "wl_gelu_bwd")
         pol = _gemm("d_ffn1", M, E, F4)
         if pol is not None:
             dx2 = layer_gemm(pol, du, cache.t("w1"))
         else:
             dx2 = torch.mm(du, cache.w1)
         dh2 = torch.empty(M, E, device=dev, dtype=torch.float32)
-        daout = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+        daout = torch.empty(M, E, device=dev, dtype=hd)
         ln1, ln2 = layer.layer_norm, layer.final_layer_norm
-        check(lib().rdx_wl_ln_bwd(_p(dx2), E, _p(h2), _p(mean2), _p(rstd2), _p(ln2.weight), _p(g), _p(dh2), sdp,
+        check(L.rdx_wl_ln_bwd(_p(dx2), E, _p(h2), _p(mean2), _p(rstd2), _p(ln2.weight), _p(g), _p(dh2), sdp,
                                   salt + 1, p_hidden, _p(daout), M, E, st), "wl_ln_bwd")
         pol = _gemm("d_out", M, E, E)
         if pol is not None:
@@ -295,12 +303,12 @@ class WavLMLayerFn(torch.autograd.Function):
         else:
             do = torch.mm(daout, cache.wo)
         D = torch.empty(B, H, T, device=dev, dtype=torch.float32)
-        dqkv = torch.empty(M, 3 * E, device=dev, dtype=torch.bfloat16)
+        dqkv = torch.empty(M, 3 * E, device=dev, dtype=hd)
         dgate = torch.empty(M, H, device=dev, dtype=torch.float32)
         with _timed("attn_bwd", hf, 2.0 * 5 * B * H * T * T * 64):
             attn_bwd_launch(_p(qkv), 3 * E, _off(qkv, E), 3 * E, _off(qkv, 2 * E), 3 * E, gate, rel, ctx.mask,
                             _p(zseed), int(index), p_attn, _p(o), E, lse, _p(do), E, D, _p(dqkv), _off(dqkv, E),
-                            _off(dqkv, 2 * E), 3 * E, dgate, B, T, H, st)
+                            _off(dqkv, 2 * E), 3 * E, dgate, B, T, H, st, hd)
         pol = _gemm("d_qkv", M, ldx, 3 * E) if not lora else None   # (active LoRA: wext changes every step)
         if pol is not None:
             dx1 = layer_gemm(pol, dqkv, cache.t("wqkv"))
@@ -312,9 +320,9 @@ class WavLMLayerFn(torch.autograd.Function):
             sgp = _p(chain.g)                                   # this input's layer-weighted-sum gradient
             swp = ctypes.c_void_p(chain.p.data_ptr() + 4 * index)
         if chain is not None and index > 0:
-            ddrop = torch.empty(M, E, device=dev, dtype=torch.bfloat16)
+            ddrop = torch.empty(M, E, device=dev, dtype=hd)
             ddp = _p(ddrop)
-        check(lib().rdx_wl_ln1_bwd_ex(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
+        check(L.rdx_wl_ln1_bwd_ex(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
                                       _p(ln1.bias), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
                                       _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3, salt + 4,
                                       p_lora, _p(dh2), _p(dh), None, sgp, swp, salt - 8 + 2, p_hidden, ddp, M, E, st),
@@ -330,7 +338,7 @@ class WavLMLayerFn(torch.autograd.Function):
                 if prm.grad is None:
                     prm.grad = torch.zeros_like(prm)
                 gs.append(prm.grad)
-            check(lib().rdx_wl_lora_grad(_p(dqkv), 3 * E, _p(x1), ldx, _p(dx1), ldx, sdp, salt + 3, salt + 4,
+            check(L.rdx_wl_lora_grad(_p(dqkv), 3 * E, _p(x1), ldx, _p(dx1), ldx, sdp, salt + 3, salt + 4,
                                          p_lora, scale, _p(gs[0]), _p(gs[1]), _p(gs[2]), _p(gs[3]), M, E, 8, st),
                   "wl_lora_grad")
         return (dh.view(B, T, E),) + (None,) * 14
@@ -356,8 +364,9 @@ class FusedEncoderRunner:
 
     def prepare(self, device):
         loras = [_lora_parts(layer.attention) for layer in self.encoder.layers]
+        hd = half_dtype()
         for layer, cache, lp in zip(self.encoder.layers, self.caches, loras):
-            cache.refresh(layer, lp)
+            cache.refresh(layer, lp, hd)
         if loras[0] is None:
             return loras
         key = tuple(c.wext.data_ptr() for c in self.caches) + tuple(
@@ -370,7 +379,7 @@ class FusedEncoderRunner:
             self.pack_key = key
         lp0 = loras[0][0]
         n = len(self.caches)
-        check(lib().rdx_wl_lora_pack(n, self.tab[0].data_ptr(), self.tab[1].data_ptr(), self.tab[2].data_ptr(),
+        check(_L(hd).rdx_wl_lora_pack(n, self.tab[0].data_ptr(), self.tab[1].data_ptr(), self.tab[2].data_ptr(),
                                      self.caches[0].wext.shape[1], 8, float(lp0.scaling[lp0.adapter]), E_FUSED,
                                      _stream(self.tab)), "wl_lora_pack")
         return loras

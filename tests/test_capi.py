@@ -1,4 +1,4 @@
-"""libradhip.so loads, exports every symbol include/radhip.h declares, and its host-only entry
+"""libradhip.so (and libradhip_f16.so) load, export every symbol include/radhip.h declares, and its host-only entry
 points behave (no GPU needed: argument checks return before any HIP call)."""
 import ctypes
 import os
@@ -17,6 +17,28 @@ def test_library_loads_and_exports_header_symbols():
         assert hasattr(L, name), f"libradhip.so does not export {name}"
         assert name in _lib.SIGNATURES, f"no ctypes signature for {name}"
     assert L.rdx_version().decode().startswith("radhip")
+
+
+def test_f16_library_exports_the_same_entry_points():
+    """libradhip_f16.so: the same sources built with -DRDX_F16 (fp16 16-bit storage), the same C ABI, loaded
+    beside libradhip.so with its own bindings (-Bsymbolic, RTLD_LOCAL)."""
+    L, L16 = _lib.lib(), _lib.lib16()
+    for name in _lib.header_symbols():
+        assert hasattr(L16, name), f"libradhip_f16.so does not export {name}"
+    assert L16._handle != L._handle
+    # a host-only entry point answers from the f16 library itself
+    assert L16.rdx_strerror(-2) == b"unsupported shape"
+    assert L16.rdx_scan_nblk_d(288) == L.rdx_scan_nblk_d(288)
+
+
+def test_ops_pick_the_library_by_storage_dtype():
+    import torch
+    from radhip import ops
+    assert ops._L(torch.bfloat16) is _lib.lib() and ops._L(torch.float32) is _lib.lib()
+    assert ops._L(torch.float16) is _lib.lib16() and ops._L(torch.float32, torch.float16) is _lib.lib16()
+    with pytest.raises(TypeError):
+        ops._L(torch.bfloat16, torch.float16)
+    assert ops._dtype_code(torch.empty(0, dtype=torch.float16)) == ops._dtype_code(torch.empty(0, dtype=torch.bfloat16))
 
 
 def test_error_codes():

@@ -119,15 +119,17 @@ def test_mamba_golden_reference_block(golden):
         np.testing.assert_allclose(p.grad.cpu().numpy(), g[f"grad:{k}"], rtol=2e-3, atol=1e-5, err_msg=k)
 
 
-def test_scan2_matches_segmented_scan_bf16():
-    """The chunked scan against csrc/bimamba.hip's segmented kernels at the Phase-6 shape in bf16 storage: the same
-    outputs and gradients up to fp32 summation order (both chains run in fp32)."""
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_scan2_matches_segmented_scan_16bit(dt):
+    """The chunked scan against csrc/bimamba.hip's segmented kernels at the Phase-6 shape in bf16 / fp16 storage
+    (libradhip.so / libradhip_f16.so): the same outputs and gradients up to fp32 summation order (both chains run
+    in fp32)."""
     from radhip import ops
     g = torch.Generator(device=DEV).manual_seed(3)
     dirs, B, L, D, N, R = 2, 4, 201, 288, 16, 9
-    u = torch.randn(dirs, B, L, D, device=DEV, generator=g).to(torch.bfloat16)
-    delta = (0.5 * torch.randn(dirs, B, L, D, device=DEV, generator=g)).to(torch.bfloat16)
-    xdbl = torch.randn(dirs, B, L, R + 2 * N, device=DEV, generator=g).to(torch.bfloat16)
+    u = torch.randn(dirs, B, L, D, device=DEV, generator=g).to(dt)
+    delta = (0.5 * torch.randn(dirs, B, L, D, device=DEV, generator=g)).to(dt)
+    xdbl = torch.randn(dirs, B, L, R + 2 * N, device=DEV, generator=g).to(dt)
     A_log = torch.log(torch.arange(1, N + 1, device=DEV, dtype=torch.float32)).repeat(D, 1)
     Dp = torch.randn(D, device=DEV, generator=g)
     bias = 0.1 * torch.randn(D, device=DEV, generator=g)
@@ -181,7 +183,7 @@ def test_dwconv_both_directions_vs_torch():
 
 
 # -------------------------------------------------------------------- layer-weighted sum -----
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_layer_weighted_sum(dtype):
     from radhip.ops import layer_weighted_sum
     hs = [torch.randn(2, 201, 1024, device=DEV).to(dtype).requires_grad_(True) for _ in range(25)]
@@ -326,7 +328,7 @@ def test_fgm_attack_matches_reference_fixture(golden):
     assert torch.equal(p, torch.ones(10, device=DEV))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("first", [True, False])
 def test_fused_residual_block_matches_torch(dtype, first):
     """SincNet Residual_block with frozen BN: fused NHWC epilogues (bnselu, res_tail) == the torch
@@ -345,7 +347,7 @@ def test_fused_residual_block_matches_torch(dtype, first):
     x = torch.randn(2, filts[0], 7, 101, device=DEV)
     x[..., :3] = 0.0                              # ties inside the first pooling windows
     x = x.contiguous(memory_format=torch.channels_last)
-    bf16 = dtype == torch.bfloat16
+    bf16 = dtype != torch.float32            # a 16-bit autocast dtype (bf16 or fp16)
 
     def run(fused, amp):
         b = Residual_block(filts, first=first).to(DEV)
@@ -354,7 +356,7 @@ def test_fused_residual_block_matches_torch(dtype, first):
         if not fused:
             b._fused_ok = lambda _x: False         # torch conv/bn/selu/add/maxpool graph
         xx = x.detach().clone().requires_grad_()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=dtype if amp else torch.bfloat16, enabled=amp):
             y = b(xx)
         assert (not fused) or b._fused_ok(xx)
         y.backward(g.to(y.dtype))
@@ -371,8 +373,8 @@ def test_fused_residual_block_matches_torch(dtype, first):
             scale = b.abs().max().item() + 1e-6
             torch.testing.assert_close(fused[n] / scale, b / scale, rtol=1e-4, atol=1e-5, msg=n)
     else:
-        # bf16 rounding can flip a max-pool argmax between near-equal values, which moves whole gradient
-        # entries: hold the fused path to torch's own bf16 graph's distance from the fp32 result
+        # 16-bit rounding can flip a max-pool argmax between near-equal values, which moves whole gradient
+        # entries: hold the fused path to torch's own graph's distance (same autocast dtype) from the fp32 result
         tb16 = run(False, True)
         for n, b in ref32.items():
             e_f = ((fused[n] - b).norm() / (b.norm() + 1e-12)).item()
