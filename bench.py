@@ -33,7 +33,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PEAKS = {"hbm": 8000.0, "fp32": 157.3, "bf16": 2500.0}  # GB/s ; TFLOP/s (MI355X_MICROARCH.md, dense)
+PEAKS = {"hbm": 8000.0, "fp32": 157.3, "bf16": 2500.0}  # GB/s ; TFLOP/s (MI355X_MICROARCH.md, dense; "bf16" = the
+# 16-bit MFMA peak, which fp16 shares: --amp fp16 runs the same kernels from libradhip_f16.so at the same rate)
 KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "sincconv_mfma": ("mfma", "bf16"), "selective_scan_fwd": ("hbm", None),
                 "selective_scan_bwd": ("hbm", None), "layer_wsum_fwd": ("hbm", None),
                 "layer_wsum_bwd": ("hbm", None), "rawboost_batch": ("hbm", None),

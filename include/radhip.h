@@ -1,5 +1,5 @@
 /*
- * radhip.h — C ABI of libradhip.so, the hand-written HIP (gfx950 / MI355X) kernels of the
+ * radhip.h — C ABI of libradhip.so (and libradhip_f16.so), the hand-written HIP (gfx950 / MI355X) kernels of the
  * Phase-6 audio-deepfake hot path (lux-liang/Robust-Audio-Deepfake-Evolution).
  *
  * Conventions ("C-ABI conventions"):
@@ -11,8 +11,14 @@
  *   - `stream` is a hipStream_t (0 = legacy default stream). Nothing synchronises the host,
  *     so every launch function is graph-capturable.
  *   - Tensors are row-major and contiguous unless a leading dimension (ld*) is given.
- *   - dtype selects the storage type of the "activation" operands (RDX_F32 or RDX_BF16);
- *     arithmetic is fp32 (fp64 for the RawBoost filters and reductions).
+ *   - dtype selects the storage type of the "activation" operands (RDX_F32 or RDX_BF16 = the library's
+ *     16-bit type); arithmetic is fp32 (fp64 for the RawBoost filters and reductions).
+ *   - Two libraries export this same ABI from the same sources: libradhip.so stores 16-bit operands
+ *     as bf16, libradhip_f16.so (built with -DRDX_F16) as IEEE fp16 — the reference trains under
+ *     torch.cuda.amp.autocast(), i.e. fp16 (src/main.py:28,1049). In libradhip_f16.so every "bf16"
+ *     in a comment or an entry-point name (rdx_gemm_bf16, rdx_wgemm_bf16_ex, ...) reads "fp16"; the
+ *     MFMA forms (v_mfma_f32_*_f16 vs *_bf16) take the same cycles. Both are linked -Bsymbolic so one
+ *     process can load both (radhip/_lib.py: lib() and lib16()).
  *   - No global state: thread-compatible, one process per GPU.
  *
  * Each function names the reference interface it replaces (file:line into the reference).

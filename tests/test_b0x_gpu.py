@@ -86,12 +86,13 @@ def _rel(a, b):
 
 
 def _same_forward(y1, y0):
-    """bf16: bit-identical. fp16: within one ulp (relative 2^-10) everywhere and bit-identical on >= 99.8 %."""
+    """bf16: bit-identical. fp16: bit-identical on >= 99.8 % of the outputs, elsewhere within one fp16 ulp of the
+    pre-pool terms (conv2 + conv_downsample, |.| <= ~4: 2^-9 absolute; the sum can cancel, so the bound is not
+    relative to the output)."""
     if y0.dtype == torch.bfloat16:
         return torch.equal(y1, y0)
     a, b = y1.float(), y0.float()
-    ulp = torch.pow(2.0, (torch.frexp(b.abs().clamp_min(2.0 ** -14))[1] - 11).float())
-    return bool(((a - b).abs() <= ulp).all()) and float((y1 != y0).float().mean()) < 2e-3
+    return bool(((a - b).abs() <= 2.0 ** -9 + 2.0 ** -10 * b.abs()).all()) and float((y1 != y0).float().mean()) < 2e-3
 
 
 @pytest.mark.parametrize("N,H,W,dt", CASES)

@@ -36,3 +36,12 @@ for dt in (torch.bfloat16, torch.float16):
             # per channel / per row histogram
             print("   channels", bad.sum((0, 2, 3)).tolist())
             print("   rows", bad.sum((0, 1, 3)).tolist())
+
+# the test's criterion
+from test_b0x_gpu import _same_forward  # noqa: E402
+blk = _block(2 + 21490)
+x = _x(2, 23, 21490, seed=21490)
+y1, y0 = run(blk, x, True, torch.float16), run(blk, x, False, torch.float16)
+d = (y1.float() - y0.float()).abs()
+print("max abs diff", float(d.max()), "mismatch frac", float((y1 != y0).float().mean()), "same_forward",
+      _same_forward(y1, y0))
