@@ -3,10 +3,10 @@
 
 One step = one optimizer step of the Phase-6 recipe on every rank: `accum` (4) micro-batches of
 `micro_batch` (8) synthetic utterances, each micro-batch = GPU RawBoost (algo 5, p 0.8) + codec
-resampling (p 0.3 x 0.5) + pad_random/tile to 64 600 + mixup, bf16-autocast forward of the full
-DualStreamSEMamba (random-init WavLM-Large + LoRA r8 q/v, SincNet, 4 Bi-Mamba layers), focal loss,
-backward, FGM attack (eps 0.5 on feature_projection) + adversarial forward/backward + restore; then
-all-reduce (RCCL, N > 1), clip 3.0, AdamW, EMA, LR schedule. An utterance counts once per step.
+resampling (p 0.3 x 0.5) + pad_random/tile to 64 600 + mixup, fp16-autocast forward (the reference's dtype,
+src/main.py:28,1049; the kernels of libradhip_f16.so; --amp bf16 runs libradhip.so) of the full DualStreamSEMamba (random-init WavLM-Large + LoRA r8 q/v, SincNet, 4 Bi-Mamba layers), focal loss,
+backward (GradScaler-scaled, as src/main.py:1077-1108), FGM attack (eps 0.5 on feature_projection) + adversarial
+forward/backward + restore; then all-reduce (RCCL, N > 1), unscale + clip 3.0, AdamW, EMA, LR schedule. An utterance counts once per step.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -78,7 +78,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--accum", type=int, default=4)
-    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--amp", default="fp16", choices=["bf16", "fp16", "fp32"],
+                    help="autocast dtype: fp16 + GradScaler = the reference's (default); bf16 the same kernels "
+                         "with bf16 storage")
     ap.add_argument("--layerdrop", type=float, default=0.0,
                     help="WavLM LayerDrop during the bench (0 = every layer runs; never less work)")
     ap.add_argument("--pool", type=int, default=64, help="synthetic utterances resident in HBM per rank")

@@ -11,8 +11,9 @@ Same flags, config keys and output layout as the reference (src/main.py:161-796,
       weights/checkpoint_epoch_{e:03d}.pth (last 3 kept), weights/swa.pth,
       metrics/dev_score.txt, metrics/dev_t-DCF_EER_{e}epo.txt, metrics/t-DCF_EER_{e:03d}epo.txt,
       {eval_output}, t-DCF_EER.txt, eval_scores_2021DF.txt + t-DCF_EER_2021DF.txt (auto_eval_2021_df)
-Extra flags: --amp {bf16,fp16,fp32} (the reference's fp16 autocast + GradScaler is --amp fp16; bf16 is
-the MI355X default), --eager (no HIP graphs), --loader-threads.
+Extra flags: --amp {fp16,bf16,fp32} (default fp16: the reference's fp16 autocast + GradScaler, on the kernels of
+libradhip_f16.so; bf16 runs the same kernels with bf16 storage, no GradScaler), --eager (no HIP graphs),
+--loader-threads.
 
 Differences, all documented in DESIGN.md:
   * data-parallel: one process per GPU (RCCL); the train list is sharded per global micro-step; by default
@@ -515,12 +516,13 @@ def parse_args(argv=None):
     parser.add_argument("--start_epoch", type=int, default=0, help="epoch to start training from")
     parser.add_argument("--pretrained_weights", type=str, default=None, help="pretrained weights for fine-tuning")
     parser.add_argument("--model", type=str, default=None, help="override the model architecture")
-    parser.add_argument("--amp", default="bf16", choices=sorted(AMP), help="autocast dtype (reference: fp16)")
-    parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "bf16"],
-                        help="scoring precision: fp32 as the reference scores (default), or bf16 autocast, which runs "
-                             "the hand-written HIP encoder / SincNet path (tools/bench_eval.py: throughput and score "
-                             "deviation). bf16 scores are parity-unpinned against the reference (no fixture pins its "
-                             "EER); with --eval_amp bf16 they also drive the dev-set best-model selection")
+    parser.add_argument("--amp", default="fp16", choices=sorted(AMP), help="autocast dtype (reference: fp16)")
+    parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "bf16", "fp16"],
+                        help="scoring precision: fp32 as the reference scores (default), or bf16 / fp16 autocast, which "
+                             "runs the hand-written HIP encoder / SincNet path (tools/bench_eval.py: throughput and "
+                             "score deviation). 16-bit scores are parity-unpinned against the reference (no fixture "
+                             "pins its EER); with --eval_amp bf16 / fp16 they also drive the dev-set best-model "
+                             "selection")
     parser.add_argument("--eager", action="store_true", help="launch kernel by kernel (no HIP graphs)")
     parser.add_argument("--no-window", dest="no_window", action="store_true",
                         help="replay one graph pair per micro-batch instead of the batched accumulation window")

@@ -159,7 +159,7 @@ def test_cli_flags_and_output_layout(tmp_path):
     a = cli.parse_args(["--config", "config/Phase6_Proposed.conf", "--comment", "x", "--eval",
                         "--eval_model_weights", "w.pth", "--seed", "7", "--start_epoch", "2"])
     assert a.eval and a.seed == 7 and a.start_epoch == 2 and a.eval_model_weights == "w.pth"
-    assert a.output_dir == "./exp_result" and a.amp == "bf16" and not a.eager
+    assert a.output_dir == "./exp_result" and a.amp == "fp16" and not a.eager   # the reference's autocast dtype
     cfg = {"track": "LA", "num_epochs": 20, "batch_size": 8}
     assert str(cli.model_tag_dir(a, cfg)) == os.path.join("exp_result", "LA_Phase6_Proposed_ep20_bs8_x")
     from pathlib import Path
