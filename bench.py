@@ -227,8 +227,9 @@ def cpu_baseline(config, threads, protocol):
     protocol "full" = BASELINE.md §3: 3 warm-up + 10 timed steps at micro-batch 2 and at 8, a step being
     one FGM micro-batch step (an optimizer step is 4 of them: the per-utterance rate is the same, and the
     optimizer-step reading at B = 8 would take ~25 min, past one GPU-box call).
-    protocol "bounded" (bench default): 1 warm-up + 2 timed steps at micro-batch 2 and 1 + 1 at micro-batch 8
-    (~1 min on the box's 16-CPU share; the reported value is the B = 8 rate, the reference's batch)."""
+    protocol "bounded" (bench default): 1 warm-up + 2 timed steps at micro-batch 2 and 1 + 3 at micro-batch 8
+    (~1.5 min on the box's 16-CPU share; the reported value is the B = 8 rate, the reference's batch). The full
+    protocol's result is committed under profiles/ (bench.py --cpu-only --cpu-protocol full)."""
     from oracle import rawboost as orb
     from oracle.data import pad_random
     from oracle.model import OracleModel
@@ -295,7 +296,7 @@ def cpu_baseline(config, threads, protocol):
             opt.step()
             opt.zero_grad()
 
-    plan = [(2, 3, 10), (8, 3, 10)] if protocol == "full" else [(2, 1, 2), (8, 1, 1)]
+    plan = [(2, 3, 10), (8, 3, 10)] if protocol == "full" else [(2, 1, 2), (8, 1, 3)]
     runs = []
     for B, warm, timed in plan:
         for i in range(warm):
