@@ -74,7 +74,7 @@ class Heartbeat:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)   # ~1.5 s of GPU work; 5 steps read +-1 %
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--micro-batch", type=int, default=8)
     ap.add_argument("--accum", type=int, default=4)
