@@ -139,10 +139,14 @@ def test_cli_train_eval_and_2021(tmp_path, golden):
     os.environ.pop("WORLD_SIZE", None)
 
 
-def test_cli_full_resume_equals_continuous(tmp_path, golden):
+@pytest.mark.parametrize("amp", ["bf16", "fp16"])
+def test_cli_full_resume_equals_continuous(tmp_path, golden, amp):
     """Two epochs in one run vs one epoch, then --resume from train_state_epoch_000.pt in a new run: the
     second epoch's weights, EMA/SWA files and dev scores agree (up to the GPU's atomic-accumulation
-    order, far below any training step's effect)."""
+    order, far below any training step's effect). fp16 (the default: GradScaler state resumed too): a weight whose
+    gradient is ~0 moves by ~lr * sign(g) either way, and fp16 rounding flips such signs more often than bf16's
+    fixed-order paths do, so there the bound is on the whole model (5 % of its movement) with a loose per-tensor
+    check; a lost optimizer / scaler / RNG state moves it by as much as the epoch itself."""
     import main as cli
     db = tmp_path / "LA"
     _database(db, golden)
@@ -151,28 +155,33 @@ def test_cli_full_resume_equals_continuous(tmp_path, golden):
     conf.write_text(json.dumps(cfg, indent=2))
     out = tmp_path / "exp"
     cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--save_train_state",
-                             "--comment", "cont"]))
+                             "--comment", "cont", "--amp", amp]))
     cont = out / "LA_Tiny_ep2_bs2_cont"
     state0 = cont / "weights" / "train_state_epoch_000.pt"
     assert state0.exists() and (cont / "weights" / "train_state_epoch_001.pt").exists()
     cli.main(cli.parse_args(["--config", str(conf), "--output_dir", str(out), "--resume", str(state0),
-                             "--comment", "res"]))
+                             "--comment", "res", "--amp", amp]))
     res = out / "LA_Tiny_ep2_bs2_res"
     # Tensor-wise L2 distance, judged against how far the second epoch moved each tensor: the runs are not
     # bitwise reproducible (fp32 atomics in the LoRA and scan gradient kernels; AdamW's first steps move a
     # weight by ~lr * sign(g), so an element whose gradient is ~0 can move either way), while a lost
     # optimizer / scheduler / RNG state would put the resumed epoch's update elsewhere entirely.
     w0 = torch.load(state0, weights_only=True, map_location="cpu")["model"]
+    per = 0.05 if amp == "bf16" else 0.75
     for f in ("checkpoint_epoch_001.pth", "swa.pth", "best.pth"):
         a = torch.load(cont / "weights" / f, weights_only=True, map_location="cpu")
         b = torch.load(res / "weights" / f, weights_only=True, map_location="cpu")
         assert a.keys() == b.keys()
+        d2 = m2 = 0.0
         for k in a:
             x, y = a[k].double(), b[k].double()
             moved = float((x - w0[k].double()).norm()) if k in w0 else float(x.norm())
             d = float((x - y).norm())
-            assert d <= 0.05 * moved + 1e-4 * float(x.norm()) + 1e-12, (f, k, d, moved)
+            assert d <= per * moved + 1e-4 * float(x.norm()) + 1e-12, (f, k, d, moved)
+            if k in w0 and a[k].is_floating_point():
+                d2, m2 = d2 + d * d, m2 + moved * moved
+        assert d2 <= 0.05 ** 2 * m2 + 1e-24, (f, d2 ** 0.5, m2 ** 0.5)
     sa = [float(ln.split()[3]) for ln in (cont / "metrics" / "dev_score.txt").read_text().splitlines()]
     sb = [float(ln.split()[3]) for ln in (res / "metrics" / "dev_score.txt").read_text().splitlines()]
-    np.testing.assert_allclose(sb, sa, rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(sb, sa, rtol=1e-3 if amp == "bf16" else 1e-2, atol=1e-4 if amp == "bf16" else 1e-3)
     os.environ.pop("WORLD_SIZE", None)
