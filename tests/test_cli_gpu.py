@@ -177,7 +177,10 @@ def test_cli_full_resume_equals_continuous(tmp_path, golden, amp):
             x, y = a[k].double(), b[k].double()
             moved = float((x - w0[k].double()).norm()) if k in w0 else float(x.norm())
             d = float((x - y).norm())
-            assert d <= per * moved + 1e-4 * float(x.norm()) + 1e-12, (f, k, d, moved)
+            # attention_pool.bias is one scalar added to every score of a softmax over time: its gradient is zero
+            # up to rounding, so AdamW moves it by lr * sign(noise) either way (whole-model check below only)
+            if k != "attention_pool.bias":
+                assert d <= per * moved + 1e-4 * float(x.norm()) + 1e-12, (f, k, d, moved)
             if k in w0 and a[k].is_floating_point():
                 d2, m2 = d2 + d * d, m2 + moved * moved
         assert d2 <= 0.05 ** 2 * m2 + 1e-24, (f, d2 ** 0.5, m2 ** 0.5)
