@@ -119,35 +119,49 @@ __global__ __launch_bounds__(256, 2) void sincconv_mfma_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t p0 = (int64_t)blockIdx.x * SM_RANGE;
   const float* xb = x + (int64_t)b * len;
-  // 8 shifted copies: xc[s][i] = x[p0 + i + s] (0 past the utterance), 8 samples (16 bytes) per store
-  for (int q = tid; q < 8 * (SM_XW / 8); q += 256) {
-    const int s = q / (SM_XW / 8), i0 = (q - s * (SM_XW / 8)) * 8;
-    h16x8 v;
+  // 8 shifted copies: xc[s][i] = x[p0 + i + s] (0 past the utterance). A thread owns one 8-sample group i0 of every
+  // copy: it reads the 15 samples p0 + i0 .. + 14 once (float4 loads when aligned) and writes 8 16-byte vectors
+  const bool al16 = ((reinterpret_cast<uintptr_t>(xb) | (uintptr_t)(p0 * 4)) & 15) == 0;
+  for (int g = tid; g < SM_XW / 8; g += 256) {
+    const int64_t base = p0 + 8 * g;
+    float v[16];
+    if (al16 && base + 16 <= len) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t g = p0 + i0 + s + j;
-      v[j] = (_Float16)(g < len ? xb[g] : 0.f);
+      for (int q = 0; q < 4; ++q) {
+        const float4 t = *reinterpret_cast<const float4*>(xb + base + 4 * q);
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = base + j < len ? xb[base + j] : 0.f;
     }
-    *reinterpret_cast<h16x8*>(xc + s * SM_XW + i0) = v;
+#pragma unroll
+    for (int sft = 0; sft < 8; ++sft) {
+      h16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (_Float16)v[sft + j];
+      *reinterpret_cast<h16x8*>(xc + sft * SM_XW + 8 * g) = o;
+    }
   }
-  // the filter bank as A fragments: lane (row = lane & 15, kq = lane >> 4) holds W[16 cf + row][32 ks + 8 kq + j]
+  // the filter bank, rounded to f16 and zero-padded to [80][SM_KP], staged once per block in the s_c region
+  // (coalesced along the taps), then read as A fragments: lane (row = lane & 15, kq = lane >> 4) holds
+  // W[16 cf + row][32 ks + 8 kq + j], one 16-byte LDS read each
+  _Float16* bank = reinterpret_cast<_Float16*>(s_c);
+  for (int q = tid; q < 16 * SM_CF * SM_KP; q += 256) {
+    const int c = q / SM_KP, k = q - c * SM_KP;
+    bank[q] = (_Float16)((c < channels && k < K) ? filters[(int64_t)c * K + k] : 0.f);
+  }
+  __syncthreads();
   h16x8 wf[SM_CF][5];
   {
     const int row = lane & 15, kq = lane >> 4;
 #pragma unroll
-    for (int cf = 0; cf < SM_CF; ++cf) {
-      const int c = 16 * cf + row;
+    for (int cf = 0; cf < SM_CF; ++cf)
 #pragma unroll
-      for (int ks = 0; ks < 5; ++ks) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 32 * ks + 8 * kq + j;
-          wf[cf][ks][j] = (_Float16)((c < channels && k < K) ? filters[(int64_t)c * K + k] : 0.f);
-        }
-      }
-    }
+      for (int ks = 0; ks < 5; ++ks)
+        wf[cf][ks] = *reinterpret_cast<const h16x8*>(bank + (16 * cf + row) * SM_KP + 32 * ks + 8 * kq);
   }
-  __syncthreads();
+  __syncthreads();   // the s_c region is the conv image from here on
   float* ob = out + (int64_t)b * C3 * T3;
   const int col = lane & 15, kq = lane >> 4;
   for (int sub = 0; sub < SM_NSUB; ++sub) {
@@ -200,7 +214,8 @@ static int sincconv_mfma_launch(const float* x, int64_t batch, int64_t len, cons
   const int C3 = channels / 3;
   if (T3 <= 0) return RDX_EINVAL;
   if (ksize > SM_KP || channels > 16 * SM_CF) return RDX_EUNSUPPORTED;
-  const size_t smem = (size_t)8 * SM_XW * 2 + (size_t)channels * (SM_SUB + 4) * 4;
+  const size_t img = (size_t)channels * (SM_SUB + 4) * 4, stage = (size_t)16 * SM_CF * SM_KP * 2;   // bank staging
+  const size_t smem = (size_t)8 * SM_XW * 2 + (img > stage ? img : stage);
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sincconv_mfma_kernel),

@@ -174,10 +174,12 @@ def _p(t):
 
 # --------------------------------------------------------------------------------- SincConv ----
 def sinc_mfma_enabled(C, K):
-    """The f16 MFMA SincConv under CUDA autocast (bf16 or fp16: the reference's autocast runs this conv in fp16),
-    for banks of <= 80 channels x 160 taps; RADHIP_SINC_MFMA=0 keeps the fp32 kernel (A/B measurement)."""
-    return (torch.is_autocast_enabled("cuda") and C <= 80 and K <= 160
-            and os.environ.get("RADHIP_SINC_MFMA", "1") != "0")
+    """The f16 MFMA SincConv under CUDA fp16 autocast (the reference's autocast runs this conv in fp16: the same
+    input rounding), for banks of <= 80 channels x 160 taps. bf16 autocast and fp32 keep the fp32 kernel (rounding
+    the conv's inputs to fp16 there would add an error the reference's fp16 run has but a bf16 run has no reason
+    to carry); RADHIP_SINC_MFMA=0 keeps the fp32 kernel everywhere (A/B measurement)."""
+    return (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16
+            and C <= 80 and K <= 160 and os.environ.get("RADHIP_SINC_MFMA", "1") != "0")
 
 
 def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
@@ -193,8 +195,8 @@ def sincconv_absmaxpool(x, filters, mask_lo=0, mask_hi=0, mask_dev=None):
     C, K = filters.shape
     out = torch.empty(B, C // 3, (L - K + 1) // 3, device=x.device, dtype=torch.float32)
     if sinc_mfma_enabled(C, K):
-        # autocast (the training step and bf16 eval): the reference's conv1d runs in fp16 there
-        # (src/main.py:1049) -> the f16 MFMA form; the fp32 paths keep the exact fp32 kernel below
+        # fp16 autocast (the training step, fp16 eval): the reference's conv1d runs in fp16 there
+        # (src/main.py:1049) -> the f16 MFMA form; the other paths keep the exact fp32 kernel below
         per_utt = mask_dev is not None and mask_dev.dim() == 2
         if mask_dev is not None:
             assert mask_dev.dtype == torch.int32 and mask_dev.is_cuda and mask_dev.is_contiguous()

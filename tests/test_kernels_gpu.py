@@ -41,7 +41,7 @@ def test_sincconv_f16_mfma_vs_oracle(mask, L):
     from radhip.ops import sincconv_absmaxpool as hip_sinc
     bank = sinc_filterbank()
     x = seeded_array(f"k.sinc16.{L}", (3, L), scale=0.1).astype(np.float32)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=torch.float16):
         out = hip_sinc(torch.from_numpy(x).to(DEV), bank.to(DEV), *mask).cpu().numpy()
     x16 = x.astype(np.float16).astype(np.float32)
     b16 = bank.numpy().astype(np.float16).astype(np.float32)
@@ -52,9 +52,13 @@ def test_sincconv_f16_mfma_vs_oracle(mask, L):
     assert float(np.abs(out - ref).max()) <= 2e-3 * float(np.abs(ref).max())
     # the per-utterance device mask (the window's graph-replayable form) gives the same rows
     md = torch.tensor([list(mask)] * 3, dtype=torch.int32, device=DEV)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=torch.float16):
         out2 = hip_sinc(torch.from_numpy(x).to(DEV), bank.to(DEV), mask_dev=md).cpu().numpy()
     assert np.array_equal(out, out2)
+    # bf16 autocast keeps the exact fp32 kernel
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out3 = hip_sinc(torch.from_numpy(x).to(DEV), bank.to(DEV), *mask).cpu().numpy()
+    np.testing.assert_allclose(out3, ref, rtol=1e-4, atol=2e-6)
 
 
 def test_sincconv_golden(golden):
