@@ -90,10 +90,11 @@ int rdx_dwconv_bidir_fwd(int dtype, const void* x, int64_t ldx, const float* w, 
                          void* u, int B, int L, int D, int K, int dirs, void* stream);
 /* Backward. du [dirs, B, L, D]; writes dx (row stride lddx, overwritten), and partial weight / bias
  * gradients per (time chunk, batch): dw_part [P, D, K], db_part [P, D] with P = rdx_dwconv_bidir_bwd_parts(L)
- * * B (fp32; caller sums dim 0). */
+ * * B (fp32; caller sums dim 0), rows of ld_part floats (0: dense; D * K + D packs both into one [P][D * K + D]
+ * buffer, db_part = dw_part + D * K, summed with one reduction). */
 int rdx_dwconv_bidir_bwd_parts(int L);
 int rdx_dwconv_bidir_bwd(int dtype, const void* x, int64_t ldx, const float* w, const float* bias,
-                         const void* du, void* dx, int64_t lddx, float* dw_part, float* db_part,
+                         const void* du, void* dx, int64_t lddx, float* dw_part, float* db_part, int64_t ld_part,
                          int B, int L, int D, int K, int dirs, void* stream);
 
 /* Selective scan, replaces selective_scan_cuda.fwd (mamba_ssm) / MambaBlock.ssm_step
@@ -442,7 +443,8 @@ int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
  * 16: per-chunk local states and decay products, then every chunk from its composed carry. Forward: P (the
  * per-chunk decay products, kept for the backward) and hloc are [dirs][B][chunks][D][N] fp32
  * (rdx_scan2_rec_elems). Backward: gloc is a workspace of the same size; dA_part [dirs * B * chunks][D][N],
- * dD_part / dbias_part [dirs * B * chunks][D] (summed by the caller); dBC zeroed by the caller. */
+ * dD_part / dbias_part [dirs * B * chunks][D] (summed by the caller), rows of ld_part floats (0: dense; D * N + 2D
+ * packs the three into one buffer summed with one reduction); dBC zeroed by the caller. */
 int rdx_scan2_chunks(int L);
 int64_t rdx_scan2_rec_elems(int B, int L, int D, int N, int dirs);
 int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm, const void* Cm,
@@ -451,7 +453,8 @@ int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const float* A_lo
 int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm, const void* Cm,
                   int64_t ldbc, const float* Dp, const float* dt_bias, const float* ckpt, const float* P,
                   const float* dy, int64_t dy_dir_stride, void* du, void* ddelta, float* dBC, float* dA_part,
-                  float* dD_part, float* dbias_part, float* gloc, int B, int L, int D, int N, int dirs, void* stream);
+                  float* dD_part, float* dbias_part, int64_t ld_part, float* gloc, int B, int L, int D, int N,
+                  int dirs, void* stream);
 
 /* ---- bf16 MFMA GEMM of the WavLM encoder projections, LDS-DMA pipeline (csrc/wgemm.hip) ---------------
  * Same contract as rdx_gemm_bf16 for the RDX_EPI_BIAS / _BIAS_GELU / _GELU_BWD epilogues, with K % 64 == 0;

@@ -68,7 +68,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void dwconv_bwd_kernel(
     const T* __restrict__ x, int64_t ldx, const float* __restrict__ w, const float* __restrict__ bias,
     const T* __restrict__ du, T* __restrict__ dx, int64_t lddx, float* __restrict__ dw_part,
-    float* __restrict__ db_part, int B, int L, int D, int dirs) {
+    float* __restrict__ db_part, int64_t ldpw, int64_t ldpb, int B, int L, int D, int dirs) {
   __shared__ float red[DWC_SEG][64][DWC_K + 1];
   const int dl = threadIdx.x & 63, seg = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + dl;
@@ -150,8 +150,8 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(
     for (int k = 0; k <= DWC_K; ++k) {
       float s = red[0][dl][k] + red[1][dl][k] + red[2][dl][k] + red[3][dl][k];
       const int64_t pb = (int64_t)blockIdx.z * B + b;
-      if (k < DWC_K) dw_part[(pb * D + d) * DWC_K + k] = s;
-      else db_part[pb * D + d] = s;
+      if (k < DWC_K) dw_part[pb * ldpw + d * DWC_K + k] = s;
+      else db_part[pb * ldpb + d] = s;
     }
   }
 }
@@ -622,15 +622,17 @@ extern "C" int rdx_dwconv_bidir_fwd(int dtype, const void* x, int64_t ldx, const
 
 extern "C" int rdx_dwconv_bidir_bwd(int dtype, const void* x, int64_t ldx, const float* w,
                                     const float* bias, const void* du, void* dx, int64_t lddx,
-                                    float* dw_part, float* db_part, int B, int L, int D, int K,
+                                    float* dw_part, float* db_part, int64_t ld_part, int B, int L, int D, int K,
                                     int dirs, void* stream) {
   RDX_REQUIRE(x && w && bias && du && dx && dw_part && db_part && B > 0 && L > 0 && D > 0);
   RDX_REQUIRE(ldx >= D && lddx >= D && (dirs == 1 || dirs == 2));
+  RDX_REQUIRE(ld_part == 0 || ld_part >= (int64_t)D * K);
   if (K != DWC_K) return RDX_EUNSUPPORTED;
+  const int64_t ldpw = ld_part ? ld_part : (int64_t)D * K, ldpb = ld_part ? ld_part : (int64_t)D;
   dim3 grid((D + 63) / 64, B, (L + DWC_CHUNK - 1) / DWC_CHUNK);
   DISPATCH_DTYPE(dtype, hipLaunchKernelGGL(dwconv_bwd_kernel<T>, grid, dim3(256), 0, as_stream(stream),
                                            (const T*)x, ldx, w, bias, (const T*)du, (T*)dx, lddx, dw_part,
-                                           db_part, B, L, D, dirs));
+                                           db_part, ldpw, ldpb, B, L, D, dirs));
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

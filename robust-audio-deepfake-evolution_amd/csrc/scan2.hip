@@ -235,7 +235,7 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
     const float* __restrict__ ckpt, const float* __restrict__ P, const float* __restrict__ gloc,
     const float* __restrict__ dy, int64_t dy_dir_stride, T* __restrict__ du, T* __restrict__ ddelta,
     float* __restrict__ dBC, float* __restrict__ dA_part, float* __restrict__ dD_part, float* __restrict__ dbias_part,
-    int B, int L, int D) {
+    int64_t ldpa, int64_t ldpd, int B, int L, int D) {
   __shared__ float s_u[CK * CH], s_dt[CK * CH], s_dy[CK * CH], s_sig[CK * CH], s_B[CK * N], s_C[CK * N];
   __shared__ float s_red[CK][8][2 * N];     // [step][wave][dB 16 | dC 16]
   const Geo g = geo(B, L, D);
@@ -327,10 +327,11 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
       atomicAdd(&dBC[((int64_t)g.db * L + tstep(g, i, L)) * (2 * N) + j], v);
     }
   }
-  if (g.active) dA_part[rec(g, g.c, D)] = dA * Aval;   // d/dA_log = dL/dA * A
+  const int64_t part = (int64_t)g.db * g.nc + g.c;
+  if (g.active) dA_part[part * ldpa + g.d * N + g.n] = dA * Aval;   // d/dA_log = dL/dA * A
   if (g.active && g.n == 0) {
-    dD_part[((int64_t)g.db * g.nc + g.c) * D + g.d] = dDacc;
-    dbias_part[((int64_t)g.db * g.nc + g.c) * D + g.d] = dbacc;
+    dD_part[part * ldpd + g.d] = dDacc;
+    dbias_part[part * ldpd + g.d] = dbacc;
   }
   __syncthreads();
   {
@@ -384,17 +385,21 @@ extern "C" int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const 
   return RDX_OK;
 }
 
-// dA_part [dirs * B * NC][D][N], dD_part / dbias_part [dirs * B * NC][D] (NC = rdx_scan2_chunks(L)); gloc is a
-// workspace of rdx_scan2_rec_elems floats; dBC [dirs][B][L][2N] zeroed by the caller.
+// dA_part [dirs * B * NC][D][N], dD_part / dbias_part [dirs * B * NC][D] (NC = rdx_scan2_chunks(L)), rows of
+// ld_part floats (0: dense, D * N for dA and D for dD / dbias; the caller may pack the three into one [parts][D * N +
+// 2D] buffer, ld_part = D * N + 2D, and sum them with one reduction); gloc is a workspace of rdx_scan2_rec_elems
+// floats; dBC [dirs][B][L][2N] zeroed by the caller.
 extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm,
                              const void* Cm, int64_t ldbc, const float* Dp, const float* dt_bias, const float* ckpt,
                              const float* P, const float* dy, int64_t dy_dir_stride, void* du, void* ddelta,
-                             float* dBC, float* dA_part, float* dD_part, float* dbias_part, float* gloc, int B, int L,
-                             int D, int N, int dirs, void* stream) {
+                             float* dBC, float* dA_part, float* dD_part, float* dbias_part, int64_t ld_part,
+                             float* gloc, int B, int L, int D, int N, int dirs, void* stream) {
   RDX_REQUIRE(u && delta && A_log && Bm && Cm && Dp && dt_bias && ckpt && P && dy && du && ddelta && dBC);
   RDX_REQUIRE(dA_part && dD_part && dbias_part && gloc);
   RDX_REQUIRE(B > 0 && L > 0 && D > 0 && (dirs == 1 || dirs == 2) && ldbc >= N && dy_dir_stride >= 0);
+  RDX_REQUIRE(ld_part == 0 || ld_part >= (int64_t)D * N);
   if (N != s2::N) return RDX_EUNSUPPORTED;
+  const int64_t ldpa = ld_part ? ld_part : (int64_t)D * N, ldpd = ld_part ? ld_part : (int64_t)D;
   const dim3 grid((D + s2::CH - 1) / s2::CH, rdx_scan2_chunks(L), dirs * B);
   hipStream_t st = as_stream(stream);
   if (dtype == RDX_BF16) {
@@ -404,7 +409,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
     RDX_LAUNCH_CHECK();
     hipLaunchKernelGGL(s2::bwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, P, gloc, dy, dy_dir_stride, (T*)du,
-                       (T*)ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D);
+                       (T*)ddelta, dBC, dA_part, dD_part, dbias_part, ldpa, ldpd, B, L, D);
   } else if (dtype == RDX_F32) {
     using T = float;
     hipLaunchKernelGGL(s2::bwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)delta, A_log, (const T*)Cm,
@@ -412,7 +417,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
     RDX_LAUNCH_CHECK();
     hipLaunchKernelGGL(s2::bwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, P, gloc, dy, dy_dir_stride, (T*)du,
-                       (T*)ddelta, dBC, dA_part, dD_part, dbias_part, B, L, D);
+                       (T*)ddelta, dBC, dA_part, dD_part, dbias_part, ldpa, ldpd, B, L, D);
   } else {
     return RDX_EINVAL;
   }

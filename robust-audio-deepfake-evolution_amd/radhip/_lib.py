@@ -67,7 +67,7 @@ SIGNATURES = {
                                                     c_vp]),
     "rdx_dwconv_bidir_fwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_dwconv_bidir_bwd_parts": (c_int, [c_int]),
-    "rdx_dwconv_bidir_bwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+    "rdx_dwconv_bidir_bwd": (c_int, [c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                      c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_scan_ckpt_elems": (c_i64, [c_int, c_int, c_int, c_int, c_int]),
     "rdx_scan_nblk_d": (c_int, [c_int]),
@@ -119,7 +119,8 @@ SIGNATURES = {
     "rdx_scan2_chunks": (c_int, [c_int]),
     "rdx_scan2_rec_elems": (c_i64, [c_int, c_int, c_int, c_int, c_int]),
     "rdx_scan2_fwd": (c_int, [c_int] + [c_vp] * 5 + [c_i64] + [c_vp] * 6 + [c_int] * 5 + [c_vp]),
-    "rdx_scan2_bwd": (c_int, [c_int] + [c_vp] * 5 + [c_i64] + [c_vp] * 5 + [c_i64] + [c_vp] * 7 + [c_int] * 5 + [c_vp]),
+    "rdx_scan2_bwd": (c_int, [c_int] + [c_vp] * 5 + [c_i64] + [c_vp] * 5 + [c_i64] + [c_vp] * 6 + [c_i64, c_vp]
+                      + [c_int] * 5 + [c_vp]),
     "rdx_pgemm_bf16": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64,
                                c_vp, c_i64, c_int, c_int, c_vp]),
     "rdx_pgemm_prof": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp,

@@ -275,12 +275,14 @@ class DWConvBidir(torch.autograd.Function):
         du = du.contiguous().to(x.dtype)
         dx = torch.empty(B, L, D, device=x.device, dtype=x.dtype)
         parts = lib().rdx_dwconv_bidir_bwd_parts(L) * B
-        dw_part = torch.empty(parts, D, K, device=x.device, dtype=torch.float32)
-        db_part = torch.empty(parts, D, device=x.device, dtype=torch.float32)
+        # weight and bias partials packed into one [parts][D*K + D] buffer: one reduction launch for both
+        part = torch.empty(parts, D * K + D, device=x.device, dtype=torch.float32)
         check(_L(x).rdx_dwconv_bidir_bwd(_dtype_code(x), _p(x), _rowview_ld(x), _p(w), _p(b), _p(du), _p(dx), D,
-                                         _p(dw_part), _p(db_part), B, L, D, K, ctx.dirs, _stream(x)),
+                                         _p(part), ctypes.c_void_p(part.data_ptr() + 4 * D * K), D * K + D,
+                                         B, L, D, K, ctx.dirs, _stream(x)),
               "dwconv_bidir_bwd")
-        return dx, dw_part.sum(0).view(ctx.wshape), db_part.sum(0), None
+        tot = part.sum(0)
+        return dx, tot[:D * K].view(ctx.wshape), tot[D * K:], None
 
 
 def scan2_enabled():
@@ -345,19 +347,30 @@ class SelectiveScan(torch.autograd.Function):
         du = torch.empty_like(u)
         ddelta = torch.empty_like(u)
         dBC = torch.zeros(dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)  # accumulated atomically
-        parts = dirs * B * (int(lib().rdx_scan2_chunks(L)) if ctx.chunked else 1)
-        dA = torch.empty(parts, D, N, device=u.device, dtype=torch.float32)
-        dD = torch.empty(parts, D, device=u.device, dtype=torch.float32)
-        dbias = torch.empty(parts, D, device=u.device, dtype=torch.float32)
         es = u.element_size()
         if ctx.chunked:
+            # dA_log / D / dt_bias partials of every (dir, b, chunk) packed into one [parts][D*N + 2D] buffer:
+            # one reduction launch for the three
+            parts = dirs * B * int(lib().rdx_scan2_chunks(L))
+            part = torch.empty(parts, D * N + 2 * D, device=u.device, dtype=torch.float32)
+            base = part.data_ptr()
             gloc = torch.empty(int(lib().rdx_scan2_rec_elems(B, L, D, N, dirs)), device=u.device, dtype=torch.float32)
             with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
                 check(_L(u).rdx_scan2_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm), ctx.ldbc,
                                           _p(Dp), _p(dt_bias), _p(ck), _p(P), _p(dy), dy_stride, _p(du), _p(ddelta),
-                                          _p(dBC), _p(dA), _p(dD), _p(dbias), _p(gloc), B, L, D, N, dirs, _stream(u)),
+                                          _p(dBC), ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * D * N),
+                                          ctypes.c_void_p(base + 4 * (D * N + D)), D * N + 2 * D, _p(gloc), B, L, D,
+                                          N, dirs, _stream(u)),
                       "scan2_bwd")
+            tot = part.sum(0)
+            dBC = dBC.to(Bm.dtype)
+            return (du, ddelta, tot[:D * N].view(D, N), dBC[..., :N], dBC[..., N:], tot[D * N:D * N + D],
+                    tot[D * N + D:])
         else:
+            parts = dirs * B
+            dA = torch.empty(parts, D, N, device=u.device, dtype=torch.float32)
+            dD = torch.empty(parts, D, device=u.device, dtype=torch.float32)
+            dbias = torch.empty(parts, D, device=u.device, dtype=torch.float32)
             with _timed("selective_scan_bwd", u, dirs * B * L * (D * (4 * es + 4) + 2 * N * es)):
                 check(_L(u).rdx_selective_scan_bwd(_dtype_code(u), _p(u), _p(delta), _p(A_log), _p(Bm), _p(Cm),
                                                    ctx.ldbc, _p(Dp), _p(dt_bias), _p(ck), _p(dy), dy_stride, _p(du),
