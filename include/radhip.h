@@ -160,6 +160,10 @@ int rdx_layer_wsum_fwd(int dtype, int nl, const void* const* hs, const float* w,
 int rdx_layer_wsum_nblk(int64_t n);
 int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, const float* w, const void* g,
                        void* const* dhs, float* dot_part, int64_t n, void* stream);
+/* fp32 -> the library's 16-bit type (bf16 / fp16) of n <= 64 tensors in one launch: dst[k][i] = src[k][i] for
+ * i < numel[k] (round to nearest even). The accumulation window casts the detector head's fp32 linear weights to the
+ * autocast dtype once per window with it (radhip/window.py; autocast's own cast cache: one launch per tensor). */
+int rdx_cast_f32_many(int n, const float* const* src, void* const* dst, const int64_t* numel, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * RawBoost, batched over utterances with host-drawn parameters. Replaces RawBoost.process and
@@ -444,7 +448,8 @@ int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
  * per-chunk decay products, kept for the backward) and hloc are [dirs][B][chunks][D][N] fp32
  * (rdx_scan2_rec_elems). Backward: gloc is a workspace of the same size; dA_part [dirs * B * chunks][D][N],
  * dD_part / dbias_part [dirs * B * chunks][D] (summed by the caller), rows of ld_part floats (0: dense; D * N + 2D
- * packs the three into one buffer summed with one reduction); dBC zeroed by the caller. */
+ * packs the three into one buffer summed with one reduction); dBC [dirs][B][L][2N] fp32 is zeroed and accumulated
+ * by the call. */
 int rdx_scan2_chunks(int L);
 int64_t rdx_scan2_rec_elems(int B, int L, int D, int N, int dirs);
 int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm, const void* Cm,

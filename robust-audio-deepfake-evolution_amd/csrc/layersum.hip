@@ -189,3 +189,41 @@ extern "C" int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, cons
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
+
+// ---- fp32 -> 16-bit casts of up to RDX_CAST_MAX tensors in one launch (the window's per-window cast of the
+// detector head's fp32 weights to the autocast dtype, radhip/window.py: one launch instead of one per tensor)
+constexpr int RDX_CAST_MAX = 64;
+struct CastTable {
+  const float* src[RDX_CAST_MAX];
+  hst* dst[RDX_CAST_MAX];
+  int64_t n[RDX_CAST_MAX];
+};
+
+__global__ __launch_bounds__(256) void cast_many_kernel(CastTable t) {
+  const int k = blockIdx.y;
+  const float* __restrict__ s = t.src[k];
+  hst* __restrict__ d = t.dst[k];
+  const int64_t n = t.n[k];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) d[i] = f2h(s[i]);
+}
+
+extern "C" int rdx_cast_f32_many(int n, const float* const* src, void* const* dst, const int64_t* numel,
+                                 void* stream) {
+  RDX_REQUIRE(n >= 0 && (n == 0 || (src && dst && numel)));
+  if (n > RDX_CAST_MAX) return RDX_EUNSUPPORTED;
+  if (n == 0) return RDX_OK;
+  CastTable t{};
+  int64_t mx = 1;
+  for (int k = 0; k < n; ++k) {
+    RDX_REQUIRE(src[k] && dst[k] && numel[k] >= 0);
+    t.src[k] = src[k];
+    t.dst[k] = reinterpret_cast<hst*>(dst[k]);
+    t.n[k] = numel[k];
+    mx = numel[k] > mx ? numel[k] : mx;
+  }
+  const int64_t bx = (mx + 255) / 256;
+  hipLaunchKernelGGL(cast_many_kernel, dim3((unsigned)(bx < 64 ? bx : 64), (unsigned)n), dim3(256), 0,
+                     as_stream(stream), t);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}

@@ -25,6 +25,7 @@ constexpr int N = 16;            // d_state
 constexpr int CK = 16;           // steps per chunk (== SCAN_CK of bimamba.hip: same checkpoints)
 constexpr int CH = 32;           // channels per block
 constexpr int NT = CH * N;       // 512 threads
+static_assert(NT == CK * 2 * N, "bwd 1 zeroes a chunk's dBC rows with one thread per element");
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct Geo {
@@ -184,15 +185,21 @@ __global__ __launch_bounds__(NT) void fwd_out_kernel(const T* __restrict__ u, co
   }
 }
 
-// ---- bwd 1: chunk-local reverse carry (G from 0 at the chunk end): gloc = a_{s0} G_{s0}
+// ---- bwd 1: chunk-local reverse carry (G from 0 at the chunk end): gloc = a_{s0} G_{s0}; the first channel group's
+// blocks also zero their chunk's rows of dBC, which bwd 2 accumulates into (no separate fill launch)
 template <typename T>
 __global__ __launch_bounds__(NT) void bwd_chunk_kernel(const T* __restrict__ delta, const float* __restrict__ A_log,
                                                        const T* __restrict__ Cm, int64_t ldbc,
                                                        const float* __restrict__ dt_bias,
                                                        const float* __restrict__ dy, int64_t dy_dir_stride,
-                                                       float* __restrict__ gloc, int B, int L, int D) {
+                                                       float* __restrict__ gloc, float* __restrict__ dBC, int B, int L,
+                                                       int D) {
   __shared__ float s_dt[CK * CH], s_dy[CK * CH], s_C[CK * N];
   const Geo g = geo(B, L, D);
+  if (blockIdx.x == 0) {
+    const int i = threadIdx.x >> 5, j = threadIdx.x & 31;   // NT = CK * 2N: one (step, dB|dC column) per thread
+    if (i < g.cnt) dBC[((int64_t)g.db * L + tstep(g, i, L)) * (2 * N) + j] = 0.f;
+  }
   {
     const int tid = threadIdx.x, i = tid >> 5, c = tid & 31, dd = g.d0 + c;
     float dv = 0.f, dyv = 0.f;
@@ -388,7 +395,7 @@ extern "C" int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const 
 // dA_part [dirs * B * NC][D][N], dD_part / dbias_part [dirs * B * NC][D] (NC = rdx_scan2_chunks(L)), rows of
 // ld_part floats (0: dense, D * N for dA and D for dD / dbias; the caller may pack the three into one [parts][D * N +
 // 2D] buffer, ld_part = D * N + 2D, and sum them with one reduction); gloc is a workspace of rdx_scan2_rec_elems
-// floats; dBC [dirs][B][L][2N] zeroed by the caller.
+// floats; dBC [dirs][B][L][2N] is zeroed here (by the first kernel) and accumulated by the second.
 extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const float* A_log, const void* Bm,
                              const void* Cm, int64_t ldbc, const float* Dp, const float* dt_bias, const float* ckpt,
                              const float* P, const float* dy, int64_t dy_dir_stride, void* du, void* ddelta,
@@ -405,7 +412,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
   if (dtype == RDX_BF16) {
     using T = hst;
     hipLaunchKernelGGL(s2::bwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)delta, A_log, (const T*)Cm,
-                       ldbc, dt_bias, dy, dy_dir_stride, gloc, B, L, D);
+                       ldbc, dt_bias, dy, dy_dir_stride, gloc, dBC, B, L, D);
     RDX_LAUNCH_CHECK();
     hipLaunchKernelGGL(s2::bwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, P, gloc, dy, dy_dir_stride, (T*)du,
@@ -413,7 +420,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
   } else if (dtype == RDX_F32) {
     using T = float;
     hipLaunchKernelGGL(s2::bwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)delta, A_log, (const T*)Cm,
-                       ldbc, dt_bias, dy, dy_dir_stride, gloc, B, L, D);
+                       ldbc, dt_bias, dy, dy_dir_stride, gloc, dBC, B, L, D);
     RDX_LAUNCH_CHECK();
     hipLaunchKernelGGL(s2::bwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, P, gloc, dy, dy_dir_stride, (T*)du,

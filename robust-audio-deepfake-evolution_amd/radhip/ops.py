@@ -346,7 +346,8 @@ class SelectiveScan(torch.autograd.Function):
             dy_stride = B * L * D
         du = torch.empty_like(u)
         ddelta = torch.empty_like(u)
-        dBC = torch.zeros(dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)  # accumulated atomically
+        # dB | dC, accumulated atomically: scan2 zeroes it itself, the segmented kernels need it zeroed
+        dBC = (torch.empty if ctx.chunked else torch.zeros)(dirs, B, L, 2 * N, device=u.device, dtype=torch.float32)
         es = u.element_size()
         if ctx.chunked:
             # dA_log / D / dt_bias partials of every (dir, b, chunk) packed into one [parts][D*N + 2D] buffer:
@@ -527,6 +528,27 @@ def mixup_focal(logits, ya, yb, lam, rows_per_lam, focal, divisor):
     scale = 1.0 / (rows_per_lam * (C if mode == 0 else 1) * divisor)
     alpha = -1.0 if focal.alpha is None else float(focal.alpha)
     return MixupFocal.apply(logits, ya, yb, lam, rows_per_lam, alpha, float(focal.gamma), mode, scale)
+
+
+# --------------------------------------------------------------------------- multi-tensor cast ----
+def cast_many(srcs, dsts):
+    """dsts[k] = srcs[k] rounded to the dsts' 16-bit dtype (bf16 or fp16), fp32 contiguous sources, one launch per
+    64 tensors (csrc/layersum.hip rdx_cast_f32_many)."""
+    if not srcs:
+        return
+    dt = dsts[0].dtype
+    if dt not in HALF or len(srcs) != len(dsts):
+        raise ValueError("radhip cast_many: 16-bit destinations, one per source")
+    for a, b in zip(srcs, dsts):
+        if (a.dtype != torch.float32 or b.dtype != dt or a.numel() != b.numel() or not a.is_contiguous()
+                or not b.is_contiguous() or not a.is_cuda or a.device != b.device):
+            raise ValueError("radhip cast_many: contiguous fp32 -> 16-bit tensors of equal size on one device")
+    for i in range(0, len(srcs), 64):
+        s, d = srcs[i:i + 64], dsts[i:i + 64]
+        check(_L(dt).rdx_cast_f32_many(len(s), ptr_array([t.data_ptr() for t in s]),
+                                       ptr_array([t.data_ptr() for t in d]),
+                                       (ctypes.c_int64 * len(s))(*[t.numel() for t in s]), _stream(s[0])),
+              "cast_f32_many")
 
 
 # ------------------------------------------------------------------------------------ FGM ----

@@ -108,6 +108,12 @@ class WindowStep:
         self.ring = _PinnedRing(8192 + 2 * N * 8 + N * (T + nl + 16) + self.K * (self.B * T + nl + 64))
         self.graphs = None
         self._wcache = {}
+        # the detector head's fp32 linear parameters (radhip.linear.SideLinear), cast to the autocast dtype once per
+        # window by ONE launch into persistent buffers (_precast_linears) instead of one cast per tensor
+        from .linear import SideLinear
+        self._lin_src = [p for mod in m.modules() if isinstance(mod, SideLinear)
+                         for p in (mod.weight, mod.bias) if p is not None and p.dtype == torch.float32]
+        self._lin_dst = None
         self.chain_captured = False
         self.feats = None
         self._host = None
@@ -215,9 +221,22 @@ class WindowStep:
             for p, v in zip(self.handed, views):
                 p.grad = v
 
+    def _precast_linears(self):
+        """Fill the window's weight-cast cache (radhip.linear._cast) for every SideLinear parameter with one
+        multi-tensor launch (ops.cast_many); the parameters do not change within a window."""
+        dt = self.tr.amp_dtype
+        if dt not in ops.HALF or not self._lin_src or not self._lin_src[0].is_cuda:
+            return
+        if self._lin_dst is None or self._lin_dst[0].dtype != dt:
+            self._lin_dst = [torch.empty_like(p, dtype=dt) for p in self._lin_src]
+        ops.cast_many([p.detach() for p in self._lin_src], self._lin_dst)
+        for p, c in zip(self._lin_src, self._lin_dst):
+            self._wcache[("lin", id(p))] = (p, c)
+
     def _clean_pass(self):
         self._wcache = {}                  # weight layouts prepared by this pass, reused by the window's others
         ops.SCONV_WCACHE = self._wcache
+        self._precast_linears()
         self._pass_grads(self._clean_pass_body)
 
     def _sinc_adv_forward(self):

@@ -264,3 +264,17 @@ def test_f16_sincnet_block0_fused_vs_fp32():
     e8 = {k: _rel(r8[k], ref[k]) for k in ref}
     assert e16["y"] < 2e-3 and max(e16.values()) < 5e-2, e16
     assert e8["y"] > GAIN * e16["y"], (e8, e16)
+
+
+# ------------------------------------------------------------------------------ multi-tensor cast ----
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_cast_many_equals_to(dt):
+    """rdx_cast_f32_many (the window's per-window weight cast) == tensor.to(dt) bit for bit, over more than one
+    64-tensor launch and ragged sizes (including an empty tensor)."""
+    from radhip import ops
+    torch.manual_seed(0)
+    srcs = [torch.randn(n, device=DEV) * 10 ** (k % 5 - 2) for k, n in enumerate([0, 1, 7, 255, 256, 257, 83000] * 10)]
+    dsts = [torch.empty_like(s, dtype=dt) for s in srcs]
+    ops.cast_many(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(d, s.to(dt))
