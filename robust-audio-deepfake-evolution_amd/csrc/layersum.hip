@@ -215,7 +215,7 @@ extern "C" int rdx_cast_f32_many(int n, const float* const* src, void* const* ds
   CastTable t{};
   int64_t mx = 1;
   for (int k = 0; k < n; ++k) {
-    RDX_REQUIRE(src[k] && dst[k] && numel[k] >= 0);
+    RDX_REQUIRE(numel[k] >= 0 && (numel[k] == 0 || (src[k] && dst[k])));   // an empty tensor may be null
     t.src[k] = src[k];
     t.dst[k] = reinterpret_cast<hst*>(dst[k]);
     t.n[k] = numel[k];

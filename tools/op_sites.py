@@ -1,5 +1,6 @@
 """Diagnostics: which source lines issue the dtype casts / elementwise ops of one Phase-6 micro-step
-(bf16 autocast, full-size model, B=2), and which SDPA backend the WavLM attention takes."""
+(autocast dtype from AMP=fp16|bf16, default fp16 as bench.py; full-size model, B=2), and which SDPA backend the
+WavLM attention takes."""
 import collections
 import os
 import sys
@@ -37,6 +38,9 @@ class Sites(TorchDispatchMode):
         return out
 
 
+AMP = {"fp16": torch.float16, "bf16": torch.bfloat16}[os.environ.get("AMP", "fp16")]
+
+
 def main():
     dev = torch.device("cuda", 0)
     cfg = load_config("Phase6_Proposed.conf")
@@ -47,13 +51,13 @@ def main():
     x = torch.randn(2, 64600, device=dev) * 0.1
     y = torch.tensor([0, 1], device=dev)
     for _ in range(2):
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=AMP):
             _, out = m(x)
             loss = torch.nn.functional.cross_entropy(out.float(), y)
         loss.backward()
     torch.cuda.synchronize()
     with Sites() as s:
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=AMP):
             _, out = m(x)
             loss = torch.nn.functional.cross_entropy(out.float(), y)
         loss.backward()
