@@ -169,7 +169,8 @@ def roofline_from_rows(rows, steps, graphed=False, split=False):
                           "second capture of the window with these stamps and the SincNet branch serialized on the "
                           "main stream (the timed region replays unstamped graphs with the branch concurrent)"
                           if split else " of the timed region")
-                       + "; HIP events on the launch stream for eager launches") if graphed else
+                       + "; each stamped launch minus the average of one empty stamp pair per graph (the stamps' own "
+                         "cost, `stamp_overhead_us`); HIP events on the launch stream for eager launches") if graphed else
                       "HIP events on the launch stream around every launch of the timed region"}
     return roof, rows
 
@@ -497,6 +498,9 @@ def main():
     wall_max = float(t.item())
     loss = trainer.epoch_loss()
     roof, rows = roofline_from_rows(rows, args.steps, graphed=not args.eager, split=split)
+    if graph_timer is not None and roof is not None:
+        khz = ops.lib().rdx_wallclock_khz(dev.index or 0)
+        roof["stamp_overhead_us"] = round(graph_timer.overhead_ticks() / khz * 1e3, 3) if khz > 0 else None
     utts = ws * args.steps * args.accum * B
     value = utts / wall_max
     if rank == 0:

@@ -60,10 +60,30 @@ class GraphTimer:
         self.sites = []                       # (name, work, group) per slot
         self.per_graph = per_graph
         self._in_graph = {}                   # name -> group record {"total", "sampled"} of this graph
+        # one empty bracket (two back-to-back stamps) per graph: the stamps' own cost, subtracted from every
+        # bracketed launch in rows() (a bracket holds the opening stamp kernel and the launch gaps around the kernel)
+        self.calib = torch.zeros(64, 2, dtype=torch.int64, device=self.device)
+        self._ncalib = 0
 
     def new_graph(self):
         """Call before capturing each graph."""
         self._in_graph = {}
+
+    def calibrate(self, t):
+        """Inside a capture: the graph's empty bracket, once per graph (before its first stamped launch)."""
+        if self._in_graph.get("__calib__") or self._ncalib >= self.calib.shape[0]:
+            return
+        self._in_graph["__calib__"] = True
+        site = self.calib[self._ncalib]
+        self._ncalib += 1
+        check(lib().rdx_timestamp_acc(_p(site), -1, _stream(t)), "timestamp")
+        check(lib().rdx_timestamp_acc(_p(site), 1, _stream(t)), "timestamp")
+
+    def overhead_ticks(self):
+        """Average ticks of an empty bracket (0 before any calibrated replay)."""
+        c = self.calib[:self._ncalib].cpu().numpy()
+        n = int(c[:, 1].sum()) if len(c) else 0
+        return float(c[:, 0].sum()) / n if n else 0.0
 
     def slot(self, name, work, shape=None):
         """shape: an extra key for kernels whose launch sites differ in size within one graph (the SincNet
@@ -80,6 +100,7 @@ class GraphTimer:
 
     def reset(self):
         self.acc.zero_()
+        self.calib.zero_()
 
     def rows(self, by_shape=False):
         """{name: {launches, total_ms, avg_ms, avg_work, sampled_launches}} over everything replayed since
@@ -89,11 +110,13 @@ class GraphTimer:
         if khz <= 0:
             raise RuntimeError("rdx_wallclock_khz failed")
         acc = self.acc.cpu().numpy()
+        ovh = self.overhead_ticks()
         out = {}
         for i, (name, work, grp, shape) in enumerate(self.sites):
             ticks, cnt = int(acc[i, 0]), int(acc[i, 1])
             if cnt == 0:
                 continue
+            ticks = max(ticks - ovh * cnt, 0.0)
             mult = grp["total"] / grp["sampled"]
             key = name if not by_shape or shape is None else f"{name}{list(shape)}"
             r = out.setdefault(key, {"launches": 0.0, "total_ms": 0.0, "work_sum": 0.0, "sampled_launches": 0})
@@ -117,6 +140,7 @@ class _timed:
 
     def __enter__(self):
         if CAPTURE_TIMING is not None and torch.cuda.is_current_stream_capturing():
+            CAPTURE_TIMING.calibrate(self.t)
             self.site = CAPTURE_TIMING.slot(self.name, self.work, self.shape)   # None: not a sampled site
             if self.site is not None:
                 check(lib().rdx_timestamp_acc(_p(self.site), -1, _stream(self.t)), "timestamp")
