@@ -144,33 +144,44 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   auto xslot = [&](int row) -> float* { return xr + (row & 3) * BX_XW; };
   auto oslot = [&](int row) -> char* { return os + (row % 3) * BX_IMG; };
   // out1 row ro (0 .. H) at positions q0 - 1 + pp, pp < 130 (zero outside [0, W): conv2's padding)
+  // one item = (position pp, this thread's 8 channels); the out-of-image positions (conv2's zero padding) are
+  // masked with an AND rather than branched around, and a thread's items (2 or 3) read their x taps together
+  auto out1_item = [&](const float (&v0)[3], const float (&v1)[3], int pp, char* sl) {
+    const int q = q0 - 1 + pp;
+    const uint32_t msk = (q >= 0 && q < W) ? 0xffffffffu : 0u;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      float yv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float acc = v0[0] * t1[k + e][0];
+        acc = fmaf(v0[1], t1[k + e][1], acc);
+        acc = fmaf(v0[2], t1[k + e][2], acc);
+        acc = fmaf(v1[0], t1[k + e][3], acc);
+        acc = fmaf(v1[1], t1[k + e][4], acc);
+        acc = fmaf(v1[2], t1[k + e][5], acc);
+        const float cv = hround(acc);
+        yv[e] = bx_selu(fmaf((cv + cb[k + e]) - mu[k + e], sg[k + e], sh[k + e]));
+      }
+      o[k >> 1] = bx_pack2(yv[0], yv[1]) & msk;
+    }
+    *reinterpret_cast<uint4*>(sl + bx_img(pp, g8)) = make_uint4(o[0], o[1], o[2], o[3]);
+  };
   auto make_out1 = [&](int ro) {
     const float* xa = xslot(ro - 1);
     const float* xb = xslot(ro);
     char* sl = oslot(ro);
-    for (int it = tid; it < 130 * 4; it += BX_T) {
-      const int pp = it >> 2;
-      const int q = q0 - 1 + pp;
-      const float v0[3] = {xa[pp], xa[pp + 1], xa[pp + 2]}, v1[3] = {xb[pp], xb[pp + 1], xb[pp + 2]};
-      uint32_t o[4];
-#pragma unroll
-      for (int k = 0; k < 8; k += 2) {
-        float yv[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          float acc = v0[0] * t1[k + e][0];
-          acc = fmaf(v0[1], t1[k + e][1], acc);
-          acc = fmaf(v0[2], t1[k + e][2], acc);
-          acc = fmaf(v1[0], t1[k + e][3], acc);
-          acc = fmaf(v1[1], t1[k + e][4], acc);
-          acc = fmaf(v1[2], t1[k + e][5], acc);
-          const float cv = hround(acc);
-          yv[e] = bx_selu(fmaf((cv + cb[k + e]) - mu[k + e], sg[k + e], sh[k + e]));
-        }
-        o[k >> 1] = (q >= 0 && q < W) ? bx_pack2(yv[0], yv[1]) : 0u;
-      }
-      *reinterpret_cast<uint4*>(sl + bx_img(pp, g8)) = make_uint4(o[0], o[1], o[2], o[3]);
-    }
+    static_assert(2 * BX_T <= 130 * 4 && 3 * BX_T >= 130 * 4, "2 or 3 items per thread");
+    const int pa = tid >> 2, pb = (tid + BX_T) >> 2, pc = (tid + 2 * BX_T) >> 2;
+    const bool has_c = tid + 2 * BX_T < 130 * 4;
+    const int pcc = has_c ? pc : 0;
+    const float a0[3] = {xa[pa], xa[pa + 1], xa[pa + 2]}, a1[3] = {xb[pa], xb[pa + 1], xb[pa + 2]};
+    const float b0[3] = {xa[pb], xa[pb + 1], xa[pb + 2]}, b1[3] = {xb[pb], xb[pb + 1], xb[pb + 2]};
+    const float c0[3] = {xa[pcc], xa[pcc + 1], xa[pcc + 2]}, c1[3] = {xb[pcc], xb[pcc + 1], xb[pcc + 2]};
+    out1_item(a0, a1, pa, sl);
+    out1_item(b0, b1, pb, sl);
+    if (has_c) out1_item(c0, c1, pc, sl);
   };
   const int pw = wv * 32 + r;   // this lane's output position q0 + pw (B operand row of the MFMA)
 
