@@ -445,8 +445,8 @@ int rdx_gemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
  * Same operands and results as rdx_selective_scan_fwd / _bwd (src/models/modules/mamba_block.py:65-122, both
  * directions at original positions, the same checkpoint layout), the steps cut into rdx_scan2_chunks(L) chunks of
  * 16: per-chunk local states and decay products, then every chunk from its composed carry. Forward: P (the
- * per-chunk decay products, kept for the backward) and hloc are [dirs][B][chunks][D][N] fp32
- * (rdx_scan2_rec_elems). Backward: gloc is a workspace of the same size; dA_part [dirs * B * chunks][D][N],
+ * per-chunk decay products, kept for the backward) and hloc (a workspace: it ends holding every chunk's carry-in)
+ * are [dirs][B][chunks][D][N] fp32 (rdx_scan2_rec_elems). Backward: gloc is a workspace of the same size; dA_part [dirs * B * chunks][D][N],
  * dD_part / dbias_part [dirs * B * chunks][D] (summed by the caller), rows of ld_part floats (0: dense; D * N + 2D
  * packs the three into one buffer summed with one reduction); dBC [dirs][B][L][2N] fp32 is zeroed and accumulated
  * by the call. */

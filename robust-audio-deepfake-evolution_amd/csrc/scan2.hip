@@ -8,11 +8,12 @@
 // csrc/bimamba.hip, same checkpoint layout) and every (direction, utterance, chunk, 32-channel group) is one
 // 512-thread block (thread = channel x state, a DPP row of 16 lanes = one channel's 16 states):
 //   fwd 1  each chunk from h = 0: its end state hloc_c and its decay product P_c = prod a;
-//   fwd 2  carry-in h = compose(P_k, hloc_k) over the chunks before it (<= NC - 1 FMAs from L2), then the chunk
-//          from the true carry: y (staged in LDS, coalesced rows) and the checkpoint at the chunk end;
+//   fwd 1b carry-in of every chunk = compose(P_k, hloc_k) over the chunks before it (one thread per (dir, b, d, n),
+//          in place over hloc);
+//   fwd 2  the chunk from the true carry: y (staged in LDS, coalesced rows) and the checkpoint at the chunk end;
 //   bwd 1  each chunk's reverse carry from 0 (G_s = C_s dy_s + a_{s+1} G_{s+1}): gloc_c = a_{s0} G_{s0};
-//   bwd 2  carry from the right = compose(P_k, gloc_k) over the chunks after it, states re-run from the
-//          chunk's checkpoint, then every gradient of the chunk.
+//   bwd 1b carry from the right = compose(P_k, gloc_k) over the chunks after it (in place over gloc);
+//   bwd 2  states re-run from the chunk's checkpoint, then every gradient of the chunk.
 // At the Phase-6 shapes (B = 8, L = 201, Di = 288, N = 16, both directions) that is 2 x 8 x 13 x 9 = 1872 blocks
 // per launch (csrc/bimamba.hip: 384 blocks with a 201-step serial chain staged from 24-byte row slices).
 // The per-chunk products P are saved by the forward for the backward (it composes the same decays).
@@ -104,6 +105,56 @@ __device__ __forceinline__ int64_t rec(const Geo& g, int chunk, int D) {
   return (((int64_t)g.db * g.nc + chunk) * D + g.d) * N + g.n;
 }
 
+// The per-step sums over the 16 states (y, d dt, d u) and over the block's channels (dB, dC) do not feed the
+// recurrence, so the kernels keep each step's per-lane term in registers and reduce all 16 steps at the chunk end
+// in one transposed pass: 15 lane exchanges per array instead of 16 x 4 (over states), 12 instead of 16 x 2 (over a
+// wave's 4 channels). The kernels are VALU-issue-bound (every step's work is per (channel, state) lane).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// v[k] of every lane of a 16-lane row -> lane n gets the row's total of v[n] (butterfly over lane bits 3..0: xor 8
+// by row_ror, xor 4 by a bit-mode ds_swizzle, xor 2 / xor 1 by quad_perm). Every exchange runs with the whole wave
+// active: a DPP read of a lane that is switched off returns the bound value, so a lane-dependent choice between two
+// DPP patterns (which the compiler turns into two exec-masked halves) would read zeros.
+__device__ __forceinline__ float row_tr_sum16(const float* v, int n) {
+  const bool b3 = n & 8, b2 = n & 4, b1 = n & 2, b0 = n & 1;
+  float w8[8], w4[4], w2[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float keep = b3 ? v[j + 8] : v[j], send = b3 ? v[j] : v[j + 8];
+    w8[j] = keep + dppf<0x128>(send);                                        // row_ror:8 = xor 8
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float keep = b2 ? w8[j + 4] : w8[j], send = b2 ? w8[j] : w8[j + 4];
+    w4[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x101F));   // xor 4
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float keep = b1 ? w4[j + 2] : w4[j], send = b1 ? w4[j] : w4[j + 2];
+    w2[j] = keep + dppf<0x4E>(send);                                         // quad_perm [2,3,0,1]
+  }
+  const float keep = b0 ? w2[1] : w2[0], send = b0 ? w2[0] : w2[1];
+  return keep + dppf<0xB1>(send);                                            // quad_perm [1,0,3,2]
+}
+// v[k] of every lane -> x[j] = total of v[4 r + j] over the wave's 4 rows (lanes l, l ^ 16, l ^ 32, l ^ 48), in
+// every lane of row r: permlane32_swap (lanes 32-63 of the first operand <-> lanes 0-31 of the second), then
+// permlane16_swap (odd rows of the first <-> even rows of the second)
+__device__ __forceinline__ void rows_tr_sum4(const float* v, float* x) {
+  float w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 8]), false, false);
+    w[j] = __uint_as_float(p[0]) + __uint_as_float(p[1]);   // lanes 0-31: index j, lanes 32-63: j + 8
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[j]), __float_as_uint(w[j + 4]), false, false);
+    x[j] = __uint_as_float(p[0]) + __uint_as_float(p[1]);   // row r: index j + 4 r
+  }
+}
+
 // ---- fwd 1: chunk-local end state and decay product
 template <typename T>
 __global__ __launch_bounds__(NT) void fwd_chunk_kernel(const T* __restrict__ u, const T* __restrict__ delta,
@@ -132,6 +183,38 @@ __global__ __launch_bounds__(NT) void fwd_chunk_kernel(const T* __restrict__ u, 
   P[rec(g, g.c, D)] = prod;
 }
 
+// ---- fwd 1b / bwd 1b: the carry entering every chunk, in place over the chunk-local records, one thread per (dir,
+// b, d, n): forward rec_c <- compose(P_k, rec_k) over k < c in step order, backward over k > c nearest last (the FMA
+// chains the output kernels ran per thread before: 2 loads per chunk once instead of up to 2 x 16 in each of the
+// 512 threads of every block)
+__global__ __launch_bounds__(256) void carry_kernel(const float* __restrict__ P, float* __restrict__ recs, int64_t DN,
+                                                    int nc, int64_t total, int reverse) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int64_t db = t / DN;
+  const int64_t base = db * nc * DN + (t - db * DN);   // record (db, chunk, d, n) = (db * nc + chunk) * DN + d * N + n
+  float h = 0.f;
+  for (int k0 = 0; k0 < nc; k0 += CK) {     // 16 chunks' loads in flight at once, then the FMA chain
+    const int m = min(CK, nc - k0);
+    float r[CK], p[CK];
+    int64_t o[CK];
+#pragma unroll
+    for (int k = 0; k < CK; ++k) {
+      const int kk = k0 + min(k, m - 1);
+      o[k] = base + (int64_t)(reverse ? nc - 1 - kk : kk) * DN;
+      r[k] = recs[o[k]];
+      p[k] = P[o[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < CK; ++k) {
+      if (k < m) {
+        recs[o[k]] = h;
+        h = fmaf(p[k], h, r[k]);
+      }
+    }
+  }
+}
+
 // ---- fwd 2: carry-in, y and the checkpoint at the chunk end
 template <typename T>
 __global__ __launch_bounds__(NT) void fwd_out_kernel(const T* __restrict__ u, const T* __restrict__ delta,
@@ -144,40 +227,27 @@ __global__ __launch_bounds__(NT) void fwd_out_kernel(const T* __restrict__ u, co
   __shared__ float s_u[CK * CH], s_dt[CK * CH], s_B[CK * N], s_C[CK * N], s_y[CK * CH];
   const Geo g = geo(B, L, D);
   stage<T, true, false>(g, u, delta, dt_bias, Bm, Cm, ldbc, nullptr, 0, s_u, s_dt, nullptr, s_B, s_C, B, L, D);
-  // carry-in from the chunks before this one, in step order: every load issued unconditionally from a clamped
-  // index (a per-load runtime test makes hipcc branch and wait around each load), the unused ones masked to the
-  // identity (P = 1, h = 0) in registers, then the FMA chain
-  float h = 0.f;
-  if (g.active) {
-    const int nprev = g.c;
-    for (int k0 = 0; k0 < nprev; k0 += CK) {
-      const int m = min(CK, nprev - k0);
-      float pk[CK], hk[CK];
-#pragma unroll
-      for (int k = 0; k < CK; ++k) {
-        const int kk = k0 + min(k, m - 1);
-        pk[k] = P[rec(g, kk, D)];
-        hk[k] = hloc[rec(g, kk, D)];
-      }
-#pragma unroll
-      for (int k = 0; k < CK; ++k) h = fmaf(k < m ? pk[k] : 1.f, h, k < m ? hk[k] : 0.f);
-    }
-  }
+  // carry-in from the chunks before this one (composed in step order by carry_kernel)
+  float h = g.active ? hloc[rec(g, g.c, D)] : 0.f;
   __syncthreads();
   const float A2 = g.active ? -__expf(A_log[g.d * N + g.n]) * LOG2E : 0.f;
   const float Dd = g.active ? Dp[g.d] : 0.f;
+  float pv[CK];     // this state's C_s h_s terms, summed over the states at the chunk end
 #pragma unroll
   for (int i = 0; i < CK; ++i) {
+    pv[i] = 0.f;
     if (i < g.cnt) {    // block-uniform
       const float dtv = s_dt[i * CH + g.dl];
-      const float uu = s_u[i * CH + g.dl];
       const float a = __builtin_amdgcn_exp2f(dtv * A2);
-      h = fmaf(a, h, dtv * uu * s_B[i * N + g.n]);
-      const float pv = row16_sum(s_C[i * N + g.n] * h);
-      if (g.n == 0) s_y[i * CH + g.dl] = fmaf(Dd, uu, pv);
+      h = fmaf(a, h, dtv * s_u[i * CH + g.dl] * s_B[i * N + g.n]);
+      pv[i] = s_C[i * N + g.n] * h;
     }
   }
   if (g.active && g.c < g.nc - 1) ckpt[(((int64_t)g.db * (g.nc - 1) + g.c) * D + g.d) * N + g.n] = h;
+  {
+    const float yv = row_tr_sum16(pv, g.n);   // lane n: step n of channel dl
+    s_y[g.n * CH + g.dl] = fmaf(Dd, s_u[g.n * CH + g.dl], yv);
+  }
   __syncthreads();
   {
     const int i = threadIdx.x >> 5, c = threadIdx.x & 31, dd = g.d0 + c;
@@ -249,81 +319,82 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = lane >> 4;
   stage<T, true, true>(g, u, delta, dt_bias, Bm, Cm, ldbc, dy, dy_dir_stride, s_u, s_dt, s_dy, s_B, s_C, B, L, D,
                        s_sig);
-  // the carry entering from the right: compose the later chunks, nearest last
+  // the carry entering from the right (the later chunks composed nearest last by carry_kernel)
   float X = 0.f, h0 = 0.f;
   if (g.active) {
-    for (int k1 = g.nc - 1; k1 > g.c; k1 -= CK) {
-      const int m = min(CK, k1 - g.c);
-      float pk[CK], gk[CK];
-#pragma unroll
-      for (int k = 0; k < CK; ++k) {      // unconditional loads from clamped indices (see fwd_out_kernel)
-        const int kk = k1 - min(k, m - 1);
-        pk[k] = P[rec(g, kk, D)];
-        gk[k] = gloc[rec(g, kk, D)];
-      }
-#pragma unroll
-      for (int k = 0; k < CK; ++k) X = fmaf(k < m ? pk[k] : 1.f, X, k < m ? gk[k] : 0.f);
-    }
+    X = gloc[rec(g, g.c, D)];
     if (g.c > 0) h0 = ckpt[(((int64_t)g.db * (g.nc - 1) + (g.c - 1)) * D + g.d) * N + g.n];
   }
   __syncthreads();
   const float Aval = g.active ? -__expf(A_log[g.d * N + g.n]) : 0.f;
   const float A2 = Aval * LOG2E;
   const float Dd = g.active ? Dp[g.d] : 0.f;
-  // states of the chunk from its checkpoint
-  float hs[CK];
+  // states of the chunk from its checkpoint, and their decays
+  float hs[CK], av[CK];
   {
     float h = h0;
 #pragma unroll
     for (int i = 0; i < CK; ++i) {
+      av[i] = 1.f;
       if (i < g.cnt) {
         const float dtv = s_dt[i * CH + g.dl];
-        h = fmaf(__builtin_amdgcn_exp2f(dtv * A2), h, dtv * s_u[i * CH + g.dl] * s_B[i * N + g.n]);
+        av[i] = __builtin_amdgcn_exp2f(dtv * A2);
+        h = fmaf(av[i], h, dtv * s_u[i * CH + g.dl] * s_B[i * N + g.n]);
       }
       hs[i] = h;
     }
   }
-  float dA = 0.f, dDacc = 0.f, dbacc = 0.f;
-  float r_du[CK], r_dd[CK];
+  // per step, this lane's terms of the sums over states (d dt, d u) and over channels (dB, dC); a channel past D
+  // has u = dt = dy = 0 staged and X = h = 0, so every term of it is exactly 0
+  float dA = 0.f;
+  float tB[CK], tC[CK], tt[CK], tu[CK];
 #pragma unroll
   for (int i = CK - 1; i >= 0; --i) {
-    r_du[i] = 0.f;
-    r_dd[i] = 0.f;
+    tB[i] = tC[i] = tt[i] = tu[i] = 0.f;
     if (i < g.cnt) {    // block-uniform
       const int o = i * CH + g.dl;
       const float dtv = s_dt[o], uu = s_u[o], dyv = s_dy[o];
       const float Bn = s_B[i * N + g.n], Cn = s_C[i * N + g.n];
-      const float a = __builtin_amdgcn_exp2f(dtv * A2);
+      const float a = av[i];
       const float hprev = i > 0 ? hs[i > 0 ? i - 1 : 0] : h0;
       const float G = fmaf(Cn, dyv, X);
       const float ah = a * hprev;
-      float vB = g.active ? G * dtv * uu : 0.f;
-      float vC = g.active ? dyv * hs[i] : 0.f;
-      vB += __shfl_xor(vB, 16, 64);
-      vB += __shfl_xor(vB, 32, 64);
-      vC += __shfl_xor(vC, 16, 64);
-      vC += __shfl_xor(vC, 32, 64);
-      if (row == 0) s_red[i][wave][g.n] = vB;
-      if (row == 1) s_red[i][wave][N + g.n] = vC;
-      dA = fmaf(G * dtv, ah, dA);
-      const float ddt = row16_sum(G * fmaf(Aval, ah, Bn * uu));
-      const float dus = row16_sum(G * dtv * Bn);
-      const float ddl = ddt * s_sig[o];         // softplus'(pre) = sigmoid(pre) (= 1 - exp(-dt))
-      r_du[i] = fmaf(Dd, dyv, dus);
-      r_dd[i] = ddl;
-      dDacc = fmaf(dyv, uu, dDacc);
-      dbacc += ddl;
+      const float Gdt = G * dtv;
+      tB[i] = Gdt * uu;
+      tC[i] = dyv * hs[i];
+      dA = fmaf(Gdt, ah, dA);
+      tt[i] = G * fmaf(Aval, ah, Bn * uu);
+      tu[i] = Gdt * Bn;
       X = a * G;
     }
   }
-  __syncthreads();                           // every read of s_u / s_dt done: reuse them for du / ddelta
-  if (g.n == 0) {
+  // lane n of each row: step n of its channel (d dt, d u over the states); lane (row r, n): steps 4 r .. 4 r + 3
+  // of dB / dC[n] over the wave's 4 channels
+  const float ddt = row_tr_sum16(tt, g.n);
+  const float dus = row_tr_sum16(tu, g.n);
+  {
+    float xb[4], xc[4];
+    rows_tr_sum4(tB, xb);
+    rows_tr_sum4(tC, xc);
 #pragma unroll
-    for (int i = 0; i < CK; ++i) {
-      s_u[i * CH + g.dl] = r_du[i];
-      s_dt[i * CH + g.dl] = r_dd[i];
+    for (int j = 0; j < 4; ++j) {
+      s_red[4 * row + j][wave][g.n] = xb[j];
+      s_red[4 * row + j][wave][N + g.n] = xc[j];
     }
   }
+  float r_du = 0.f, r_dd = 0.f, dDt = 0.f;
+  if (g.n < g.cnt) {
+    const int o = g.n * CH + g.dl;
+    const float dyv = s_dy[o];
+    r_dd = ddt * s_sig[o];         // softplus'(pre) = sigmoid(pre) (= 1 - exp(-dt))
+    r_du = fmaf(Dd, dyv, dus);
+    dDt = dyv * s_u[o];
+  }
+  const float dDacc = row16_sum(dDt);
+  const float dbacc = row16_sum(r_dd);
+  __syncthreads();                           // every read of s_u / s_dt done: reuse them for du / ddelta
+  s_u[g.n * CH + g.dl] = r_du;
+  s_dt[g.n * CH + g.dl] = r_dd;
   {
     const int tid = threadIdx.x;
     const int i = tid >> 5, j = tid & 31;      // one (step, dB|dC column) per thread
@@ -351,6 +422,13 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
   }
 }
 
+__host__ inline void launch_carry(const float* P, float* recs, int B, int L, int D, int dirs, int reverse,
+                                 hipStream_t st) {
+  const int64_t DN = (int64_t)D * N, total = (int64_t)dirs * B * DN;
+  hipLaunchKernelGGL(carry_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, P, recs, DN,
+                     (L + CK - 1) / CK, total, reverse);
+}
+
 }  // namespace s2
 }  // namespace rdx
 
@@ -376,6 +454,7 @@ extern "C" int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const 
     hipLaunchKernelGGL(s2::fwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, ldbc, dt_bias, hloc, P, B, L, D);
     RDX_LAUNCH_CHECK();
+    s2::launch_carry(P, hloc, B, L, D, dirs, 0, st);
     hipLaunchKernelGGL(s2::fwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, hloc, P, y, ckpt, B, L, D);
   } else if (dtype == RDX_F32) {
@@ -383,6 +462,7 @@ extern "C" int rdx_scan2_fwd(int dtype, const void* u, const void* delta, const 
     hipLaunchKernelGGL(s2::fwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, ldbc, dt_bias, hloc, P, B, L, D);
     RDX_LAUNCH_CHECK();
+    s2::launch_carry(P, hloc, B, L, D, dirs, 0, st);
     hipLaunchKernelGGL(s2::fwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, hloc, P, y, ckpt, B, L, D);
   } else {
@@ -414,6 +494,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
     hipLaunchKernelGGL(s2::bwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)delta, A_log, (const T*)Cm,
                        ldbc, dt_bias, dy, dy_dir_stride, gloc, dBC, B, L, D);
     RDX_LAUNCH_CHECK();
+    s2::launch_carry(P, gloc, B, L, D, dirs, 1, st);
     hipLaunchKernelGGL(s2::bwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, P, gloc, dy, dy_dir_stride, (T*)du,
                        (T*)ddelta, dBC, dA_part, dD_part, dbias_part, ldpa, ldpd, B, L, D);
@@ -422,6 +503,7 @@ extern "C" int rdx_scan2_bwd(int dtype, const void* u, const void* delta, const 
     hipLaunchKernelGGL(s2::bwd_chunk_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)delta, A_log, (const T*)Cm,
                        ldbc, dt_bias, dy, dy_dir_stride, gloc, dBC, B, L, D);
     RDX_LAUNCH_CHECK();
+    s2::launch_carry(P, gloc, B, L, D, dirs, 1, st);
     hipLaunchKernelGGL(s2::bwd_out_kernel<T>, grid, dim3(s2::NT), 0, st, (const T*)u, (const T*)delta, A_log,
                        (const T*)Bm, (const T*)Cm, ldbc, Dp, dt_bias, ckpt, P, gloc, dy, dy_dir_stride, (T*)du,
                        (T*)ddelta, dBC, dA_part, dD_part, dbias_part, ldpa, ldpd, B, L, D);

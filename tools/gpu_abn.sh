@@ -15,6 +15,7 @@ if [ -n "$PRE" ]; then
   cat gpurun_out/$TAG/pre.log | grep -v amdgpu.ids
   [ $rc -eq 0 ] || exit $rc
 fi
+[ -n "$VARIANTS_FILE" ] && VARIANTS=$(cat "$VARIANTS_FILE")   # variants whose values carry quotes (JSON)
 IFS=';' read -ra VS <<< "$VARIANTS"
 for i in $(seq 1 ${ROUNDS:-2}); do
   timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/$TAG/v0_$i.json 2> gpurun_out/$TAG/v0_$i.err || exit $?

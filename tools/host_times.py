@@ -23,6 +23,7 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--amp", default="fp16", choices=["bf16", "fp16"])
     a = ap.parse_args()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -33,7 +34,8 @@ def main():
     config["training_config"]["accumulation_steps"] = 4
     config["batch_size"] = 8
     model = bench.build(config, dev, 0.0)
-    tr = Trainer(model, config, dev, total_optimizer_steps(1, 400, 4), torch.bfloat16)
+    tr = Trainer(model, config, dev, total_optimizer_steps(1, 400, 4),
+                 torch.float16 if a.amp == "fp16" else torch.bfloat16)
     dc = config["data_config"]
     aug = Augmenter(dev, algo=dc.get("rawboost_algo", 0), rawboost_p=dc.get("rawboost_p", 1.0),
                     use_codec=dc.get("use_codec_aug", False), codec_p=dc.get("codec_p", 0.5))
