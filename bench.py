@@ -41,7 +41,8 @@ KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "sincconv_mfma": ("mfma
                 "attn_fwd": ("mfma", "bf16"), "attn_bwd": ("mfma", "bf16"),
                 "posconv_fwd": ("mfma", "bf16"), "posconv_bwd": ("mfma", "bf16"),
                 "sincnet_b0_bwd": ("hbm", None), "sincnet_b0_fwd": ("hbm", None),
-                "b0x_fwd": ("mfma", "bf16"), "b0x_bwd": ("mfma", "bf16"), "wgrad_acc": ("mfma", "bf16"), "sconv_fwd": ("hbm", None), "sconv_wgrad": ("hbm", None),
+                "b0x_fwd": ("mfma", "bf16"), "b0x_bwd": ("mfma", "bf16"), "wgrad_acc": ("mfma", "bf16"), "wgrad_many": ("mfma", "bf16"),
+                "sconv_fwd": ("hbm", None), "sconv_wgrad": ("hbm", None),
                 "sconv_dgrad_bnselu": ("hbm", None),
                 "fe_conv0": ("hbm", None), "fe_ln_gelu": ("hbm", None), "fe_conv_gemm": ("mfma", "bf16"),
                 "gemm": ("mfma", "bf16"), "wgemm": ("mfma", "bf16"), "pgemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}

@@ -513,6 +513,14 @@ int rdx_wgrad_chunk(int M, int N, int K);
 int64_t rdx_wgrad_ws_floats(int M, int N, int K);
 int rdx_wgrad_acc(const void* dy, int64_t ldy, const void* x, int64_t ldx, int M, int N, int K, float* dw, int64_t ldw,
                   float* db, float* ws, int64_t ws_floats, void* stream);
+/* Batched form: n <= 32 problems (arrays of n entries; db[k] may be NULL), every dw / db distinct, in two launches:
+ * one workgroup per (problem, 64 x 64 output block, run of 128-row sub-chunks), then one fixed-order reduction of
+ * the runs' partials into each dW / db. ws >= rdx_wgrad_many_ws_floats (has_db[k] = db[k] != NULL). radhip.ops.
+ * wgrad_batch collects a backward pass's SideLinear gradients into one call. */
+int64_t rdx_wgrad_many_ws_floats(int n, const int* M, const int* N, const int* K, const int* has_db);
+int rdx_wgrad_acc_many(int n, const void* const* dy, const int64_t* ldy, const void* const* x, const int64_t* ldx,
+                       const int* M, const int* N, const int* K, float* const* dw, const int64_t* ldw,
+                       float* const* db, float* ws, int64_t ws_floats, void* stream);
 
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.

@@ -165,6 +165,165 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// ---- Batched form: every weight gradient of one backward pass in two launches (rdx_wgrad_acc_many). Launched one
+// per linear, the pair above costs ~12 us per layer in a captured graph, nearly all of it launch boundary; 31 of
+// them per detector-head backward. One workgroup owns (problem, 64 x 64 output block, run of R sub-chunks of 128
+// token rows): the next sub-chunk's dY / X panels are loaded into registers while the current one's MFMAs run
+// (accumulating in registers), so a run costs about one load latency per sub-chunk and leaves ONE fp32 partial.
+constexpr int WGM_MC = 128;                        // token rows per sub-chunk (32 KB of LDS: several groups per CU)
+constexpr int WGM_ITEMS = WGM_MC * 8 / WR_T;       // 16-byte items per thread per operand
+constexpr int WGM_MAXP = 32;                       // problems per launch (the table is a kernel argument)
+static_assert(WGM_MC == 4 * (WR_T / 8), "db: 32 row groups of 4 rows x 8 column chunks per sub-chunk");
+struct WgmProb {
+  const hst* dy;
+  const hst* x;
+  float* dw;
+  float* db;
+  float* part;    // [S][N][K]
+  float* partb;   // [S][N] (db only)
+  int ldy, ldx, ldw, M, N, K, S, R, nbn, nbk, vec, blk0, out0;
+};
+struct WgmTable {
+  WgmProb p[WGM_MAXP];
+  int n;
+};
+
+__device__ __forceinline__ void wgm_gather(uint4 (&v)[WGM_ITEMS], const hst* __restrict__ src, int64_t ld, int M,
+                                           int C, int m0, int c0, bool vec) {
+#pragma unroll
+  for (int j = 0; j < WGM_ITEMS; ++j) {
+    const int i = threadIdx.x + WR_T * j;
+    const int row = i >> 3, ch = i & 7;
+    const int m = m0 + row, c = c0 + 8 * ch;
+    v[j] = make_uint4(0u, 0u, 0u, 0u);
+    if (m < M) {
+      const hst* p = src + (int64_t)m * ld + c;
+      if (vec && c + 8 <= C) {
+        v[j] = *reinterpret_cast<const uint4*>(p);
+      } else {
+        uint16_t e[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) e[t] = (c + t < C) ? hbits_of(p[t]) : (uint16_t)0;
+        v[j] = make_uint4(e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
+                          e[6] | ((uint32_t)e[7] << 16));
+      }
+    }
+  }
+}
+__device__ __forceinline__ void wgm_put(char* img, const uint4 (&v)[WGM_ITEMS]) {
+#pragma unroll
+  for (int j = 0; j < WGM_ITEMS; ++j) {
+    const int i = threadIdx.x + WR_T * j;
+    *reinterpret_cast<uint4*>(img + wr_img(i >> 3, i & 7)) = v[j];
+  }
+}
+// the problem owning block b of a grid dealt as [problem 0's blocks | problem 1's | ...] (first[k] = its first block)
+// (a fixed-count loop: the table's scalar loads issue together instead of one load latency per problem)
+__device__ __forceinline__ int wgm_find(const WgmTable& t, int b, bool out) {
+  int p = 0;
+#pragma unroll
+  for (int k = 1; k < WGM_MAXP; ++k) p = (k < t.n && b >= (out ? t.p[k].out0 : t.p[k].blk0)) ? k : p;
+  return __builtin_amdgcn_readfirstlane(p);
+}
+
+__global__ __launch_bounds__(WR_T, 4) void wgrad_part_many_kernel(WgmTable t) {
+  __shared__ __attribute__((aligned(16))) char iy[WGM_MC * 128], ix[WGM_MC * 128];
+  const WgmProb& q = t.p[wgm_find(t, blockIdx.x, false)];
+  const int nb = q.nbn * q.nbk, local = blockIdx.x - q.blk0;
+  const int s = local / nb, blk = local - s * nb;
+  const int bn = blk / q.nbk, bk = blk - bn * q.nbk;
+  const int n0 = bn * 64, k0 = bk * 64;
+  const int r0 = s * q.R * WGM_MC;
+  const int nsub = min(q.R, (q.M - r0 + WGM_MC - 1) / WGM_MC);
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int tn = wv >> 1, tk = wv & 1;
+  const bool bsum = q.partb && bk == 0;     // block-uniform: the whole group sums dY's columns
+  wrf32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // columns 8 (tid & 7) .. + 7 over rows 4 (tid >> 3) .. + 3
+  uint4 vy[WGM_ITEMS], vx[WGM_ITEMS];
+  wgm_gather(vy, q.dy, q.ldy, q.M, q.N, r0, n0, q.vec & 1);
+  wgm_gather(vx, q.x, q.ldx, q.M, q.K, r0, k0, q.vec & 2);
+  for (int j = 0; j < nsub; ++j) {
+    __syncthreads();                          // the previous sub-chunk's LDS reads are done
+    wgm_put(iy, vy);
+    wgm_put(ix, vx);
+    if (j + 1 < nsub) {                       // the next sub-chunk's loads run under this one's MFMAs
+      const int m1 = r0 + (j + 1) * WGM_MC;
+      wgm_gather(vy, q.dy, q.ldy, q.M, q.N, m1, n0, q.vec & 1);
+      wgm_gather(vx, q.x, q.ldx, q.M, q.K, m1, k0, q.vec & 2);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < WGM_MC / 16; ++st)
+      acc = mfma32x32x16(wr_read_tr(iy, tn * 32, st, lane), wr_read_tr(ix, tk * 32, st, lane), acc);
+    if (bsum) {     // db: this thread's 8 columns over its 4 rows of the sub-chunk (rows past M are zeros)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const uint4 v = *reinterpret_cast<const uint4*>(iy + wr_img(4 * (tid >> 3) + rr, tid & 7));
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bv[2 * e] += hlo(w[e]);
+          bv[2 * e + 1] += hhi(w[e]);
+        }
+      }
+    }
+  }
+  if (bsum) {       // the 32 row groups' sums of each column, added in row-group order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(ix);            // [32 row groups][64 columns]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(tid >> 3) * 64 + 8 * (tid & 7) + e] = bv[e];
+    __syncthreads();
+    if (tid < 64) {
+      float t = 0.f;
+      for (int g = 0; g < 32; ++g) t += red[g * 64 + tid];
+      bv[0] = t;
+    }
+  }
+  const int r = lane & 31, hh = lane >> 5;
+  const int k = k0 + tk * 32 + r;
+  float* out = q.part + (int64_t)s * q.N * q.K;
+  if (k < q.K) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = n0 + tn * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (n < q.N) out[(int64_t)n * q.K + k] = acc[i];
+    }
+  }
+  if (bsum && tid < 64 && n0 + tid < q.N) q.partb[(int64_t)s * q.N + n0 + tid] = bv[0];
+}
+
+// dW += sum_s part[s], db += sum_s partb[s] for every problem: one output per thread, the runs added in run order
+// (deterministic), 256 outputs per block
+constexpr int WGM_RED = 256;
+__global__ __launch_bounds__(WGM_RED) void wgrad_reduce_many_kernel(WgmTable t) {
+  const WgmProb& q = t.p[wgm_find(t, blockIdx.x, true)];
+  const int64_t nk = (int64_t)q.N * q.K;
+  const int64_t tot = nk + (q.db ? q.N : 0);
+  const int64_t i = (int64_t)(blockIdx.x - q.out0) * WGM_RED + threadIdx.x;
+  if (i >= tot) return;
+  const float* src = i < nk ? q.part + i : q.partb + (i - nk);
+  const int64_t st = i < nk ? nk : (int64_t)q.N;
+  float v[8];
+  float acc = 0.f;
+  for (int s0 = 0; s0 < q.S; s0 += 8) {      // 8 runs' loads in flight, then added in order
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = s0 + k < q.S ? src[(int64_t)(s0 + k) * st] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k];
+  }
+  if (i < nk) {
+    const int n = (int)(i / q.K), k = (int)(i - (int64_t)n * q.K);
+    q.dw[(int64_t)n * q.ldw + k] += acc;
+  } else {
+    q.db[i - nk] += acc;
+  }
+}
+
+
 }  // namespace rdx
 
 using namespace rdx;
@@ -223,6 +382,84 @@ extern "C" int rdx_wgrad_acc(const void* dy, int64_t ldy, const void* x, int64_t
   const int64_t tot = (int64_t)N * K + (db ? N : 0);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0, st, ws, a.partb, S, N, K,
                      dw, ldw, db);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+// Plan of a batched launch: every problem runs S runs of R sub-chunks (S, R from its token count and the group's
+// total output blocks: about 4 workgroups per CU, its occupancy, over the whole group; at least 2 runs per block).
+static void wgm_plan(int n, const int* M, const int* N, const int* K, int* S, int* R) {
+  int64_t outb = 0;
+  for (int k = 0; k < n; ++k) outb += (int64_t)((N[k] + 63) / 64) * ((K[k] + 63) / 64);
+  int64_t runs = (4 * 256 + outb - 1) / (outb > 0 ? outb : 1);
+  if (runs < 2) runs = 2;
+  for (int k = 0; k < n; ++k) {
+    const int nsub = (M[k] + WGM_MC - 1) / WGM_MC;
+    R[k] = (int)((nsub + runs - 1) / runs);
+    S[k] = (nsub + R[k] - 1) / R[k];
+  }
+}
+
+extern "C" int64_t rdx_wgrad_many_ws_floats(int n, const int* M, const int* N, const int* K, const int* has_db) {
+  if (n <= 0 || n > WGM_MAXP || !M || !N || !K || !has_db) return 0;
+  int S[WGM_MAXP], R[WGM_MAXP];
+  wgm_plan(n, M, N, K, S, R);
+  int64_t f = 0;
+  for (int k = 0; k < n; ++k) f += (int64_t)S[k] * ((int64_t)N[k] * K[k] + (has_db[k] ? N[k] : 0));
+  return f;
+}
+
+extern "C" int rdx_wgrad_acc_many(int n, const void* const* dy, const int64_t* ldy, const void* const* x,
+                                  const int64_t* ldx, const int* M, const int* N, const int* K, float* const* dw,
+                                  const int64_t* ldw, float* const* db, float* ws, int64_t ws_floats, void* stream) {
+  RDX_REQUIRE(n >= 0 && n <= WGM_MAXP);
+  if (n == 0) return RDX_OK;
+  RDX_REQUIRE(dy && ldy && x && ldx && M && N && K && dw && ldw && db && ws);
+  int has_db[WGM_MAXP];
+  for (int k = 0; k < n; ++k) {
+    RDX_REQUIRE(dy[k] && x[k] && dw[k] && M[k] > 0 && N[k] > 0 && K[k] > 0 && ldy[k] >= N[k] && ldx[k] >= K[k] &&
+                ldw[k] >= K[k] && ldy[k] < (1ll << 31) && ldx[k] < (1ll << 31) && ldw[k] < (1ll << 31));
+    for (int j = 0; j < k; ++j) RDX_REQUIRE(dw[j] != dw[k] && (!db[k] || db[j] != db[k]));   // one add per output
+    has_db[k] = db[k] != nullptr;
+  }
+  RDX_REQUIRE(ws_floats >= rdx_wgrad_many_ws_floats(n, M, N, K, has_db));
+  int S[WGM_MAXP], R[WGM_MAXP];
+  wgm_plan(n, M, N, K, S, R);
+  WgmTable t{};
+  t.n = n;
+  int64_t blk = 0, outb = 0, off = 0;
+  for (int k = 0; k < n; ++k) {
+    WgmProb& q = t.p[k];
+    q.dy = (const hst*)dy[k];
+    q.x = (const hst*)x[k];
+    q.dw = dw[k];
+    q.db = db[k];
+    q.part = ws + off;
+    off += (int64_t)S[k] * N[k] * K[k];
+    q.partb = db[k] ? ws + off : nullptr;
+    off += db[k] ? (int64_t)S[k] * N[k] : 0;
+    q.ldy = (int)ldy[k];
+    q.ldx = (int)ldx[k];
+    q.ldw = (int)ldw[k];
+    q.M = M[k];
+    q.N = N[k];
+    q.K = K[k];
+    q.S = S[k];
+    q.R = R[k];
+    q.nbn = (N[k] + 63) / 64;
+    q.nbk = (K[k] + 63) / 64;
+    q.vec = ((ldy[k] % 8 == 0) && (((uintptr_t)dy[k] & 15) == 0) ? 1 : 0) |
+            ((ldx[k] % 8 == 0) && (((uintptr_t)x[k] & 15) == 0) ? 2 : 0);
+    q.blk0 = (int)blk;
+    q.out0 = (int)outb;
+    blk += (int64_t)S[k] * q.nbn * q.nbk;
+    outb += ((int64_t)N[k] * K[k] + (db[k] ? N[k] : 0) + WGM_RED - 1) / WGM_RED;
+  }
+  RDX_REQUIRE(blk < (1ll << 31) && outb < (1ll << 31));
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(wgrad_part_many_kernel, dim3((unsigned)blk), dim3(WR_T), 0, st, t);
+  RDX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3((unsigned)outb), dim3(WGM_RED), 0, st, t);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }

@@ -1453,11 +1453,85 @@ def wgrad_acc(dy, x, dw, db=None):
         raise ValueError(f"radhip wgrad_acc: shapes dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)}")
     if db is not None and (db.shape != (N,) or db.dtype != torch.float32 or not db.is_contiguous()):
         raise ValueError("radhip wgrad_acc: db must be fp32 [N]")
+    if _WGRAD_BATCH is not None and torch.cuda.current_stream(dy.device) == _WGRAD_BATCH[0]:
+        _WGRAD_BATCH[1].append((dy, x, dw, db))       # run with the pass's other weight gradients (wgrad_batch)
+        return
     ws = torch.empty(int(lib().rdx_wgrad_ws_floats(M, N, K)), device=dy.device, dtype=torch.float32)
     with _timed("wgrad_acc", dy, gemm_flops(N, K, M), shape=(M, N, K)):
         check(_L(dy).rdx_wgrad_acc(_p(dy), dy.stride(0), _p(x), x.stride(0), M, N, K, _p(dw), dw.stride(0),
                                   _p(db) if db is not None else None, _p(ws), ws.numel(), _stream(dy)), "wgrad_acc")
 
+
+
+# (stream, [(dy, x, dw, db), ...]) while a backward pass batches its weight gradients (wgrad_batch)
+_WGRAD_BATCH = None
+WGRAD_MANY_MAX = 32     # problems per batched launch (csrc/wgrad.hip WGM_MAXP)
+
+
+class wgrad_batch:
+    """Within the block, wgrad_acc calls on the current stream (SideLinear's backward: the detector head's 31
+    linears per pass) are collected instead of launched, and on exit run as batched launches (csrc/wgrad.hip
+    rdx_wgrad_acc_many, two kernels per up to 32 gradients instead of two per gradient). Launched one by one in a
+    captured graph they cost ~12 us each, almost all launch boundary. The accumulation into each .grad is the
+    same add; only its place in the stream moves to the end of the backward, before anything reads .grad.
+    RADHIP_WGRAD_BATCH=0 (or a nested block) leaves the launches where they were."""
+
+    def __init__(self, device=None):
+        self.device = device
+
+    def __enter__(self):
+        global _WGRAD_BATCH
+        self.on = (_WGRAD_BATCH is None and torch.cuda.is_available()
+                   and os.environ.get("RADHIP_WGRAD_BATCH", "1") != "0")
+        if self.on:
+            _WGRAD_BATCH = (torch.cuda.current_stream(self.device), [])
+        return self
+
+    def __exit__(self, et, ev, tb):
+        global _WGRAD_BATCH
+        if not self.on:
+            return False
+        pend = _WGRAD_BATCH[1]
+        _WGRAD_BATCH = None
+        if et is None:
+            wgrad_acc_many(pend)
+        return False
+
+
+def wgrad_acc_many(items):
+    """dw += dy^T x (and db += dy.sum(0)) for every (dy, x, dw, db) of `items`, each as wgrad_acc takes them, in
+    batched launches of up to WGRAD_MANY_MAX problems of one dtype. A launch holds each output once: a gradient
+    whose dw / db an earlier item of the launch already targets starts the next launch (same stream: the adds stay
+    in item order)."""
+    groups, cur, seen = [], [], set()
+    for it in items:
+        keys = {it[2].data_ptr()} | ({it[3].data_ptr()} if it[3] is not None else set())
+        if cur and (len(cur) == WGRAD_MANY_MAX or keys & seen or it[0].dtype != cur[0][0].dtype):
+            groups.append(cur)
+            cur, seen = [], set()
+        cur.append(it)
+        seen |= keys
+    if cur:
+        groups.append(cur)
+    for g in groups:
+        n = len(g)
+        ints = lambda vals: (ctypes.c_int * n)(*vals)
+        i64s = lambda vals: (ctypes.c_int64 * n)(*vals)
+        M = ints([it[0].shape[0] for it in g])
+        N = ints([it[0].shape[1] for it in g])
+        K = ints([it[1].shape[1] for it in g])
+        L = _L(g[0][0])
+        nws = int(lib().rdx_wgrad_many_ws_floats(n, M, N, K, ints([int(it[3] is not None) for it in g])))
+        dy0 = g[0][0]
+        ws = torch.empty(nws, device=dy0.device, dtype=torch.float32)
+        flops = sum(gemm_flops(it[0].shape[1], it[1].shape[1], it[0].shape[0]) for it in g)
+        with _timed("wgrad_many", dy0, flops, shape=(n, sum(it[0].shape[0] for it in g))):
+            check(L.rdx_wgrad_acc_many(n, ptr_array([it[0].data_ptr() for it in g]),
+                                       i64s([it[0].stride(0) for it in g]), ptr_array([it[1].data_ptr() for it in g]),
+                                       i64s([it[1].stride(0) for it in g]), M, N, K,
+                                       ptr_array([it[2].data_ptr() for it in g]), i64s([it[2].stride(0) for it in g]),
+                                       ptr_array([it[3].data_ptr() if it[3] is not None else None for it in g]),
+                                       _p(ws), ws.numel(), _stream(dy0)), "wgrad_acc_many")
 
 _WG_WS = {}
 

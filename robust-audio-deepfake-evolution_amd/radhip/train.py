@@ -21,7 +21,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, ops
 from .augment import CODEC_RATES, draw_rawboost
 from .ops import fgm_attack, pad_mixup, rawboost_batch, resample_batch, resample_kernel
 from .wavlm import compute_time_mask
@@ -497,12 +497,14 @@ class Trainer:
         yb = y[torch.tensor(perm, device=self.device)] if perm is not None else y
         self.cnn_reuse("store" if self.fgm is not None else None)
         loss = self._fwd_loss(x, ya, yb, lam)
-        self.scaler.scale(loss).backward()
+        with ops.wgrad_batch():
+            self.scaler.scale(loss).backward()
         if self.fgm is not None:
             self.fgm.attack()
             self.cnn_reuse("use")
             adv = self._fwd_loss(x, ya, yb, lam)
-            self.scaler.scale(adv).backward()
+            with ops.wgrad_batch():
+                self.scaler.scale(adv).backward()
             self.fgm.restore()
         self.cnn_reuse(None, drop=True)
         B = x.shape[0]
@@ -737,7 +739,8 @@ class GraphedMicroStep:
         with torch.autocast("cuda", dtype=tr.amp_dtype, enabled=tr.amp_dtype != torch.float32, cache_enabled=False):
             _, out = tr.model(self.x, Freq_aug=tr.freq_aug)
             loss = (self.lam * tr.criterion(out, self.ya) + (1.0 - self.lam) * tr.criterion(out, self.yb)) / tr.accum
-        loss.backward()
+        with ops.wgrad_batch():
+            loss.backward()
         if k == 0:
             tr.loss_sum.add_(loss.detach().double() * (tr.accum * self.B))
 

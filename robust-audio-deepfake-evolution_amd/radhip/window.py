@@ -289,7 +289,8 @@ class WindowStep:
             with self._amp():
                 _, out = tr.model(self.x, Freq_aug=tr.freq_aug)
                 loss = self._pass_loss(out)
-            tr.scaler.scale(loss).backward()
+            with ops.wgrad_batch():
+                tr.scaler.scale(loss).backward()
             tr.loss_sum.add_(loss.detach().double() * (tr.accum * B))
         finally:
             self._sinc_join()
@@ -322,7 +323,8 @@ class WindowStep:
             with self._amp():
                 _, out = tr.model(self.x[k * B:(k + 1) * B], Freq_aug=tr.freq_aug)
                 adv = self._pass_loss(out, k)
-            tr.scaler.scale(adv).backward()
+            with ops.wgrad_batch():
+                tr.scaler.scale(adv).backward()
         finally:
             core.cnn_feats_given = None
             if self.sinc_batched:

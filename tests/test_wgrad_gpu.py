@@ -46,3 +46,50 @@ def test_wgrad_acc_strided_views():
     wgrad_acc(dy, x, dw)
     ref = dy.double().t() @ x.double()
     assert float((dw.double() - ref).abs().max() / ref.abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_wgrad_batch_matches_one_by_one(dt):
+    """radhip.ops.wgrad_batch: the head's weight gradients of one pass collected and run as batched launches
+    (rdx_wgrad_acc_many) equal the one-by-one launches to fp32 summation order (1e-5 of the max-norm), at the
+    per-layer shapes of a B = 8 pass, with a strided view, a gradient without bias, a dw targeted twice (it must
+    start a second launch: both adds land) and more than 32 problems (several launches); repeat runs bit-identical."""
+    from radhip import ops
+    g = torch.Generator(device="cpu").manual_seed(11)
+    M = 1608
+    shapes = [(576, 144), (41, 288), (288, 9), (144, 288), (576, 144), (144, 576)] * 6 + [(144, 1024), (2, 144)]
+    big = torch.randn(M, 50, generator=g).to(DEV).to(dt)
+    items, refs = [], []
+    for i, (N, K) in enumerate(shapes):
+        dy = big[:, 9:50] if (N, K) == (41, 288) else torch.randn(M, N, generator=g).to(DEV).to(dt)
+        x = torch.randn(M, K, generator=g).to(DEV).to(dt)
+        dw = torch.randn(N, K, generator=g).to(DEV)
+        db = torch.randn(N, generator=g).to(DEV) if i % 3 else None
+        items.append((dy, x, dw, db))
+    items.append((items[0][0], items[0][1], items[0][2], items[0][3]))      # the same dw again
+    outs = []
+    for rep in range(2):
+        got = [(dw.clone(), db.clone() if db is not None else None) for _, _, dw, db in items]
+        seen = {}
+        batch = []
+        for (dy, x, dw, db), (gw, gb) in zip(items, got):
+            key = dw.data_ptr()
+            gw, gb = seen.get(key, (gw, gb))
+            seen[key] = (gw, gb)
+            batch.append((dy, x, gw, gb))
+        with ops.wgrad_batch():
+            for it in batch:
+                ops.wgrad_acc(*it)
+            assert ops._WGRAD_BATCH is not None and len(ops._WGRAD_BATCH[1]) == len(items)   # nothing launched yet
+        outs.append([(b[2], b[3]) for b in batch])
+    for (dy, x, dw, db), (gw, gb), (gw2, gb2) in zip(items, outs[0], outs[1]):
+        assert torch.equal(gw, gw2) and (gb is None or torch.equal(gb, gb2))
+    n0 = sum(1 for it in items if it[2].data_ptr() == items[0][2].data_ptr())
+    for i, ((dy, x, dw, db), (gw, gb)) in enumerate(zip(items, outs[0])):
+        reps = n0 if dw.data_ptr() == items[0][2].data_ptr() else 1
+        prod = dy.double().t() @ x.double()
+        ref = dw.double() + reps * prod
+        assert float((gw.double() - ref).abs().max()) / float(prod.abs().max().clamp_min(1.0)) < 1e-5, i
+        if db is not None:
+            s = dy.double().sum(0)
+            assert float((gb.double() - (db.double() + reps * s)).abs().max()) / float(s.abs().max().clamp_min(1.0)) < 1e-5
