@@ -462,7 +462,8 @@ def main():
     if prof is not None:
         prof.__exit__(None, None, None)
         with open(os.environ["RADHIP_TORCH_PROFILE"], "w") as f:
-            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="count", row_limit=250,
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="count", row_limit=int(
+                os.environ.get("RADHIP_TORCH_PROFILE_ROWS", "250")),
                                                                          max_name_column_width=40,
                                                                          max_shapes_column_width=120))
     ev1.record(stream)
