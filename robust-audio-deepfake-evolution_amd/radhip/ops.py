@@ -1498,11 +1498,9 @@ class wgrad_batch:
         return False
 
 
-def wgrad_acc_many(items):
-    """dw += dy^T x (and db += dy.sum(0)) for every (dy, x, dw, db) of `items`, each as wgrad_acc takes them, in
-    batched launches of up to WGRAD_MANY_MAX problems of one dtype. A launch holds each output once: a gradient
-    whose dw / db an earlier item of the launch already targets starts the next launch (same stream: the adds stay
-    in item order)."""
+def wgrad_groups(items):
+    """Split (dy, x, dw, db) items into launches of at most WGRAD_MANY_MAX problems of one dtype in which every dw /
+    db is targeted once, keeping item order."""
     groups, cur, seen = [], [], set()
     for it in items:
         keys = {it[2].data_ptr()} | ({it[3].data_ptr()} if it[3] is not None else set())
@@ -1513,7 +1511,15 @@ def wgrad_acc_many(items):
         seen |= keys
     if cur:
         groups.append(cur)
-    for g in groups:
+    return groups
+
+
+def wgrad_acc_many(items):
+    """dw += dy^T x (and db += dy.sum(0)) for every (dy, x, dw, db) of `items`, each as wgrad_acc takes them, in
+    batched launches of up to WGRAD_MANY_MAX problems of one dtype. A launch holds each output once: a gradient
+    whose dw / db an earlier item of the launch already targets starts the next launch (same stream: the adds stay
+    in item order)."""
+    for g in wgrad_groups(items):
         n = len(g)
         ints = lambda vals: (ctypes.c_int * n)(*vals)
         i64s = lambda vals: (ctypes.c_int64 * n)(*vals)
