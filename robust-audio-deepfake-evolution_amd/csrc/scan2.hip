@@ -187,8 +187,10 @@ __global__ __launch_bounds__(NT) void fwd_chunk_kernel(const T* __restrict__ u, 
 // b, d, n): forward rec_c <- compose(P_k, rec_k) over k < c in step order, backward over k > c nearest last (the FMA
 // chains the output kernels ran per thread before: 2 loads per chunk once instead of up to 2 x 16 in each of the
 // 512 threads of every block)
+template <int REVERSE>     // a template argument only so that profiles tell the forward's launches from the backward's
 __global__ __launch_bounds__(256) void carry_kernel(const float* __restrict__ P, float* __restrict__ recs, int64_t DN,
-                                                    int nc, int64_t total, int reverse) {
+                                                    int nc, int64_t total) {
+  constexpr bool reverse = REVERSE != 0;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= total) return;
   const int64_t db = t / DN;
@@ -425,8 +427,11 @@ __global__ __launch_bounds__(NT) void bwd_out_kernel(
 __host__ inline void launch_carry(const float* P, float* recs, int B, int L, int D, int dirs, int reverse,
                                  hipStream_t st) {
   const int64_t DN = (int64_t)D * N, total = (int64_t)dirs * B * DN;
-  hipLaunchKernelGGL(carry_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, P, recs, DN,
-                     (L + CK - 1) / CK, total, reverse);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (reverse)
+    hipLaunchKernelGGL(carry_kernel<1>, grid, dim3(256), 0, st, P, recs, DN, (L + CK - 1) / CK, total);
+  else
+    hipLaunchKernelGGL(carry_kernel<0>, grid, dim3(256), 0, st, P, recs, DN, (L + CK - 1) / CK, total);
 }
 
 }  // namespace s2
