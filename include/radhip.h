@@ -522,6 +522,18 @@ int rdx_wgrad_acc_many(int n, const void* const* dy, const int64_t* ldy, const v
                        const int* M, const int* N, const int* K, float* const* dw, const int64_t* ldw,
                        float* const* db, float* ws, int64_t ws_floats, void* stream);
 
+/* ---- AdamW over a list of fp32 tensors (csrc/optim.hip) ------------------------------------------------------
+ * torch.optim.AdamW's update (decoupled weight decay; the reference's optimizer, src/main.py:416-457) for up to
+ * rdx_adamw_many_max() tensors per call: params, grads, exp_avg, exp_avg_sq [numel[k]] fp32, step[k] the tensor's
+ * step count (a device fp32 scalar, already incremented). grad_scale (may be NULL): grads are divided by it and
+ * stored back; found_inf (may be NULL): nonzero skips the update (GradScaler's fused-optimizer contract). Each
+ * block owns 4096 elements of one tensor; the element math follows torch's fused AdamW functor (double
+ * hyper-parameters). radhip.optim.AdamW drives it and keeps torch's state layout. */
+int rdx_adamw_many_max(void);
+int rdx_adamw_many(int n, float* const* params, float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                   const float* const* step, const int64_t* numel, double lr, double beta1, double beta2,
+                   double weight_decay, double eps, const float* grad_scale, const float* found_inf, void* stream);
+
 /* ---- Timing inside replayed HIP graphs (bench instrumentation; no reference counterpart) -------
  * rdx_timestamp_acc: one-lane kernel, acc[0] += sign * wall_clock64(); acc[1] += 1 when sign == +1.
  * Launch with sign -1 before and +1 after a kernel on the same stream: acc[0] accumulates its

@@ -116,6 +116,8 @@ SIGNATURES = {
     "rdx_wgrad_acc": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rdx_wgrad_many_ws_floats": (c_i64, [c_int, c_vp, c_vp, c_vp, c_vp]),
     "rdx_wgrad_acc_many": (c_int, [c_int] + [c_vp] * 10 + [c_vp, c_i64, c_vp]),
+    "rdx_adamw_many_max": (c_int, []),
+    "rdx_adamw_many": (c_int, [c_int] + [c_vp] * 6 + [c_f64] * 5 + [c_vp, c_vp, c_vp]),
     "rdx_wgemm_counters": (c_i64, [c_int, c_int, c_int]),
     "rdx_sincconv_absmaxpool_f16mfma": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int,
                                                 c_vp, c_vp]),

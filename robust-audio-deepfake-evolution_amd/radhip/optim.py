@@ -1,0 +1,99 @@
+"""torch.optim.AdamW (the reference's optimizer, src/main.py:416-457) whose CUDA step runs csrc/optim.hip.
+
+Same parameter groups, hyper-parameters, state layout (state[p] = {"step": fp32 device scalar, "exp_avg",
+"exp_avg_sq"}) and state_dict as torch's fused AdamW, and the same GradScaler contract (`grad_scale` / `found_inf`
+set on the optimizer by GradScaler.step, steps rolled back when found_inf). torch's fused kernel deals ~64 K
+elements to a block, so the head's ~3 M parameters ran on ~50 blocks for ~0.45 ms per step; rdx_adamw_many gives
+every 4096 elements a block. Anything the kernel does not cover (CPU tensors, amsgrad, maximize, non-fp32 or
+non-contiguous tensors) takes torch's own AdamW step.
+"""
+import ctypes
+
+import torch
+
+from ._lib import check, lib, ptr_array
+
+
+class AdamW(torch.optim.AdamW):
+    _step_supports_amp_scaling = True
+
+    def __init__(self, params, **kw):
+        kw.pop("fused", None)
+        kw.pop("foreach", None)
+        super().__init__(params, foreach=False, **kw)
+
+    def _covered(self, group, ps):
+        return (all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
+                    and p.grad.is_contiguous() and not p.grad.is_sparse for p in ps)
+                and not group["amsgrad"] and not group["maximize"] and not group.get("differentiable", False)
+                and not torch.is_tensor(group["lr"]))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        grad_scale = getattr(self, "grad_scale", None)
+        found_inf = getattr(self, "found_inf", None)
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            if not self._covered(group, ps):
+                self._torch_step(group, ps, grad_scale, found_inf)
+                continue
+            ms, vs, ss = [], [], []
+            for p in ps:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                ms.append(st["exp_avg"])
+                vs.append(st["exp_avg_sq"])
+                ss.append(st["step"])
+            torch._foreach_add_(ss, 1)
+            b1, b2 = group["betas"]
+            stream = torch.cuda.current_stream(ps[0].device).cuda_stream
+            gsp = grad_scale.data_ptr() if grad_scale is not None else None
+            fip = found_inf.data_ptr() if found_inf is not None else None
+            mx = int(lib().rdx_adamw_many_max())
+            for i in range(0, len(ps), mx):
+                sl = slice(i, i + mx)
+                n = len(ps[sl])
+                check(lib().rdx_adamw_many(n, ptr_array([p.data_ptr() for p in ps[sl]]),
+                                           ptr_array([p.grad.data_ptr() for p in ps[sl]]),
+                                           ptr_array([t.data_ptr() for t in ms[sl]]),
+                                           ptr_array([t.data_ptr() for t in vs[sl]]),
+                                           ptr_array([t.data_ptr() for t in ss[sl]]),
+                                           (ctypes.c_int64 * n)(*[p.numel() for p in ps[sl]]),
+                                           float(group["lr"]), float(b1), float(b2), float(group["weight_decay"]),
+                                           float(group["eps"]), gsp, fip, stream), "adamw_many")
+            if found_inf is not None:
+                torch._foreach_sub_(ss, [found_inf] * len(ss))
+        return loss
+
+    def _torch_step(self, group, ps, grad_scale, found_inf):
+        """torch's own AdamW update for a group the kernel does not cover (same state layout)."""
+        from torch.optim.adamw import adamw
+        ms, vs, mxs, ss = [], [], [], []
+        for p in ps:
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device) if p.is_cuda else torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                if group["amsgrad"]:
+                    st["max_exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            ms.append(st["exp_avg"])
+            vs.append(st["exp_avg_sq"])
+            ss.append(st["step"])
+            if group["amsgrad"]:
+                mxs.append(st["max_exp_avg_sq"])
+        b1, b2 = group["betas"]
+        fused = all(p.is_cuda for p in ps)      # torch's fused form is the one that takes grad_scale / found_inf
+        adamw(ps, [p.grad for p in ps], ms, vs, mxs, ss, foreach=False, capturable=False, differentiable=False,
+              fused=fused or None, grad_scale=grad_scale, found_inf=found_inf, amsgrad=group["amsgrad"], beta1=b1, beta2=b2,
+              lr=group["lr"], weight_decay=group["weight_decay"], eps=group["eps"], maximize=group["maximize"],
+              has_complex=False)

@@ -402,10 +402,15 @@ class Trainer:
                   {"params": [], "lr": oc["base_lr"]}]
         if param_groups is not None:
             groups = param_groups
-        try:
-            self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"], fused=True)
-        except (RuntimeError, TypeError):
-            self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"])
+        if self.device.type == "cuda" and os.environ.get("RADHIP_ADAMW", "1") != "0":
+            # torch.optim.AdamW's update on csrc/optim.hip (same state and GradScaler contract; radhip/optim.py)
+            from .optim import AdamW as RdxAdamW
+            self.opt = RdxAdamW(groups, weight_decay=oc["weight_decay"])
+        else:
+            try:
+                self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"], fused=True)
+            except (RuntimeError, TypeError):
+                self.opt = torch.optim.AdamW(groups, weight_decay=oc["weight_decay"])
         # --- FGM (main.py:514-544): unfreeze feature_projection, add it as its own group at wavlm_lr.
         # The reference adds this group AFTER building its LR schedulers; on torch >= 2.x that makes
         # SequentialLR's milestone step fail (strict zip over param groups), and on older torch the
