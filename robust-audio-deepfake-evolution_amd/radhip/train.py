@@ -206,11 +206,25 @@ class FlatGrads:
         dev = self.params[0].device
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
         off = 0
+        self._ptrs = []
         for p in self.params:
             n = p.numel()
             assert p.dtype == torch.float32
             p.grad = self.flat[off:off + n].view_as(p)
+            self._ptrs.append(p.grad.data_ptr())
             off += n
+
+    def bound(self):
+        """True while every parameter's .grad is still its view of the flat buffer."""
+        return all(p.grad is not None and p.grad.data_ptr() == q for p, q in zip(self.params, self._ptrs))
+
+    def clip_norm_(self, max_norm):
+        """torch.nn.utils.clip_grad_norm_ over the parameters (error_if_nonfinite off) on the flat buffer: the total
+        2-norm in one reduction and min(1, max_norm / (norm + 1e-6)) applied in one multiply, instead of a norm per
+        tensor (torch's multi-tensor kernels deal 64 K elements per block: ~0.1 ms per step for these ~3 M)."""
+        norm = torch.linalg.vector_norm(self.flat, 2)
+        self.flat.mul_(torch.clamp(max_norm / (norm + 1e-6), max=1.0))
+        return norm
 
     def zero(self):
         self.flat.zero_()
@@ -522,7 +536,10 @@ class Trainer:
     def optimizer_step(self):
         self.grads.all_reduce_mean(self.group)
         self.scaler.unscale_(self.opt)
-        torch.nn.utils.clip_grad_norm_(self.params, max_norm=3.0, foreach=True)
+        if self.grads.bound():
+            self.grads.clip_norm_(3.0)
+        else:
+            torch.nn.utils.clip_grad_norm_(self.params, max_norm=3.0, foreach=True)
         self.scaler.step(self.opt)
         self.scaler.update()
         self.grads.zero()
