@@ -503,6 +503,23 @@ int rdx_pgemm_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, void*
 int rdx_pgemm_prof(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                    const void* bias, int tile, int group_m, void* prof, void* stream);
 
+/* ---- Ping-pong MFMA GEMM of the WavLM encoder projections (csrc/hgemm.hip) -------------------------------------
+ * Same operands, layouts and epilogues as rdx_wgemm_bf16_ex (K % 64 == 0; q/k/v, out_proj, FFN1, FFN2 and their input
+ * gradients of HF WavLMEncoderLayerStableLayerNorm, src/models/DualStreamSEMamba.py:292-439, under the autocast of
+ * src/main.py:1049), on one 512-thread workgroup per output tile (or per split of one): 8 waves as 2 x 4, the two row
+ * groups one barrier apart so each SIMD pairs one wave's MFMA segment with its partner's LDS reads and LDS-DMA issue,
+ * a ring of 8 KB slabs refilled one phase after they are read (counted vmcnt, never drained in the loop). tile codes
+ * (csrc/hgemm.hip hg::geometry): 0 = 256 x 256, 1 = 256 x 192, 2 = 128 x 256, 3 = 128 x 192, 4 = 128 x 128,
+ * 5 = 256 x 128; + 100: s_setprio(1) around every MFMA segment, + 200: static priority 1 for the second row group.
+ * group_m: XCD-contiguous runs ordered group_m row tiles x every column tile (0 = column-panel order). splits > 1:
+ * split-K with an in-launch last-arriver sum in split order (deterministic); ws / counters as rdx_wgemm_bf16_ex
+ * (rdx_hgemm_ws_bytes, rdx_hgemm_counters), one workspace per stream. */
+int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+              const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out, int64_t ldao, int tile,
+              int splits, int group_m, void* ws, int64_t ws_bytes, int* counters, int64_t n_counters, void* stream);
+int64_t rdx_hgemm_ws_bytes(int M, int N, int tile, int splits);
+int64_t rdx_hgemm_counters(int M, int N, int tile);
+
 /* ---- Weight / bias gradients of the head's linears, accumulated in fp32 (csrc/wgrad.hip) ----------------
  * dW[n][k] += sum_m dY[m][n] X[m][k], db[n] += sum_m dY[m][n] (db may be NULL): bf16 dY [M, ldy] and X [M, ldx],
  * fp32 dW [N, ldw] (the flat gradient buffer's views), the token rows split over the chip in chunks of

@@ -1,0 +1,526 @@
+// Ping-pong MFMA GEMM for the WavLM encoder projections on gfx950: the q/k/v, out_proj, FFN1, FFN2 GEMMs of HF
+// WavLMEncoderLayerStableLayerNorm and their input gradients (src/models/DualStreamSEMamba.py:292-439, run under
+// autocast, src/main.py:1049), at M = B x 201 token rows (B = 8: 1608, B = 32: 6432).
+//
+//   C[M, N] = A[M, K] . B[N, K]^T     (both operands K-contiguous; the epilogues of csrc/wgemm.hip)
+//
+// Structure (cdna_hip_programming.md "The 256^2 8-phase template", MI355X_MICROARCH.md "Two waves per SIMD"):
+//   * one 512-thread workgroup per CU: 8 waves as 2 (M) x 4 (N), two per SIMD. Waves 0-3 (row group 0) and 4-7
+//     (row group 1) run staggered by one s_barrier, so on every SIMD one wave is in its MFMA segment while its
+//     partner reads fragments from LDS and issues LDS-DMA loads;
+//   * a 64-deep K step is cut into NPH = NPA x NPB phases, each the MFMAs of one (A part, B part) pair of the
+//     wave's tile (snake order, so every fragment is read from LDS once per K step and stays in registers while
+//     needed); a phase is [fragment reads, LDS-DMA issue, counted vmcnt + lgkmcnt(0)] s_barrier [MFMA] s_barrier;
+//   * the LDS is a ring of S = U x SPK slabs of 64 rows x 64 k (8 KB, one buffer_load_dwordx4 ... lds per thread).
+//     A K step's slabs are ordered by the phase that first reads them; a slab read in phase p is refilled in phase
+//     p + 1 with the same slab of K step kt + U (the read was retired by lgkmcnt(0) before the barrier the refill
+//     follows), so S - (slabs read in phases p and p + 1) slabs stay in flight across every barrier, and phase p's
+//     counted vmcnt retires exactly the slabs phase p + 1 reads. Past the last K step the refills take a buffer
+//     descriptor of zero records (no memory traffic; the count stays exact);
+//   * LDS images are 128-B rows with the 16-byte chunk XOR-swizzled by (row >> 1) & 7 (conflict-free
+//     ds_read_b128 for the 16x16x32 fragments), applied to the DMA's SOURCE chunk (the DMA writes lane-linear);
+//     a slab's 64 image rows gather the tile rows its phase reads (any row order is free for the per-lane
+//     source address); rows >= M / N read as zeros through the buffer range;
+//   * v_mfma_f32_16x16x32 computing C^T: a lane ends with 4 consecutive output columns of one row;
+//   * work ids are dealt to XCDs in contiguous runs (bijective remap), then GROUP_M row tiles x every column tile
+//     per group; split-K (splits > 1): the splits of a tile are consecutive work ids, publish fp32 partials and
+//     the last arriver sums them in split order (deterministic) and runs the epilogue;
+//   * epilogue through an LDS image of the tile (16-byte padded rows), whole rows stored 16 bytes per lane.
+#include <utility>
+
+#include "common.h"
+
+namespace rdx {
+namespace hg {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+__device__ void buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds, int size, int voffset,
+                                int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ i32x4 rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)(uint32_t)(a >> 32);
+  r.z = (int)bytes;
+  r.w = 0x00020000;  // raw buffer: dword-aligned, no swizzle, range-checked
+  return r;
+}
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return hpack2(a, b); }
+
+template <int N, class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
+struct Args {
+  const hst* A;
+  int64_t lda;
+  const hst* B;
+  int64_t ldb;
+  hst* C;
+  int64_t ldc;
+  int M, N, K;
+  const hst* bias;   // [N] or null
+  const hst* aux;    // GELU_BWD: u [M, ldaux]
+  int64_t ldaux;
+  hst* aux_out;      // BIAS_GELU: gelu(u) [M, ldao]
+  int64_t ldao;
+  int tiles_m, tiles_n, group_m;
+  int splits;        // split-K factor; split s covers k-steps [s*nk/S, (s+1)*nk/S)
+  float* ws;         // split-K partial slabs [tile][split][FM*FN][512][4] fp32
+  int* counters;     // split-K arrival tickets, one per tile, zero between launches
+  int wide;          // C / aux / aux_out rows 16-byte aligned: 16-byte row-phase accesses
+};
+
+// The phase / slab plan of a BM x BN tile with its A part split NPA ways and its B part NPB ways.
+template <int BM, int BN, int NPA, int NPB>
+struct Plan {
+  static constexpr int FM = BM / 32, FN = BN / 64;        // 16x16 fragments per wave (2 x 4 waves)
+  static constexpr int WTM = BM / 2, WTN = BN / 4;
+  static constexpr int FMP = FM / NPA, FNP = FN / NPB;    // fragments of one part
+  static constexpr int RA = WTM / NPA, RB = WTN / NPB;    // rows of one wave's part
+  static constexpr int SA = BM / NPA / 64, SB = BN / NPB / 64;   // slabs of one part (both groups / all 4 waves)
+  static constexpr int NPH = NPA * NPB;
+  static constexpr int SPK = BM / 64 + BN / 64;           // slabs per K step
+  static_assert(FM % NPA == 0 && FN % NPB == 0 && (BM / NPA) % 64 == 0 && (BN / NPB) % 64 == 0, "plan");
+  static constexpr int pa(int q) { return q / NPB; }
+  static constexpr int pb(int q) { return ((q / NPB) & 1) ? NPB - 1 - q % NPB : q % NPB; }
+  static constexpr bool anew(int q) { return q % NPB == 0; }
+  static constexpr bool bnew(int q) { return q < NPB; }
+  static constexpr int reads(int q) { return (anew(q) ? SA : 0) + (bnew(q) ? SB : 0); }
+  static constexpr int first(int q) { return q == 0 ? 0 : first(q - 1) + reads(q - 1); }
+  // slab index (in the K step's read order) of A part a / B part b
+  static constexpr int ja(int a) { return first(a * NPB); }
+  static constexpr int jb(int b) { return first(b) + (anew(b) ? SA : 0); }
+  // slab j -> (is B, part, slab within part)
+  static constexpr int slab_isb(int j) {
+    for (int q = 0; q < NPH; ++q) {
+      const int f = first(q);
+      if (j >= f && j < f + reads(q)) return (anew(q) && j < f + SA) ? 0 : 1;
+    }
+    return -1;
+  }
+  static constexpr int slab_part(int j) {
+    for (int q = 0; q < NPH; ++q) {
+      const int f = first(q);
+      if (j >= f && j < f + reads(q)) return (anew(q) && j < f + SA) ? pa(q) : pb(q);
+    }
+    return -1;
+  }
+  static constexpr int slab_in_part(int j) {
+    for (int q = 0; q < NPH; ++q) {
+      const int f = first(q);
+      if (j >= f && j < f + reads(q)) return (anew(q) && j < f + SA) ? j - f : j - f - (anew(q) ? SA : 0);
+    }
+    return -1;
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO>
+__global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
+  using P = Plan<BM, BN, NPA, NPB>;
+  constexpr int FM = P::FM, FN = P::FN, WTM = P::WTM, WTN = P::WTN, FMP = P::FMP, FNP = P::FNP;
+  constexpr int NPH = P::NPH, SPK = P::SPK, S = U * SPK;
+  constexpr int SLAB = 8192;
+  static_assert(S * SLAB <= 160 * 1024, "ring");
+  extern __shared__ __attribute__((aligned(1024))) char lds[];
+
+  // work id -> (tile, split) -> (mt, nt)
+  const int SPL = g.splits;
+  const int nwg = g.tiles_m * g.tiles_n * SPL;
+  int t;
+  {
+    const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tile = t / SPL, split = t - tile * SPL;
+  int mt, nt;
+  {
+    const int gm = g.group_m;
+    if (gm <= 0 || gm >= g.tiles_m) {
+      nt = tile / g.tiles_m;
+      mt = tile - nt * g.tiles_m;
+    } else {
+      const int per = gm * g.tiles_n, grp = tile / per, first = grp * gm;
+      const int gsz = min(g.tiles_m - first, gm), rem = tile - grp * per;
+      nt = rem / gsz;
+      mt = first + (rem - nt * gsz);
+    }
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int M = g.M, N = g.N, K = g.K;
+  const int nk_all = K / 64;
+  const int kb = split * nk_all / SPL, nk = (split + 1) * nk_all / SPL - kb;
+
+  const int64_t lda_b = g.lda * 2, ldb_b = g.ldb * 2;
+  const int rows_a = min(BM, M - m0), rows_b = min(BN, N - n0);
+  const i32x4 ra = rsrc(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)(rows_a - 1) * lda_b + (int64_t)K * 2));
+  const i32x4 rb = rsrc(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(rows_b - 1) * ldb_b + (int64_t)K * 2));
+  const i32x4 rnull = rsrc(g.A, 0u);
+
+  // loop-invariant DMA source offsets of this lane, one per slab of a K step: image row ir = 8 * wave + lane / 8,
+  // position lane % 8 holding source chunk swz(ir, lane % 8)
+  int voff[SPK];
+  {
+    const int ir = 8 * wave + (lane >> 3), ch = swz(ir, lane & 7);
+    static_for<SPK>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      constexpr int isb = P::slab_isb(j), part = P::slab_part(j), sip = P::slab_in_part(j);
+      const int rr = sip * 64 + ir;
+      int row;
+      if constexpr (isb == 0) row = (rr / P::RA) * WTM + part * P::RA + rr % P::RA;
+      else row = (rr / P::RB) * WTN + part * P::RB + rr % P::RB;
+      voff[j] = (int)(row * (isb ? ldb_b : lda_b)) + ch * 16;
+    });
+  }
+  // issue slab j of K step kst into ring position pos (slot pos * SPK + j)
+  auto issue = [&](auto JC, int pos, int kst) {
+    constexpr int j = decltype(JC)::value;
+    constexpr int isb = P::slab_isb(j);
+    const bool live = kst < nk;
+    const i32x4 rs = live ? (isb ? rb : ra) : rnull;
+    const int kbytes = live ? (kb + kst) * 128 : 0;
+    buffer_load_lds(rs, (__attribute__((address_space(3))) uint32_t*)(lds + (pos * SPK + j) * SLAB + wave * 1024),
+                    16, voff[j], kbytes, 0, 0);
+  };
+
+  // per-lane fragment read offsets: row fr of a 16-row fragment, chunk kk * 4 + fq, swizzled by the row
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fr >> 1) & 7;
+  const int lofs0 = fr * 128 + 16 * ((0 * 4 + fq) ^ sw), lofs1 = fr * 128 + 16 * ((1 * 4 + fq) ^ sw);
+  const int arow0 = wm * P::RA, brow0 = wn * P::RB;
+
+  hx8 af[2][FM], bf[2][FN];
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the whole ring (K steps 0 .. U - 1), then retire what phase 0 reads
+#pragma unroll
+  for (int u = 0; u < U; ++u) static_for<SPK>([&](auto JC) { issue(JC, u, u); });
+  wait_barrier<S - P::reads(0)>();
+  __builtin_amdgcn_sched_barrier(0);
+  if (wm == 1) __builtin_amdgcn_s_barrier();     // row group 1 runs one barrier behind group 0
+  __builtin_amdgcn_sched_barrier(0);
+  if (PRIO == 2 && wm == 1) __builtin_amdgcn_s_setprio(1);
+
+  // one phase q of K step kt held at ring position u
+  auto phase = [&](auto UC, auto QC, int kt) {
+    constexpr int u = decltype(UC)::value, q = decltype(QC)::value;
+    constexpr int a = P::pa(q), b = P::pb(q);
+    // 1. this phase's first reads
+    if constexpr (P::anew(q)) {
+      const char* base = lds + (u * SPK + P::ja(a)) * SLAB + arow0 * 128;
+#pragma unroll
+      for (int i = 0; i < FMP; ++i) {
+        af[0][a * FMP + i] = *reinterpret_cast<const hx8*>(base + i * 2048 + lofs0);
+        af[1][a * FMP + i] = *reinterpret_cast<const hx8*>(base + i * 2048 + lofs1);
+      }
+    }
+    if constexpr (P::bnew(q)) {
+      const char* base = lds + (u * SPK + P::jb(b)) * SLAB + brow0 * 128;
+#pragma unroll
+      for (int j = 0; j < FNP; ++j) {
+        bf[0][b * FNP + j] = *reinterpret_cast<const hx8*>(base + j * 2048 + lofs0);
+        bf[1][b * FNP + j] = *reinterpret_cast<const hx8*>(base + j * 2048 + lofs1);
+      }
+    }
+    // 2. refill the slabs the previous phase read, with the same slabs U K steps later
+    if constexpr (q >= 1) {
+      constexpr int f = P::first(q - 1), n = P::reads(q - 1);
+      static_for<n>([&](auto IC) { issue(std::integral_constant<int, f + decltype(IC)::value>{}, u, kt + U); });
+    } else {
+      constexpr int f = P::first(NPH - 1), n = P::reads(NPH - 1);
+      constexpr int up = (u + U - 1) % U;
+      if (n > 0 && kt > 0)
+        static_for<n>([&](auto IC) { issue(std::integral_constant<int, f + decltype(IC)::value>{}, up, kt - 1 + U); });
+    }
+    // 3. retire this phase's reads and the slabs the next phase reads; meet the partner group
+    wait_barrier<S - P::reads(q) - P::reads((q + 1) % NPH)>();
+    __builtin_amdgcn_sched_barrier(0);
+    // 4. MFMA segment
+    if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < FMP; ++i)
+#pragma unroll
+        for (int j = 0; j < FNP; ++j)
+          acc[a * FMP + i][b * FNP + j] =
+              mfma16x16x32(bf[kk][b * FNP + j], af[kk][a * FMP + i], acc[a * FMP + i][b * FNP + j]);
+    if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto kstep = [&](auto UC, int kt) {
+    static_for<NPH>([&](auto QC) { phase(UC, QC, kt); });
+  };
+
+  for (int kt = 0; kt < nk; kt += U) {
+    kstep(std::integral_constant<int, 0>{}, kt);
+    static_for<U - 1>([&](auto IC) {
+      constexpr int u = decltype(IC)::value + 1;
+      if (kt + u < nk) kstep(std::integral_constant<int, u>{}, kt + u);
+    });
+  }
+  if (PRIO == 2 && wm == 1) __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
+  if (wm == 0) __builtin_amdgcn_s_barrier();     // group 0 catches up with group 1's last barrier
+  __builtin_amdgcn_sched_barrier(0);
+  wait_barrier<0>();                              // the trailing zero-record refills have landed too
+
+  // split-K: publish this split's fp32 partial (fragment order), take a ticket; the last arriver sums the
+  // partials in split order (cdna_hip_programming.md "Projection GEMM at M = 256" item 2)
+  if (SPL > 1) {
+    constexpr int NT = 512;
+    float* slab = g.ws + (int64_t)tile * SPL * (FM * FN * NT * 4);
+    {
+      float* mine = slab + (int64_t)split * (FM * FN * NT * 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(mine + ((i * FN + j) * NT + tid) * 4) = acc[i][j];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(g.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = ticket;
+      if (ticket == SPL - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        g.counters[tile] = 0;
+      }
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(flag[0]) != SPL - 1) return;
+    __syncthreads();                              // every wave has read the flag before the image overwrites it
+    // the sum in split order, every partial (this split's included) read back from its slab
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = *reinterpret_cast<const f32x4*>(slab + ((i * FN + j) * NT + tid) * 4);
+    for (int s2 = 1; s2 < SPL; ++s2) {
+      const float* ps = slab + (int64_t)s2 * (FM * FN * NT * 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += *reinterpret_cast<const f32x4*>(ps + ((i * FN + j) * NT + tid) * 4);
+    }
+  }
+
+  // epilogue: acc[i][j][e] = C[m0 + wm*WTM + i*16 + fr][n0 + wn*WTN + j*16 + 4*fq + e], through an LDS image
+  constexpr int PITCH = BN * 2 + 16;
+  static_assert(BM * PITCH <= 160 * 1024, "epilogue image");
+  char* img = lds;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int r = wm * WTM + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = wn * WTN + j * 16 + 4 * fq;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (EPI != RDX_EPI_GELU_BWD && g.bias && n0 + c < N) {
+        const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n0 + c);
+        v[0] += hlo(bb.x);
+        v[1] += hhi(bb.x);
+        v[2] += hlo(bb.y);
+        v[3] += hhi(bb.y);
+      }
+      *reinterpret_cast<uint2*>(img + r * PITCH + c * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+#pragma unroll 4
+  for (int idx = tid; idx < BM * CPR; idx += 512) {
+    const int r = idx / CPR, c = (idx - r * CPR) * 8;
+    const int m = m0 + r, n = n0 + c;
+    if (m >= M || n >= N) continue;
+    const bool full = n + 8 <= N;
+    const bool wide = full && g.wide;
+    auto ld8 = [&](const hst* src) -> uint4 {
+      if (wide) return *reinterpret_cast<const uint4*>(src);
+      const uint2 lo = *reinterpret_cast<const uint2*>(src);
+      const uint2 hi = full ? *reinterpret_cast<const uint2*>(src + 4) : make_uint2(0u, 0u);
+      return make_uint4(lo.x, lo.y, hi.x, hi.y);
+    };
+    auto st8 = [&](hst* dst, uint4 v) {
+      if (wide) { *reinterpret_cast<uint4*>(dst) = v; return; }
+      *reinterpret_cast<uint2*>(dst) = make_uint2(v.x, v.y);
+      if (full) *reinterpret_cast<uint2*>(dst + 4) = make_uint2(v.z, v.w);
+    };
+    uint4 qv = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
+    if (EPI == RDX_EPI_GELU_BWD) {
+      const uint4 uu = ld8(g.aux + (int64_t)m * g.ldaux + n);
+      const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w}, uw[4] = {uu.x, uu.y, uu.z, uu.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2(hlo(qw[e]) * gelu_grad(hlo(uw[e])), hhi(qw[e]) * gelu_grad(hhi(uw[e])));
+      qv = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    st8(g.C + (int64_t)m * g.ldc + n, qv);
+    if (EPI == RDX_EPI_BIAS_GELU) {
+      const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2(gelu(hlo(qw[e])), gelu(hhi(qw[e])));
+      st8(g.aux_out + (int64_t)m * g.ldao + n, make_uint4(o[0], o[1], o[2], o[3]));
+    }
+  }
+}
+
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO>
+static int launch(Args g, hipStream_t st) {
+  g.tiles_m = (g.M + BM - 1) / BM;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  constexpr int ring = U * (BM / 64 + BN / 64) * 8192, image = BM * (BN * 2 + 16);
+  constexpr int lds = ring > image ? ring : image;
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO>;
+  static bool lds_ok = false;
+  if (!lds_ok) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    lds_ok = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(g.tiles_m * g.tiles_n * g.splits)), dim3(512), lds, st, g);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
+// tile codes (BM x BN, A / B parts, ring K steps); + 100: s_setprio(1) around each MFMA segment; + 200: static
+// priority 1 for row group 1
+template <int EPI, int PRIO>
+static int dispatch(const Args& g, int tile, hipStream_t st) {
+  switch (tile) {
+    case 0: return launch<256, 256, 2, 2, 2, EPI, PRIO>(g, st);   // 16 slabs, 128 KB
+    case 1: return launch<256, 192, 2, 1, 2, EPI, PRIO>(g, st);   // 14 slabs
+    case 2: return launch<128, 256, 1, 2, 3, EPI, PRIO>(g, st);   // 18 slabs
+    case 3: return launch<128, 192, 2, 1, 4, EPI, PRIO>(g, st);   // 20 slabs
+    case 4: return launch<128, 128, 1, 1, 4, EPI, PRIO>(g, st);   // 16 slabs
+    case 5: return launch<256, 128, 2, 1, 3, EPI, PRIO>(g, st);   // 18 slabs
+    default: return RDX_EINVAL;
+  }
+}
+
+static bool geometry(int tile, int* bm, int* bn) {
+  switch (tile % 100) {
+    case 0: *bm = 256; *bn = 256; return true;
+    case 1: *bm = 256; *bn = 192; return true;
+    case 2: *bm = 128; *bn = 256; return true;
+    case 3: *bm = 128; *bn = 192; return true;
+    case 4: *bm = 128; *bn = 128; return true;
+    case 5: *bm = 256; *bn = 128; return true;
+    default: return false;
+  }
+}
+
+}  // namespace hg
+}  // namespace rdx
+
+using namespace rdx;
+
+extern "C" int64_t rdx_hgemm_ws_bytes(int M, int N, int tile, int splits) {
+  int bm, bn;
+  if (splits <= 1) return 0;
+  if (tile < 0 || tile >= 300 || !hg::geometry(tile, &bm, &bn)) return -1;
+  const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  return tiles * splits * (int64_t)bm * bn * 4;
+}
+
+extern "C" int64_t rdx_hgemm_counters(int M, int N, int tile) {
+  int bm, bn;
+  if (tile < 0 || tile >= 300 || !hg::geometry(tile, &bm, &bn)) return -1;
+  return (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+}
+
+extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N,
+                         int K, const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out,
+                         int64_t ldao, int tile, int splits, int group_m, void* ws, int64_t ws_bytes, int* counters,
+                         int64_t n_counters, void* stream) {
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  RDX_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0 && al(A, 16) && al(B, 16) && al(C, 8));
+  RDX_REQUIRE(K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K && N % 4 == 0 && ldc >= N &&
+              ldc % 4 == 0);
+  // 32-bit buffer ranges and source offsets
+  RDX_REQUIRE((int64_t)M * lda * 2 < 0x7fffffffLL && (int64_t)N * ldb * 2 < 0x7fffffffLL);
+  RDX_REQUIRE(!bias || al(bias, 8));
+  RDX_REQUIRE(epilogue == RDX_EPI_BIAS || epilogue == RDX_EPI_BIAS_GELU || epilogue == RDX_EPI_GELU_BWD);
+  if (epilogue == RDX_EPI_BIAS_GELU) RDX_REQUIRE(aux_out && ldao >= N && ldao % 4 == 0 && al(aux_out, 8));
+  if (epilogue == RDX_EPI_GELU_BWD) RDX_REQUIRE(aux && ldaux >= N && ldaux % 4 == 0 && al(aux, 8));
+  int bm, bn;
+  RDX_REQUIRE(tile >= 0 && tile < 300 && hg::geometry(tile, &bm, &bn));
+  RDX_REQUIRE(group_m >= 0);
+  RDX_REQUIRE(splits >= 1 && splits <= 16 && splits <= K / 64);
+  if (splits > 1) {
+    const int64_t need = rdx_hgemm_ws_bytes(M, N, tile, splits), nc = rdx_hgemm_counters(M, N, tile);
+    RDX_REQUIRE(need > 0 && ws && al(ws, 16) && ws_bytes >= need && counters && n_counters >= nc);
+  }
+  hg::Args g;
+  g.A = (const hst*)A;
+  g.lda = lda;
+  g.B = (const hst*)B;
+  g.ldb = ldb;
+  g.C = (hst*)C;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.bias = (const hst*)bias;
+  g.aux = (const hst*)aux;
+  g.ldaux = ldaux;
+  g.aux_out = (hst*)aux_out;
+  g.ldao = ldao;
+  g.tiles_m = g.tiles_n = 0;
+  g.group_m = group_m;
+  g.splits = splits;
+  g.ws = (float*)ws;
+  g.counters = counters;
+  g.wide = al(C, 16) && ldc % 8 == 0;
+  if (epilogue == RDX_EPI_BIAS_GELU) g.wide = g.wide && al(aux_out, 16) && ldao % 8 == 0;
+  if (epilogue == RDX_EPI_GELU_BWD) g.wide = g.wide && al(aux, 16) && ldaux % 8 == 0;
+  hipStream_t st = as_stream(stream);
+  const int prio = tile / 100, base = tile % 100;
+  switch (epilogue) {
+    case RDX_EPI_BIAS:
+      return prio == 0 ? hg::dispatch<RDX_EPI_BIAS, 0>(g, base, st)
+           : prio == 1 ? hg::dispatch<RDX_EPI_BIAS, 1>(g, base, st) : hg::dispatch<RDX_EPI_BIAS, 2>(g, base, st);
+    case RDX_EPI_BIAS_GELU:
+      return prio == 0 ? hg::dispatch<RDX_EPI_BIAS_GELU, 0>(g, base, st)
+           : prio == 1 ? hg::dispatch<RDX_EPI_BIAS_GELU, 1>(g, base, st)
+                       : hg::dispatch<RDX_EPI_BIAS_GELU, 2>(g, base, st);
+    default:
+      return prio == 0 ? hg::dispatch<RDX_EPI_GELU_BWD, 0>(g, base, st)
+           : prio == 1 ? hg::dispatch<RDX_EPI_GELU_BWD, 1>(g, base, st)
+                       : hg::dispatch<RDX_EPI_GELU_BWD, 2>(g, base, st);
+  }
+}

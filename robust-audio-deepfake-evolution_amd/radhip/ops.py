@@ -1431,6 +1431,8 @@ def wgemm_policy(name, M, N, K):
         return None
     if ent[0] == "pg":
         return ("pg", int(ent[1]), int(ent[2]))
+    if ent[0] == "hg":
+        return ("hg", int(ent[1]), int(ent[2]), int(ent[3]))
     return (int(ent[0]), int(ent[1]))
 
 
@@ -1438,6 +1440,8 @@ def layer_gemm(pol, a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None):
     """Run a WavLM layer GEMM C = a @ b^T (+ epilogue) on the kernel `pol` names (wgemm_policy, not None)."""
     if pol[0] == "pg":
         return pgemm(a, b, bias, epilogue=epilogue, aux=aux, tile=pol[1], group_m=pol[2])
+    if pol[0] == "hg":
+        return hgemm(a, b, bias, epilogue=epilogue, aux=aux, tile=pol[1], splits=pol[2], group_m=pol[3])
     return wgemm(a, b, bias, epilogue=epilogue, aux=aux, tile=pol[0], splits=pol[1])
 
 
@@ -1624,6 +1628,43 @@ def pgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
                                    _p(aux_out) if aux_out is not None else None,
                                    aux_out.stride(0) if aux_out is not None else 0, int(tile), int(group_m),
                                    _stream(a)), "pgemm_bf16")
+    return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
+
+
+def hgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=0, splits=1, group_m=0,
+          name="hgemm"):
+    """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/hgemm.hip (8-wave ping-pong MFMA GEMM with a slab
+    ring, one workgroup per output tile or split): 16-bit (bf16 / fp16) row views a, b (unit inner stride, 16-byte
+    aligned, K % 64 == 0); returns C, or (C, gelu(C)) for EPI_BIAS_GELU. splits > 1: split-K with the in-launch
+    last-arriver sum (the per-stream workspace of wgemm)."""
+    _require_gpu(a, b)
+    if a.dtype not in HALF or b.dtype != a.dtype or a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("radhip hgemm: bf16 / fp16 operands of one dtype with unit inner stride required")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2 or K % 64:
+        raise ValueError(f"radhip hgemm: K {K} vs {K2} (K % 64 == 0 required)")
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=a.dtype)
+    if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
+        aux_out = torch.empty(M, N, device=a.device, dtype=a.dtype)
+    ws = cnt = None
+    ws_bytes = n_cnt = 0
+    if splits > 1:
+        ws_bytes = int(lib().rdx_hgemm_ws_bytes(M, N, int(tile), int(splits)))
+        n_cnt = int(lib().rdx_hgemm_counters(M, N, int(tile)))
+        if ws_bytes <= 0 or n_cnt <= 0:
+            raise ValueError(f"radhip hgemm: no split-K geometry for tile {tile}")
+        ws, cnt = _wgemm_workspace(a.device, ws_bytes, n_cnt)
+        ws_bytes, n_cnt = ws.numel(), cnt.numel()
+    with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
+        check(_L(a).rdx_hgemm(_p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0), M, N, K,
+                              _p(bias) if bias is not None else None, int(epilogue),
+                              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                              _p(aux_out) if aux_out is not None else None,
+                              aux_out.stride(0) if aux_out is not None else 0, int(tile), int(splits), int(group_m),
+                              _p(ws) if ws is not None else None, ws_bytes, _p(cnt) if cnt is not None else None,
+                              n_cnt, _stream(a)), "hgemm")
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
 
 

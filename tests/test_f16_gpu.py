@@ -26,7 +26,8 @@ def _gelu(x):
 
 # --------------------------------------------------------------------------------------- GEMMs ----
 GEMMS = [("wgemm", dict(tile=5)), ("wgemm", dict(tile=6)), ("wgemm", dict(tile=12, splits=4)),
-         ("pgemm", dict(tile=4, group_m=4)), ("pgemm", dict(tile=5, group_m=0)), ("gemm", {})]
+         ("pgemm", dict(tile=4, group_m=4)), ("pgemm", dict(tile=5, group_m=0)), ("gemm", {}),
+         ("hgemm", dict(tile=0)), ("hgemm", dict(tile=2)), ("hgemm", dict(tile=4, splits=2))]
 
 
 @pytest.mark.parametrize("kind,kw", GEMMS)

@@ -254,3 +254,54 @@ def test_pgemm_probe_stamps():
     d = prof.cpu()
     assert bool(((d[:, 0] <= d[:, 1]) & (d[:, 1] <= d[:, 2]) & (d[:, 2] <= d[:, 3])).all())
     assert bool((d[:, 5] >= d[:, 4]).all())
+
+
+# ---- csrc/hgemm.hip: the 8-wave ping-pong GEMM with the slab ring (every tile, split-K, group orders) ----
+HG_TILES = [0, 1, 2, 3, 4, 5, 100, 202]
+
+
+@pytest.mark.parametrize("tile", HG_TILES)
+@pytest.mark.parametrize("M,N,K,splits,gm", [(1608, 1024, 1024, 1, 4), (333, 3072, 1024, 1, 0),
+                                             (1608, 4096, 128, 1, 2), (64, 768, 4096, 1, 1),
+                                             (6432, 1024, 192, 1, 8), (1608, 1024, 4096, 2, 0),
+                                             (200, 1000, 1024, 3, 0), (130, 260, 128, 2, 1)])
+def test_hgemm_bias_every_tile(tile, M, N, K, splits, gm):
+    """Row tails (rows past M read as zeros through the buffer range), ragged column tiles (N % 8 == 4 takes the
+    8-byte row phase), K of 2-3 steps (shorter than the ring: the refills past the last step take the zero-record
+    descriptor) up to deep K, split-K with the last-arriver sum, every group order."""
+    from radhip.ops import hgemm
+    a, b, bias = _ops(M, N, K, seed=tile + gm + splits)
+    got = hgemm(a, b, bias, tile=tile, splits=splits, group_m=gm)
+    assert got.dtype == torch.bfloat16 and got.shape == (M, N)
+    assert _rel(got, a.float() @ b.float().t() + bias.float()) < 1e-2
+    assert _rel(hgemm(a, b, tile=tile, splits=splits, group_m=gm), a.float() @ b.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("tile,splits", [(0, 1), (2, 1), (3, 1), (4, 2), (1, 1)])
+def test_hgemm_epilogues_match_wgemm(tile, splits):
+    """The bias / bias + GELU / GELU-backward epilogues round where csrc/wgemm.hip's do (bf16 rounding of C, the
+    aux output gelu(u) of the stored u); split-K sums in split order, so two launches give the same bits."""
+    from radhip import _lib
+    from radhip.ops import hgemm, wgemm
+    a, b, bias = _ops(1608, 3072, 1024, seed=5)
+    u, v = hgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=tile, splits=splits)
+    u2, v2 = wgemm(a, b, bias, epilogue=_lib.EPI_BIAS_GELU, tile=5)
+    assert float((u.float() - u2.float()).abs().max()) <= 2 ** -7 * float(u2.float().abs().max())
+    ref_v = torch.nn.functional.gelu(u.float())
+    assert float((v.float() - ref_v.to(torch.bfloat16).float()).abs().max()) <= 2 ** -7 * float(ref_v.abs().max())
+    uu = torch.randn(1608, 3072, device=DEV).to(torch.bfloat16)
+    du = hgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile, splits=splits)
+    x = uu.float()
+    grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    assert _rel(du, (a.float() @ b.float().t()).to(torch.bfloat16).float() * grad) < 2e-2
+    assert torch.equal(hgemm(a, b, bias, tile=tile, splits=splits), hgemm(a, b, bias, tile=tile, splits=splits))
+
+
+def test_hgemm_strided_views():
+    """A as a column slice of a wider buffer and C written into a column slice (the fused layer's q/k/v views)."""
+    from radhip.ops import hgemm
+    a, b, bias = _ops(401, 512, 1024, lda=1088)
+    out = torch.zeros(401, 1536, device=DEV, dtype=torch.bfloat16)
+    hgemm(a, b, bias, out=out[:, 512:1024], tile=2)
+    assert _rel(out[:, 512:1024], a.float() @ b.float().t() + bias.float()) < 1e-2
+    assert float(out[:, :512].abs().max()) == 0.0 and float(out[:, 1024:].abs().max()) == 0.0
