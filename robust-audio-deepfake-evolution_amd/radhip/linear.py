@@ -46,11 +46,11 @@ def _cast(t, dt):
         return t
     cache = ops.SCONV_WCACHE
     if cache is not None and isinstance(t, nn.Parameter):
-        hit = cache.get(("lin", id(t)))
-        if hit is not None and hit[0] is t:
+        hit = cache.get(("lin", id(t), dt))
+        if hit is not None and hit[0] is t and hit[1].dtype == dt:
             return hit[1]
         c = t.to(dt)
-        cache[("lin", id(t))] = (t, c)
+        cache[("lin", id(t), dt)] = (t, c)
         return c
     return t.to(dt)
 

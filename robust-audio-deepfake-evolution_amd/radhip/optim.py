@@ -20,7 +20,9 @@ class AdamW(torch.optim.AdamW):
     def __init__(self, params, **kw):
         kw.pop("fused", None)
         kw.pop("foreach", None)
-        super().__init__(params, foreach=False, **kw)
+        # the group flags torch's fused AdamW saves: a checkpoint of this optimizer resumed under torch's own
+        # (RADHIP_ADAMW=0) keeps the fused form, the one that takes GradScaler's grad_scale / found_inf
+        super().__init__(params, fused=True, **kw)
 
     def _covered(self, group, ps):
         return (all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
@@ -50,6 +52,11 @@ class AdamW(torch.optim.AdamW):
                     st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                elif not (st["step"].is_cuda and st["step"].device == p.device
+                          and st["step"].dtype == torch.float32):
+                    # a loaded state_dict may hold the step as a CPU scalar (torch's non-fused AdamW, or
+                    # map_location="cpu"); the kernel reads it on the device, as torch's fused step does
+                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
                 ms.append(st["exp_avg"])
                 vs.append(st["exp_avg_sq"])
                 ss.append(st["step"])

@@ -231,7 +231,7 @@ class WindowStep:
             self._lin_dst = [torch.empty_like(p, dtype=dt) for p in self._lin_src]
         ops.cast_many([p.detach() for p in self._lin_src], self._lin_dst)
         for p, c in zip(self._lin_src, self._lin_dst):
-            self._wcache[("lin", id(p))] = (p, c)
+            self._wcache[("lin", id(p), c.dtype)] = (p, c)
 
     def _clean_pass(self):
         self._wcache = {}                  # weight layouts prepared by this pass, reused by the window's others

@@ -72,3 +72,35 @@ def test_adamw_matches_torch_fused():
     od.step()
     for pc, pd in zip(c, d):
         assert float((pc - pd).abs().max()) <= 2e-6 * float(pc.detach().abs().max().clamp_min(1.0))
+
+
+def test_adamw_cpu_step_state_and_flags():
+    """A state_dict whose step counts are CPU scalars (torch's non-fused AdamW, or a checkpoint loaded with
+    map_location="cpu") steps on the device like torch's fused AdamW; the saved groups carry torch's fused flags, so
+    torch's own AdamW resumed from them keeps the fused form (the one that takes GradScaler's arguments)."""
+    from radhip.optim import AdamW
+    a, b = _params(5), _params(5)
+    ref = torch.optim.AdamW(_groups(a), foreach=False)          # non-fused: CPU step scalars
+    for p in a:
+        p.grad = torch.ones_like(p)
+    ref.step()
+    sd = ref.state_dict()
+    assert not sd["state"][0]["step"].is_cuda
+    o = AdamW(_groups(b))
+    with torch.no_grad():
+        for pa, pb in zip(a, b):
+            pb.copy_(pa)
+    o.load_state_dict(sd)
+    for p in a + b:
+        p.grad = torch.full_like(p, 0.5)
+    ref.step()
+    o.step()
+    torch.cuda.synchronize()
+    for pa, pb in zip(a, b):
+        assert o.state[pb]["step"].is_cuda and float(o.state[pb]["step"]) == 2.0
+        assert float((pa - pb).abs().max()) <= 2e-6 * float(pa.detach().abs().max().clamp_min(1.0))
+    saved = o.state_dict()["param_groups"][0]
+    assert saved["fused"] is True
+    t = torch.optim.AdamW(_groups(_params(5)), fused=True)
+    t.load_state_dict(o.state_dict())
+    assert t.param_groups[0]["fused"] is True
