@@ -53,12 +53,12 @@ _FLOOR = {}            # the floor itself (logits max abs error, per-group gradi
 FLOOR_MAX_RATIO_FP16 = 2.0
 
 
-def _cfg(lora_mode):
+def _cfg(lora_mode, K=1):
     from radhip.build import load_config
     from radhip.wavlm import WAVLM_LARGE
     cfg = load_config("Phase6_Proposed.conf")
     tc = cfg["training_config"]
-    tc["accumulation_steps"] = 1
+    tc["accumulation_steps"] = K
     tc["lora_dropout"] = 0.0
     tc["lora_mode"] = lora_mode
     w = dict(WAVLM_LARGE, hidden_dropout=0.0, attention_dropout=0.0, activation_dropout=0.0,
@@ -118,7 +118,7 @@ def _inputs():
     return xm, y, lam, perm
 
 
-def _oracle_step(o, xo, y, lam, perm, host, amp=None, scale=1.0):
+def _oracle_step(o, xo, y, lam, perm, host, amp=None, scale=1.0, div=1.0):
     """src/main.py:1036-1097 at accumulation 1: mixup loss, backward, FGM attack on the clean gradient,
     adversarial pass with its own band / SpecAugment masks, backward, restore. amp = torch.float16 runs the
     passes under fp16 autocast with the losses multiplied by `scale` before backward, as the reference's
@@ -139,7 +139,7 @@ def _oracle_step(o, xo, y, lam, perm, host, amp=None, scale=1.0):
         out = out.float() if amp is not None else out
         return lam * focal_loss(out, ya) + (1.0 - lam) * focal_loss(out, yb)
     loss = fwd(host["c_mask"][0], host["c_tmask"])
-    (loss * scale).backward()
+    (loss / div * scale).backward()
     fp = [(n, p) for n, p in o.named_parameters() if p.requires_grad and "feature_projection" in n]
     backup = {}
     with torch.no_grad():
@@ -149,7 +149,7 @@ def _oracle_step(o, xo, y, lam, perm, host, amp=None, scale=1.0):
             if nrm != 0 and not torch.isnan(nrm):
                 p.add_(0.5 * p.grad / nrm)
     adv = fwd(host["a_mask"][0], host["a_tmask"][0])
-    (adv * scale).backward()
+    (adv / div * scale).backward()
     with torch.no_grad():
         for n, p in fp:                            # FGM.restore
             p.copy_(backup[n])
@@ -310,3 +310,109 @@ def test_bench_path_window_vs_fp64_oracle(lora_mode, amp):
         assert e < bounds[g], (g, e)
     assert np.isfinite(losses[1]) and abs(losses[1] - losses[0]) < 0.1 * abs(losses[0])
     assert torch.isfinite(got[1]).all()
+
+
+def _inputs_k(k):
+    """Micro-batch k of a K = 4 window: its own waveforms, labels, mixup coefficient and permutation."""
+    rng = np.random.default_rng(100 + k)
+    x = np.clip(0.1 * rng.standard_normal((B, 64600)), -1, 1).astype(np.float32)
+    y = (rng.random(B) < 0.3).astype(np.int64)
+    lam = float([0.37, 0.81, 0.55, 0.12][k])
+    perm = rng.permutation(B).tolist()
+    xm = (np.float32(lam) * x + np.float32(1.0 - lam) * x[perm]).astype(np.float32)
+    return xm, y, lam, perm
+
+
+def _host_k(h, k):
+    """Micro-batch k's band / SpecAugment draws from the window's staged host arrays (clean rows k*B..k*B+B-1)."""
+    sl = slice(k * B, (k + 1) * B)
+    return {"c_mask": h["c_mask"][sl], "c_tmask": h["c_tmask"][sl], "a_mask": h["a_mask"][k:k + 1],
+            "a_tmask": h["a_tmask"][k:k + 1]}
+
+
+def _group_errs(grads, og, trainable, dead, omap_inv):
+    groups = {}
+    for n in trainable:
+        if n in dead:
+            continue
+        a, b = grads[n].reshape(-1), og[omap_inv[n]].reshape(-1)
+        ga, gb = groups.setdefault(_group(n), ([], []))
+        ga.append(a)
+        gb.append(b)
+    return {g: _rel(torch.cat(a), torch.cat(b)) for g, (a, b) in groups.items()}
+
+
+def test_bench_config_fp16_k4_window_vs_fp64_oracle():
+    """The exact configuration bench.py times: fp16 autocast + GradScaler, accumulation K = 4 (the four clean passes
+    batched into one 32-utterance pass, then the four FGM chain links at B = 8) on the full Phase-6 model, against
+    the fp64 oracle running the reference's sequential chain of four micro-steps (src/main.py:1030-1108: each loss
+    / 4, FGM attacking the gradient accumulated so far, adversarial pass, restore). Bound: each gradient group
+    within 2x the reference's own floor for the same chain (its modules in fp32 weights under fp16 autocast +
+    GradScaler at 2^16, against the same fp64 run)."""
+    import copy
+    from oracle.model import from_peft_state
+    from radhip.train import Trainer
+    from radhip.window import WindowStep
+    K = 4
+    cfg, wcfg = _cfg("reference", K)
+    m = _product(cfg)
+    tr = Trainer(m, cfg, DEV, total_steps=10, amp_dtype=torch.float16)
+    assert tr.scaler.is_enabled() and tr.fgm is not None and tr.freq_aug
+    names = {id(p): n for n, p in m.named_parameters()}
+    trainable = [names[id(p)] for p in tr.grads.params]
+    w = WindowStep(tr, B, graphs=True)
+    for k in range(K):
+        w.add(k, np.zeros(B, dtype=np.int64))
+    w.capture()
+    w.reset_host()
+    got = []
+
+    def opt_step():
+        got.append(tr.grads.flat.clone())
+        tr.grads.zero()
+    tr.optimizer_step = opt_step
+    ins = [_inputs_k(k) for k in range(K)]
+    np.random.seed(7)
+    random.seed(7)
+    torch.manual_seed(7)
+    tr.loss_sum.zero_()
+    for k, (xm, y, lam, perm) in enumerate(ins):
+        w.xslot(k).copy_(torch.from_numpy(xm))
+        w.add(k, y, lam, perm)
+    host = {kk: v.copy() for kk, v in w._host.items()}
+    w.run()
+    torch.cuda.synchronize()
+    scale = float(tr.scaler.get_scale())
+    flat = got[0] / scale
+    assert torch.isfinite(flat).all(), "gradient overflow at the GradScaler's initial scale"
+    offs, grads = 0, {}
+    for p, n in zip(tr.grads.params, trainable):
+        grads[n] = flat[offs:offs + p.numel()].view_as(p).double()
+        offs += p.numel()
+    del w
+    torch.cuda.empty_cache()
+
+    o = _oracle(m, wcfg, trainable, "reference")
+    o32 = copy.deepcopy(o).float()
+    S = 65536.0
+    xos = [torch.from_numpy(xm).to(DEV).double() for xm, _, _, _ in ins]
+    for k, (xm, y, lam, perm) in enumerate(ins):
+        _oracle_step(o, xos[k], y, lam, perm, _host_k(host, k), div=K)
+        _oracle_step(o32, xos[k].float(), y, lam, perm, _host_k(host, k), amp=torch.float16, scale=S, div=K)
+    og = {n: p.grad for n, p in o.named_parameters() if p.requires_grad and "lora_" not in n}
+    og16 = {n: (p.grad.double() / S if p.grad is not None else None) for n, p in o32.named_parameters()
+            if p.requires_grad and "lora_" not in n}
+    omap_inv = {v: k for k, v in from_peft_state({n: n for n in trainable}).items()}
+    dead = [n for n in trainable if og[omap_inv[n]] is None]
+    for n in dead:
+        assert float(grads[n].abs().max()) == 0.0, n
+    errs = _group_errs(grads, og, trainable, dead, omap_inv)
+    floor = _group_errs({n: og16[omap_inv[n]] for n in trainable if n not in dead}, og, trainable, dead, omap_inv)
+    ratios = {g: errs[g] / max(floor[g], 1e-12) for g in floor}
+    print(f"\n[e2e fp16 K=4] grad rel L2 product: " + ", ".join(f"{g} {e:.3e}" for g, e in sorted(errs.items())))
+    print(f"[e2e fp16 K=4] reference floor: " + ", ".join(f"{g} {e:.3e}" for g, e in sorted(floor.items())))
+    print(f"[e2e fp16 K=4] product / floor: " + ", ".join(f"{g} {r:.2f}x" for g, r in sorted(ratios.items())))
+    assert set(errs) == set(GRAD_REL_BF16["reference"]), errs
+    for g, r in ratios.items():
+        assert r <= FLOOR_MAX_RATIO_FP16, (g, r, ratios)
+    assert float(tr.loss_sum) > 0
