@@ -50,9 +50,32 @@ __device__ __forceinline__ i32x4 rsrc(const void* base, uint32_t bytes) {
 }
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
-__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// GELU (erf form, HF "gelu" = torch.nn.functional.gelu) for the epilogues, with erf by Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7, below the fp32 rounding the result then takes to bf16 / fp16): one reciprocal, one exp2 and
+// five FMAs instead of erff's piecewise polynomial, which made the VALU tail of a 256 x 256 FFN1 tile longer than its
+// stores. With z = x / sqrt(2) and q = P(t) exp(-z^2) = 1 - erf(|z|): 1 + erf(z) = 2 - q (z >= 0) or q (z < 0), and
+// exp(-z^2) = exp(-x^2 / 2) also gives the normal density of the GELU derivative.
+struct GeluParts {
+  float one_p_erf;   // 1 + erf(x / sqrt(2))
+  float e;           // exp(-x^2 / 2)
+};
+__device__ __forceinline__ GeluParts gelu_parts(float x) {
+  const float ax = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float y = fmaf(t, 1.061405429f, -1.453152027f);
+  y = fmaf(t, y, 1.421413741f);
+  y = fmaf(t, y, -0.284496736f);
+  y = fmaf(t, y, 0.254829592f);
+  y *= t;
+  const float e = __builtin_amdgcn_exp2f(-x * x * 0.72134752044448170f);   // exp(-x^2/2) = 2^(-x^2 log2(e) / 2)
+  const float q = y * e;
+  return GeluParts{x >= 0.f ? 2.0f - q : q, e};
+}
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * gelu_parts(x).one_p_erf; }
 __device__ __forceinline__ float gelu_grad(float x) {
-  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+  const GeluParts g = gelu_parts(x);
+  return fmaf(x * 0.39894228040143268f, g.e, 0.5f * g.one_p_erf);
 }
 __device__ __forceinline__ uint32_t pack2(float a, float b) { return hpack2(a, b); }
 
@@ -134,7 +157,7 @@ __device__ __forceinline__ void wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO>
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
   using P = Plan<BM, BN, NPA, NPB>;
   constexpr int FM = P::FM, FN = P::FN, WTM = P::WTM, WTN = P::WTN, FMP = P::FMP, FNP = P::FNP;
@@ -218,11 +241,21 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the tile's bias columns: loaded ahead of the ring (older than every DMA, so the prologue's counted wait retires
+  // it too), parked in LDS past the ring and the epilogue image for the epilogue's register phase
+  constexpr int BIAS_OFF = (S * SLAB > BM * (BN * 2 + 16) ? S * SLAB : BM * (BN * 2 + 16));
+  static_assert(BIAS_OFF + BN * 2 <= 160 * 1024, "bias slot");
+  const bool has_bias = EPI != RDX_EPI_GELU_BWD && g.bias != nullptr;
+  uint2 bias4 = make_uint2(0u, 0u);
+  if (has_bias && tid < BN / 4 && n0 + 4 * tid < N) bias4 = *reinterpret_cast<const uint2*>(g.bias + n0 + 4 * tid);
+  __builtin_amdgcn_sched_barrier(0);
+
   // prologue: the whole ring (K steps 0 .. U - 1), then retire what phase 0 reads
 #pragma unroll
   for (int u = 0; u < U; ++u) static_for<SPK>([&](auto JC) { issue(JC, u, u); });
   wait_barrier<S - P::reads(0)>();
   __builtin_amdgcn_sched_barrier(0);
+  if (tid < BN / 4) *reinterpret_cast<uint2*>(lds + BIAS_OFF + 8 * tid) = bias4;   // read after later barriers
   if (wm == 1) __builtin_amdgcn_s_barrier();     // row group 1 runs one barrier behind group 0
   __builtin_amdgcn_sched_barrier(0);
   if (PRIO == 2 && wm == 1) __builtin_amdgcn_s_setprio(1);
@@ -249,7 +282,8 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
       }
     }
     // 2. refill the slabs the previous phase read, with the same slabs U K steps later
-    if constexpr (q >= 1) {
+    if constexpr (ABL == 1) {
+    } else if constexpr (q >= 1) {
       constexpr int f = P::first(q - 1), n = P::reads(q - 1);
       static_for<n>([&](auto IC) { issue(std::integral_constant<int, f + decltype(IC)::value>{}, u, kt + U); });
     } else {
@@ -259,10 +293,20 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
         static_for<n>([&](auto IC) { issue(std::integral_constant<int, f + decltype(IC)::value>{}, up, kt - 1 + U); });
     }
     // 3. retire this phase's reads and the slabs the next phase reads; meet the partner group
-    wait_barrier<S - P::reads(q) - P::reads((q + 1) % NPH)>();
+    if constexpr (ABL == 1) wait_barrier<0>();
+    else wait_barrier<S - P::reads(q) - P::reads((q + 1) % NPH)>();
     __builtin_amdgcn_sched_barrier(0);
     // 4. MFMA segment
     if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if constexpr (ABL == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < FMP; ++i) asm volatile("" ::"v"(af[kk][a * FMP + i]));
+#pragma unroll
+        for (int j = 0; j < FNP; ++j) asm volatile("" ::"v"(bf[kk][b * FNP + j]));
+      }
+    } else
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -336,30 +380,72 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
     }
   }
 
+  if constexpr (ABL == 3) {                       // timing probe: no epilogue (the accumulators kept live)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   // epilogue: acc[i][j][e] = C[m0 + wm*WTM + i*16 + fr][n0 + wn*WTN + j*16 + 4*fq + e], through an LDS image
+  // (fp32 acc + bias rounded once, as the unfused layer rounds), then whole rows, 16 bytes per lane
   constexpr int PITCH = BN * 2 + 16;
   static_assert(BM * PITCH <= 160 * 1024, "epilogue image");
   char* img = lds;
+  uint2 bb[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+    bb[j] = has_bias ? *reinterpret_cast<const uint2*>(lds + BIAS_OFF + 2 * (wn * WTN + j * 16 + 4 * fq))
+                     : make_uint2(0u, 0u);
+  __syncthreads();                                // bias read before the image overwrites nothing (own slot)
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int r = wm * WTM + i * 16 + fr;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = wn * WTN + j * 16 + 4 * fq;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (EPI != RDX_EPI_GELU_BWD && g.bias && n0 + c < N) {
-        const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n0 + c);
-        v[0] += hlo(bb.x);
-        v[1] += hhi(bb.x);
-        v[2] += hlo(bb.y);
-        v[3] += hhi(bb.y);
-      }
-      *reinterpret_cast<uint2*>(img + r * PITCH + c * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      const float v0 = acc[i][j][0] + hlo(bb[j].x), v1 = acc[i][j][1] + hhi(bb[j].x);
+      const float v2 = acc[i][j][2] + hlo(bb[j].y), v3 = acc[i][j][3] + hhi(bb[j].y);
+      *reinterpret_cast<uint2*>(img + r * PITCH + c * 2) = make_uint2(pack2(v0, v1), pack2(v2, v3));
     }
   }
   __syncthreads();
-  constexpr int CPR = BN / 8;
-#pragma unroll 4
+  constexpr int CPR = BN / 8;                     // 16-byte chunks per tile row
+  constexpr int ITER = BM * CPR / 512;
+  static_assert((BM * CPR) % 512 == 0, "row phase");
+  auto gelu8 = [&](uint4 q) -> uint4 {
+    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(gelu(hlo(qw[e])), gelu(hhi(qw[e])));
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  };
+  auto gelu_bwd8 = [&](uint4 q, uint4 u) -> uint4 {
+    const uint32_t qw[4] = {q.x, q.y, q.z, q.w}, uw[4] = {u.x, u.y, u.z, u.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(hlo(qw[e]) * gelu_grad(hlo(uw[e])), hhi(qw[e]) * gelu_grad(hhi(uw[e])));
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  };
+  if (m0 + BM <= M && n0 + BN <= N && g.wide) {
+    // whole tile in range, 16-byte aligned rows: every load issued before any store, no per-element branch
+    uint4 qv[ITER], ux[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = tid + it * 512, r = idx / CPR, c = (idx - r * CPR) * 8;
+      if (EPI == RDX_EPI_GELU_BWD) ux[it] = *reinterpret_cast<const uint4*>(g.aux + (int64_t)(m0 + r) * g.ldaux + n0 + c);
+      qv[it] = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = tid + it * 512, r = idx / CPR, c = (idx - r * CPR) * 8;
+      const uint4 q = EPI == RDX_EPI_GELU_BWD ? gelu_bwd8(qv[it], ux[it]) : qv[it];
+      *reinterpret_cast<uint4*>(g.C + (int64_t)(m0 + r) * g.ldc + n0 + c) = q;
+      if (EPI == RDX_EPI_BIAS_GELU) *reinterpret_cast<uint4*>(g.aux_out + (int64_t)(m0 + r) * g.ldao + n0 + c) = gelu8(q);
+    }
+    return;
+  }
+  // ragged tile or 8-byte rows
   for (int idx = tid; idx < BM * CPR; idx += 512) {
     const int r = idx / CPR, c = (idx - r * CPR) * 8;
     const int m = m0 + r, n = n0 + c;
@@ -378,33 +464,20 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
       if (full) *reinterpret_cast<uint2*>(dst + 4) = make_uint2(v.z, v.w);
     };
     uint4 qv = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
-    if (EPI == RDX_EPI_GELU_BWD) {
-      const uint4 uu = ld8(g.aux + (int64_t)m * g.ldaux + n);
-      const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w}, uw[4] = {uu.x, uu.y, uu.z, uu.w};
-      uint32_t o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = pack2(hlo(qw[e]) * gelu_grad(hlo(uw[e])), hhi(qw[e]) * gelu_grad(hhi(uw[e])));
-      qv = make_uint4(o[0], o[1], o[2], o[3]);
-    }
+    if (EPI == RDX_EPI_GELU_BWD) qv = gelu_bwd8(qv, ld8(g.aux + (int64_t)m * g.ldaux + n));
     st8(g.C + (int64_t)m * g.ldc + n, qv);
-    if (EPI == RDX_EPI_BIAS_GELU) {
-      const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
-      uint32_t o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = pack2(gelu(hlo(qw[e])), gelu(hhi(qw[e])));
-      st8(g.aux_out + (int64_t)m * g.ldao + n, make_uint4(o[0], o[1], o[2], o[3]));
-    }
+    if (EPI == RDX_EPI_BIAS_GELU) st8(g.aux_out + (int64_t)m * g.ldao + n, gelu8(qv));
   }
 }
 
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO>
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0>
 static int launch(Args g, hipStream_t st) {
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   constexpr int ring = U * (BM / 64 + BN / 64) * 8192, image = BM * (BN * 2 + 16);
-  constexpr int lds = ring > image ? ring : image;
+  constexpr int lds = (ring > image ? ring : image) + BN * 2;
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO>;
+  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO, ABL>;
   static bool lds_ok = false;
   if (!lds_ok) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -425,9 +498,26 @@ static int dispatch(const Args& g, int tile, hipStream_t st) {
     case 0: return launch<256, 256, 2, 2, 2, EPI, PRIO>(g, st);   // 16 slabs, 128 KB
     case 1: return launch<256, 192, 2, 1, 2, EPI, PRIO>(g, st);   // 14 slabs
     case 2: return launch<128, 256, 1, 2, 3, EPI, PRIO>(g, st);   // 18 slabs
-    case 3: return launch<128, 192, 2, 1, 4, EPI, PRIO>(g, st);   // 20 slabs
+    case 3: return launch<128, 192, 2, 1, 3, EPI, PRIO>(g, st);   // 15 slabs
     case 4: return launch<128, 128, 1, 1, 4, EPI, PRIO>(g, st);   // 16 slabs
     case 5: return launch<256, 128, 2, 1, 3, EPI, PRIO>(g, st);   // 18 slabs
+    default: return RDX_EINVAL;
+  }
+}
+
+// timing probes (bias epilogue, wrong results by design): 1000 + tile without refills in the K loop, 2000 + tile
+// without MFMA, 3000 + tile without the epilogue
+static int dispatch_probe(const Args& g, int code, hipStream_t st) {
+  switch (code) {
+    case 1000: return launch<256, 256, 2, 2, 2, RDX_EPI_BIAS, 0, 1>(g, st);
+    case 1002: return launch<128, 256, 1, 2, 3, RDX_EPI_BIAS, 0, 1>(g, st);
+    case 1004: return launch<128, 128, 1, 1, 4, RDX_EPI_BIAS, 0, 1>(g, st);
+    case 2000: return launch<256, 256, 2, 2, 2, RDX_EPI_BIAS, 0, 2>(g, st);
+    case 2002: return launch<128, 256, 1, 2, 3, RDX_EPI_BIAS, 0, 2>(g, st);
+    case 2004: return launch<128, 128, 1, 1, 4, RDX_EPI_BIAS, 0, 2>(g, st);
+    case 3000: return launch<256, 256, 2, 2, 2, RDX_EPI_BIAS, 0, 3>(g, st);
+    case 3002: return launch<128, 256, 1, 2, 3, RDX_EPI_BIAS, 0, 3>(g, st);
+    case 3004: return launch<128, 128, 1, 1, 4, RDX_EPI_BIAS, 0, 3>(g, st);
     default: return RDX_EINVAL;
   }
 }
@@ -478,7 +568,9 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
   if (epilogue == RDX_EPI_BIAS_GELU) RDX_REQUIRE(aux_out && ldao >= N && ldao % 4 == 0 && al(aux_out, 8));
   if (epilogue == RDX_EPI_GELU_BWD) RDX_REQUIRE(aux && ldaux >= N && ldaux % 4 == 0 && al(aux, 8));
   int bm, bn;
-  RDX_REQUIRE(tile >= 0 && tile < 300 && hg::geometry(tile, &bm, &bn));
+  const bool probe = tile >= 1000;
+  RDX_REQUIRE(probe ? (tile < 4000 && epilogue == RDX_EPI_BIAS && splits == 1)
+                    : (tile >= 0 && tile < 300 && hg::geometry(tile, &bm, &bn)));
   RDX_REQUIRE(group_m >= 0);
   RDX_REQUIRE(splits >= 1 && splits <= 16 && splits <= K / 64);
   if (splits > 1) {
@@ -509,6 +601,7 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
   if (epilogue == RDX_EPI_BIAS_GELU) g.wide = g.wide && al(aux_out, 16) && ldao % 8 == 0;
   if (epilogue == RDX_EPI_GELU_BWD) g.wide = g.wide && al(aux, 16) && ldaux % 8 == 0;
   hipStream_t st = as_stream(stream);
+  if (probe) return hg::dispatch_probe(g, tile, st);
   const int prio = tile / 100, base = tile % 100;
   switch (epilogue) {
     case RDX_EPI_BIAS:

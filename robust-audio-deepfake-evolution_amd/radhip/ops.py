@@ -1407,9 +1407,23 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
 # with the GELU backward fused took 30.9 us in the step vs 18.0 + 9.3 for hipBLASLt's 128 x 192 kernel + the
 # GELU backward, so it stays unfused. out_proj / its input gradient (64 x 64 tiles, 10.3 us vs 20-27) and FFN1 +
 # GELU (28.3 vs 32.7) run here; every B = 32 shape and the N = 1024, K = 3072 / 4096 ones stay on hipBLASLt.
-WGEMM_POLICY = {
+#
+# Round 5: csrc/hgemm.hip ("hg", tile, splits, group_m), the 8-wave ping-pong kernel with the slab ring and the
+# A&S-erf GELU epilogues, standalone against hipBLASLt on one box (tools/bench_hgemm.py,
+# profiles/r05_hgemm_sweep.jsonl, us): B = 8 q/k/v 15.8 vs 22.8 (pgemm 18.9), FFN1 + GELU 22.4 vs 30.2 (with torch's
+# GELU), FFN2's input gradient + GELU backward 22.4, out_proj / its input gradient 11.3 vs 21.8; B = 32 out_proj /
+# d_out 18.5 vs 23, FFN1 + GELU 71 vs 80, FFN2 56.5 vs 60, d_ffn1 56 vs 60, d_qkv 44.9 vs 46.5, q/k/v 46.7 vs 46.0,
+# d_ffn2 81.7 vs 81 (+ the separate GELU backward). The B = 8 N = 1024 long-K shapes (FFN2, d_ffn1, d_qkv: 104
+# tiles of 128 x 128 on 256 CUs) stay on hipBLASLt's split-K kernels (27-28 vs 29-30 with split-K 2 here).
+WGEMM_POLICY_R4 = {
     "b8": {"qkv": ("pg", 4, 4), "out": (5, 1), "d_out": (5, 1), "ffn1": (6, 1)},
     "b32": {},
+}
+WGEMM_POLICY = {
+    "b8": {"qkv": ("hg", 3, 1, 0), "out": ("hg", 4, 1, 0), "d_out": ("hg", 4, 1, 0), "ffn1": ("hg", 202, 1, 0),
+           "d_ffn2": ("hg", 202, 1, 0)},
+    "b32": {"qkv": ("hg", 1, 1, 0), "out": ("hg", 2, 1, 0), "d_out": ("hg", 2, 1, 0), "ffn1": ("hg", 0, 1, 0),
+            "d_ffn2": ("hg", 0, 1, 0), "ffn2": ("hg", 2, 1, 0), "d_ffn1": ("hg", 2, 1, 0), "d_qkv": ("hg", 2, 1, 0)},
 }
 
 
