@@ -519,6 +519,10 @@ int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, i
               int splits, int group_m, void* ws, int64_t ws_bytes, int* counters, int64_t n_counters, void* stream);
 int64_t rdx_hgemm_ws_bytes(int M, int N, int tile, int splits);
 int64_t rdx_hgemm_counters(int M, int N, int tile);
+/* splits == 0 (tiles 2 / 3 / 4): stream-K. One workgroup per CU; the grid's workgroups take equal contiguous runs of
+ * the (tile, 64-deep K step) units in tile order, and a tile shared by several runs is summed by the last of them to
+ * arrive, its fp32 partials in K order (deterministic). ws_bytes >= rdx_hgemm_sk_ws_bytes(M, N, K, tile). */
+int64_t rdx_hgemm_sk_ws_bytes(int M, int N, int K, int tile);
 
 /* ---- Weight / bias gradients of the head's linears, accumulated in fp32 (csrc/wgrad.hip) ----------------
  * dW[n][k] += sum_m dY[m][n] X[m][k], db[n] += sum_m dY[m][n] (db may be NULL): bf16 dY [M, ldy] and X [M, ldx],

@@ -26,6 +26,7 @@
 //     per group; split-K (splits > 1): the splits of a tile are consecutive work ids, publish fp32 partials and
 //     the last arriver sums them in split order (deterministic) and runs the epilogue;
 //   * epilogue through an LDS image of the tile (16-byte padded rows), whole rows stored 16 bytes per lane.
+#include <algorithm>
 #include <utility>
 
 #include "common.h"
@@ -35,6 +36,7 @@ namespace hg {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 __device__ void buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds, int size, int voffset,
                                 int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
@@ -102,7 +104,9 @@ struct Args {
   hst* aux_out;      // BIAS_GELU: gelu(u) [M, ldao]
   int64_t ldao;
   int tiles_m, tiles_n, group_m;
-  int splits;        // split-K factor; split s covers k-steps [s*nk/S, (s+1)*nk/S)
+  int splits;        // split-K factor; split s covers k-steps [s*nk/S, (s+1)*nk/S); 0: stream-K
+  int maxc;          // partial slots per tile in ws (splits, or the stream-K bound)
+  int grid_sk;       // stream-K grid (host side)
   float* ws;         // split-K partial slabs [tile][split][FM*FN][512][4] fp32
   int* counters;     // split-K arrival tickets, one per tile, zero between launches
   int wide;          // C / aux / aux_out rows 16-byte aligned: 16-byte row-phase accesses
@@ -157,44 +161,43 @@ __device__ __forceinline__ void wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0>
-__global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
+// output tile index -> (row tile, column tile): GROUP_M row tiles x every column tile per group (0: column-panel order)
+__device__ __forceinline__ void tile_coords(const Args& g, int tile, int& mt, int& nt) {
+  const int gm = g.group_m;
+  if (gm <= 0 || gm >= g.tiles_m) {
+    nt = tile / g.tiles_m;
+    mt = tile - nt * g.tiles_m;
+  } else {
+    const int per = gm * g.tiles_n, grp = tile / per, first = grp * gm;
+    const int gsz = min(g.tiles_m - first, gm), rem = tile - grp * per;
+    nt = rem / gsz;
+    mt = first + (rem - nt * gsz);
+  }
+}
+
+// bijective deal of n work ids onto the 8 XCDs in contiguous runs (blocks b and b + 8 share an XCD)
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int xcd = bid & 7, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// One output tile's K steps [kb, kb + nk): the ring, the phases, then either the epilogue (nc == 1) or this
+// contribution's fp32 partial in slot `slot` of the tile's nc and, for the last of them to arrive, the sum of the nc
+// partials in slot order and the epilogue.
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL>
+__device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, int nt, int tile, int kb, int nk,
+                                            int slot, int nc, int maxc) {
   using P = Plan<BM, BN, NPA, NPB>;
   constexpr int FM = P::FM, FN = P::FN, WTM = P::WTM, WTN = P::WTN, FMP = P::FMP, FNP = P::FNP;
   constexpr int NPH = P::NPH, SPK = P::SPK, S = U * SPK;
   constexpr int SLAB = 8192;
   static_assert(S * SLAB <= 160 * 1024, "ring");
-  extern __shared__ __attribute__((aligned(1024))) char lds[];
-
-  // work id -> (tile, split) -> (mt, nt)
-  const int SPL = g.splits;
-  const int nwg = g.tiles_m * g.tiles_n * SPL;
-  int t;
-  {
-    const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int tile = t / SPL, split = t - tile * SPL;
-  int mt, nt;
-  {
-    const int gm = g.group_m;
-    if (gm <= 0 || gm >= g.tiles_m) {
-      nt = tile / g.tiles_m;
-      mt = tile - nt * g.tiles_m;
-    } else {
-      const int per = gm * g.tiles_n, grp = tile / per, first = grp * gm;
-      const int gsz = min(g.tiles_m - first, gm), rem = tile - grp * per;
-      nt = rem / gsz;
-      mt = first + (rem - nt * gsz);
-    }
-  }
+  __syncthreads();                                // the previous segment's epilogue is done with the LDS
   const int m0 = mt * BM, n0 = nt * BN;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int M = g.M, N = g.N, K = g.K;
-  const int nk_all = K / 64;
-  const int kb = split * nk_all / SPL, nk = (split + 1) * nk_all / SPL - kb;
 
   const int64_t lda_b = g.lda * 2, ldb_b = g.ldb * 2;
   const int rows_a = min(BM, M - m0), rows_b = min(BN, N - n0);
@@ -244,7 +247,8 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
   // the tile's bias columns: loaded ahead of the ring (older than every DMA, so the prologue's counted wait retires
   // it too), parked in LDS past the ring and the epilogue image for the epilogue's register phase
   constexpr int BIAS_OFF = (S * SLAB > BM * (BN * 2 + 16) ? S * SLAB : BM * (BN * 2 + 16));
-  static_assert(BIAS_OFF + BN * 2 <= 160 * 1024, "bias slot");
+  constexpr int FLAG_OFF = BIAS_OFF + BN * 2;     // the split / stream-K arrival broadcast
+  static_assert(FLAG_OFF + 16 <= 160 * 1024, "bias slot");
   const bool has_bias = EPI != RDX_EPI_GELU_BWD && g.bias != nullptr;
   uint2 bias4 = make_uint2(0u, 0u);
   if (has_bias && tid < BN / 4 && n0 + 4 * tid < N) bias4 = *reinterpret_cast<const uint2*>(g.bias + n0 + 4 * tid);
@@ -337,41 +341,44 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
   __builtin_amdgcn_sched_barrier(0);
   wait_barrier<0>();                              // the trailing zero-record refills have landed too
 
-  // split-K: publish this split's fp32 partial (fragment order), take a ticket; the last arriver sums the
-  // partials in split order (cdna_hip_programming.md "Projection GEMM at M = 256" item 2)
-  if (SPL > 1) {
+  // split-K / stream-K: publish this contribution's fp32 partial (fragment order), take a ticket; the last arriver
+  // sums the partials in slot (= K) order (cdna_hip_programming.md "Projection GEMM at M = 256" item 2)
+  if (nc > 1) {
     constexpr int NT = 512;
-    float* slab = g.ws + (int64_t)tile * SPL * (FM * FN * NT * 4);
+    float* slab = g.ws + (int64_t)tile * maxc * (FM * FN * NT * 4);
     {
-      float* mine = slab + (int64_t)split * (FM * FN * NT * 4);
+      // write-through (sc1) 16-byte stores: the partial reaches memory without an L2 write-back, so the ticket
+      // needs no release fence (cdna_hip_programming.md Guideline 16, R1; a release fence here wrote the L2 back
+      // and cost ~6 us per partial)
+      float* mine = slab + (int64_t)slot * (FM * FN * NT * 4);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(mine, 0, FM * FN * NT * 16, 0x00020000);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(mine + ((i * FN + j) * NT + tid) * 4) = acc[i][j];
+        for (int j = 0; j < FN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, ((i * FN + j) * NT + tid) * 16,
+                                                 0, 16);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its write-through stores
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(lds);
+    int* flag = reinterpret_cast<int*>(lds + FLAG_OFF);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int ticket = __hip_atomic_fetch_add(g.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = ticket;
-      if (ticket == SPL - 1) {
+      if (ticket == nc - 1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         g.counters[tile] = 0;
       }
     }
     __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(flag[0]) != SPL - 1) return;
-    __syncthreads();                              // every wave has read the flag before the image overwrites it
-    // the sum in split order, every partial (this split's included) read back from its slab
+    if (__builtin_amdgcn_readfirstlane(flag[0]) != nc - 1) return;
+    // the sum in slot order, every partial (this one's included) read back from its slab
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = *reinterpret_cast<const f32x4*>(slab + ((i * FN + j) * NT + tid) * 4);
-    for (int s2 = 1; s2 < SPL; ++s2) {
+    for (int s2 = 1; s2 < nc; ++s2) {
       const float* ps = slab + (int64_t)s2 * (FM * FN * NT * 4);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -470,14 +477,51 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
   }
 }
 
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0>
+// splits >= 1: work id (XCD-dealt) = tile * splits + split; splits == 0 (stream-K): the grid's workgroups take
+// equal contiguous runs of the (tile, K step) units in tile order, a tile shared by several runs summed by the last
+// of them to arrive (its partial slots in K order).
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0, int SK = 0>
+__global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
+  extern __shared__ __attribute__((aligned(1024))) char lds[];
+  const int nk_all = g.K / 64;
+  const int tiles = g.tiles_m * g.tiles_n;
+  if constexpr (SK == 0) {
+    const int SPL = g.splits;
+    const int t = xcd_remap(blockIdx.x, tiles * SPL);
+    const int tile = t / SPL, split = t - tile * SPL;
+    int mt, nt;
+    tile_coords(g, tile, mt, nt);
+    const int kb = split * nk_all / SPL, nk = (split + 1) * nk_all / SPL - kb;
+    run_segment<BM, BN, NPA, NPB, U, EPI, PRIO, ABL>(g, lds, mt, nt, tile, kb, nk, split, SPL, SPL);
+    return;
+  }
+  if (g.splits != 0) return;
+  const int G = gridDim.x;
+  const int64_t UT = (int64_t)tiles * nk_all;
+  const int w = xcd_remap(blockIdx.x, G);
+  const int64_t u1 = (int64_t)(w + 1) * UT / G;
+  auto owner = [&](int64_t x) { return (int)(((x + 1) * G - 1) / UT); };   // the run holding unit x
+  for (int64_t u = (int64_t)w * UT / G; u < u1;) {
+    const int tile = (int)(u / nk_all);
+    const int kb = (int)(u - (int64_t)tile * nk_all);
+    const int ke = (int)min((int64_t)nk_all, kb + (u1 - u));
+    const int wf = owner((int64_t)tile * nk_all), wl = owner((int64_t)tile * nk_all + nk_all - 1);
+    int mt, nt;
+    tile_coords(g, tile, mt, nt);
+    run_segment<BM, BN, NPA, NPB, U, EPI, PRIO, ABL>(g, lds, mt, nt, tile, kb, ke - kb, w - wf, wl - wf + 1,
+                                                     g.maxc);
+    u += ke - kb;
+  }
+}
+
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0, int SK = 0>
 static int launch(Args g, hipStream_t st) {
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   constexpr int ring = U * (BM / 64 + BN / 64) * 8192, image = BM * (BN * 2 + 16);
-  constexpr int lds = (ring > image ? ring : image) + BN * 2;
+  constexpr int lds = (ring > image ? ring : image) + BN * 2 + 16;   // + the bias slot and the arrival flag
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO, ABL>;
+  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO, ABL, SK>;
   static bool lds_ok = false;
   if (!lds_ok) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -485,7 +529,8 @@ static int launch(Args g, hipStream_t st) {
     if (e != hipSuccess) return (int)e;
     lds_ok = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)(g.tiles_m * g.tiles_n * g.splits)), dim3(512), lds, st, g);
+  const unsigned grid = g.splits >= 1 ? (unsigned)(g.tiles_m * g.tiles_n * g.splits) : (unsigned)g.grid_sk;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, g);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -494,6 +539,14 @@ static int launch(Args g, hipStream_t st) {
 // priority 1 for row group 1
 template <int EPI, int PRIO>
 static int dispatch(const Args& g, int tile, hipStream_t st) {
+  if (g.splits == 0) {                           // stream-K: the ingest-bound tiles of the N = 1024 shapes
+    switch (tile) {
+      case 2: return launch<128, 256, 1, 2, 3, EPI, PRIO, 0, 1>(g, st);
+      case 3: return launch<128, 192, 2, 1, 3, EPI, PRIO, 0, 1>(g, st);
+      case 4: return launch<128, 128, 1, 1, 4, EPI, PRIO, 0, 1>(g, st);
+      default: return RDX_EINVAL;
+    }
+  }
   switch (tile) {
     case 0: return launch<256, 256, 2, 2, 2, EPI, PRIO>(g, st);   // 16 slabs, 128 KB
     case 1: return launch<256, 192, 2, 1, 2, EPI, PRIO>(g, st);   // 14 slabs
@@ -539,6 +592,39 @@ static bool geometry(int tile, int* bm, int* bn) {
 
 using namespace rdx;
 
+namespace {
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+// stream-K geometry: grid (one workgroup per CU, at most one per unit) and the partial slots a tile can need
+void sk_geometry(int64_t tiles, int nk_all, int* grid, int* maxc) {
+  const int64_t ut = tiles * nk_all;
+  const int G = (int)std::min<int64_t>(cu_count(), ut);
+  const int64_t per = ut / G;                   // every run holds per or per + 1 units
+  int mc = per >= 1 ? (int)((nk_all - 1) / per + 2) : nk_all;
+  *grid = G;
+  *maxc = std::min(mc, G);
+}
+}  // namespace
+
+extern "C" int64_t rdx_hgemm_sk_ws_bytes(int M, int N, int K, int tile) {
+  int bm, bn;
+  if (tile < 0 || tile >= 300 || !hg::geometry(tile, &bm, &bn) || K < 64) return -1;
+  const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  int grid, maxc;
+  sk_geometry(tiles, K / 64, &grid, &maxc);
+  return tiles * maxc * (int64_t)bm * bn * 4;
+}
+
 extern "C" int64_t rdx_hgemm_ws_bytes(int M, int N, int tile, int splits) {
   int bm, bn;
   if (splits <= 1) return 0;
@@ -572,9 +658,11 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
   RDX_REQUIRE(probe ? (tile < 4000 && epilogue == RDX_EPI_BIAS && splits == 1)
                     : (tile >= 0 && tile < 300 && hg::geometry(tile, &bm, &bn)));
   RDX_REQUIRE(group_m >= 0);
-  RDX_REQUIRE(splits >= 1 && splits <= 16 && splits <= K / 64);
-  if (splits > 1) {
-    const int64_t need = rdx_hgemm_ws_bytes(M, N, tile, splits), nc = rdx_hgemm_counters(M, N, tile);
+  RDX_REQUIRE(splits >= 0 && splits <= 16 && splits <= K / 64);
+  RDX_REQUIRE(splits >= 1 || !probe);
+  if (splits != 1) {
+    const int64_t need = splits > 1 ? rdx_hgemm_ws_bytes(M, N, tile, splits) : rdx_hgemm_sk_ws_bytes(M, N, K, tile);
+    const int64_t nc = rdx_hgemm_counters(M, N, tile);
     RDX_REQUIRE(need > 0 && ws && al(ws, 16) && ws_bytes >= need && counters && n_counters >= nc);
   }
   hg::Args g;
@@ -595,6 +683,12 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
   g.tiles_m = g.tiles_n = 0;
   g.group_m = group_m;
   g.splits = splits;
+  g.maxc = splits;
+  g.grid_sk = 0;
+  if (splits == 0) {
+    const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    sk_geometry(tiles, K / 64, &g.grid_sk, &g.maxc);
+  }
   g.ws = (float*)ws;
   g.counters = counters;
   g.wide = al(C, 16) && ldc % 8 == 0;

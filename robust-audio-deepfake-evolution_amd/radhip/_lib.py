@@ -134,6 +134,7 @@ SIGNATURES = {
                           c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "rdx_hgemm_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
     "rdx_hgemm_counters": (c_i64, [c_int, c_int, c_int]),
+    "rdx_hgemm_sk_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
     "rdx_gemm_bf16_strided": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                                       c_vp, c_vp]),
     "rdx_fe_conv0": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_int, c_int, c_vp, c_vp]),

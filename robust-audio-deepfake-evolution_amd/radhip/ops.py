@@ -1414,14 +1414,16 @@ def gemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=No
 # GELU), FFN2's input gradient + GELU backward 22.4, out_proj / its input gradient 11.3 vs 21.8; B = 32 out_proj /
 # d_out 18.5 vs 23, FFN1 + GELU 71 vs 80, FFN2 56.5 vs 60, d_ffn1 56 vs 60, d_qkv 44.9 vs 46.5, q/k/v 46.7 vs 46.0,
 # d_ffn2 81.7 vs 81 (+ the separate GELU backward). The B = 8 N = 1024 long-K shapes (FFN2, d_ffn1, d_qkv: 104
-# tiles of 128 x 128 on 256 CUs) stay on hipBLASLt's split-K kernels (27-28 vs 29-30 with split-K 2 here).
+# tiles of 128 x 128 on 256 CUs) take split-K 2 with write-through partials: 25.2 vs 25.6, 20.9 vs 21.2
+# (profiles/r05_hgemm_splitk.jsonl; stream-K over all 256 CUs measured slower, 29.3: two prologues and two partials
+# per run).
 WGEMM_POLICY_R4 = {
     "b8": {"qkv": ("pg", 4, 4), "out": (5, 1), "d_out": (5, 1), "ffn1": (6, 1)},
     "b32": {},
 }
 WGEMM_POLICY = {
     "b8": {"qkv": ("hg", 3, 1, 0), "out": ("hg", 4, 1, 0), "d_out": ("hg", 4, 1, 0), "ffn1": ("hg", 202, 1, 0),
-           "d_ffn2": ("hg", 202, 1, 0)},
+           "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 4, 2, 0), "d_ffn1": ("hg", 4, 2, 0), "d_qkv": ("hg", 4, 2, 0)},
     "b32": {"qkv": ("hg", 1, 1, 0), "out": ("hg", 2, 1, 0), "d_out": ("hg", 2, 1, 0), "ffn1": ("hg", 0, 1, 0),
             "d_ffn2": ("hg", 0, 1, 0), "ffn2": ("hg", 2, 1, 0), "d_ffn1": ("hg", 2, 1, 0), "d_qkv": ("hg", 2, 1, 0)},
 }
@@ -1558,24 +1560,45 @@ def wgrad_acc_many(items):
                                        _p(ws), ws.numel(), _stream(dy0)), "wgrad_acc_many")
 
 _WG_WS = {}
+_WG_NEED = {}   # device index -> (bytes, counters): the largest split-K workspace an eager launch has asked for
 
 
 def _wgemm_workspace(dev, ws_bytes, n_counters):
-    """Split-K workspace of csrc/wgemm.hip: fp32 partial slabs and per-tile arrival tickets (zeroed once here;
-    the last arriver re-zeroes its ticket). One per (device, stream): launches on one stream run one after
-    another (graph replays included), while two launches in flight at once on different streams (the SincNet
-    side stream, SideLinear's) must not share slabs or tickets. Grown outside graph capture only: the first
-    launch of every shape on a stream happens in the eager warm-up."""
+    """Split-K workspace of csrc/wgemm.hip / csrc/hgemm.hip: fp32 partial slabs and per-tile arrival tickets (zeroed
+    once here; the last arriver re-zeroes its ticket). Eager launches take one per (device, stream): launches on one
+    stream run one after another, while two launches in flight at once on different streams (the SincNet side
+    stream, SideLinear's) must not share slabs or tickets. Launches captured into HIP graphs take the device's graph
+    workspace, reserved before capture (reserve_graph_workspace) at the largest size the eager warm-up asked for:
+    the graphs' split-K GEMMs (the WavLM layers') are captured on one stream and replayed one graph after another."""
+    need = _WG_NEED.get(dev.index, (0, 0))
+    _WG_NEED[dev.index] = (max(need[0], ws_bytes), max(need[1], n_counters))
+    if torch.cuda.is_current_stream_capturing():
+        cur = _WG_WS.get((dev.index, "graph"))
+        if cur is None or cur[0].numel() < ws_bytes or cur[1].numel() < n_counters:
+            raise RuntimeError("radhip split-K GEMM: graph workspace not reserved before capture "
+                               "(ops.reserve_graph_workspace after an eager warm-up)")
+        return cur
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     cur = _WG_WS.get(key)
     if cur is None or cur[0].numel() < ws_bytes or cur[1].numel() < n_counters:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("radhip wgemm: split-K workspace must be allocated before graph capture")
         nb = max(ws_bytes, cur[0].numel() if cur else 0)
         nc = max(n_counters, cur[1].numel() if cur else 0)
         cur = (torch.empty(nb, dtype=torch.uint8, device=dev), torch.zeros(nc, dtype=torch.int32, device=dev))
         _WG_WS[key] = cur
     return cur
+
+
+def reserve_graph_workspace(dev):
+    """Allocate (outside capture) the graph split-K workspace at the largest size an eager launch on `dev` needed."""
+    dev = torch.device(dev)
+    nb, nc = _WG_NEED.get(dev.index, (0, 0))
+    if nb == 0:
+        return
+    key = (dev.index, "graph")
+    cur = _WG_WS.get(key)
+    if cur is None or cur[0].numel() < nb or cur[1].numel() < nc:
+        _WG_WS[key] = (torch.empty(max(nb, cur[0].numel() if cur else 0), dtype=torch.uint8, device=dev),
+                       torch.zeros(max(nc, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
 
 
 def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm",
@@ -1650,7 +1673,8 @@ def hgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
     """C[M, N] = a[M, K] @ b[N, K]^T (+ fused epilogue) on csrc/hgemm.hip (8-wave ping-pong MFMA GEMM with a slab
     ring, one workgroup per output tile or split): 16-bit (bf16 / fp16) row views a, b (unit inner stride, 16-byte
     aligned, K % 64 == 0); returns C, or (C, gelu(C)) for EPI_BIAS_GELU. splits > 1: split-K with the in-launch
-    last-arriver sum (the per-stream workspace of wgemm)."""
+    last-arriver sum (the per-stream workspace of wgemm); splits == 0: stream-K (one workgroup per CU over equal runs
+    of the (tile, K step) units, shared tiles summed by their last arriver; tiles 2-4)."""
     _require_gpu(a, b)
     if a.dtype not in HALF or b.dtype != a.dtype or a.stride(-1) != 1 or b.stride(-1) != 1:
         raise ValueError("radhip hgemm: bf16 / fp16 operands of one dtype with unit inner stride required")
@@ -1664,8 +1688,9 @@ def hgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=N
         aux_out = torch.empty(M, N, device=a.device, dtype=a.dtype)
     ws = cnt = None
     ws_bytes = n_cnt = 0
-    if splits > 1:
-        ws_bytes = int(lib().rdx_hgemm_ws_bytes(M, N, int(tile), int(splits)))
+    if splits != 1:
+        ws_bytes = int(lib().rdx_hgemm_ws_bytes(M, N, int(tile), int(splits)) if splits > 1
+                       else lib().rdx_hgemm_sk_ws_bytes(M, N, K, int(tile)))
         n_cnt = int(lib().rdx_hgemm_counters(M, N, int(tile)))
         if ws_bytes <= 0 or n_cnt <= 0:
             raise ValueError(f"radhip hgemm: no split-K geometry for tile {tile}")

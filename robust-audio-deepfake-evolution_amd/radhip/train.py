@@ -802,6 +802,7 @@ class GraphedMicroStep:
         torch.cuda.synchronize(tr.device)
         gs = []
         from . import ops
+        ops.reserve_graph_workspace(tr.device)
         for k in ((0, 1) if self.adv else (0,)):
             if ops.CAPTURE_TIMING is not None:
                 ops.CAPTURE_TIMING.new_graph()

@@ -389,6 +389,7 @@ class WindowStep:
         if chain:   # capture must not leave the warm-up's FGM state behind: feature_projection was restored
             tr.fgm.backup = {}
 
+        ops.reserve_graph_workspace(tr.device)   # split-K GEMMs of the captured passes (the warm-up sized it)
         def new_graph():
             if ops.CAPTURE_TIMING is not None:   # bench.py: stamp the first launch sites of each graph
                 ops.CAPTURE_TIMING.new_graph()

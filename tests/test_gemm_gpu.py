@@ -305,3 +305,23 @@ def test_hgemm_strided_views():
     hgemm(a, b, bias, out=out[:, 512:1024], tile=2)
     assert _rel(out[:, 512:1024], a.float() @ b.float().t() + bias.float()) < 1e-2
     assert float(out[:, :512].abs().max()) == 0.0 and float(out[:, 1024:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("tile", [2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(1608, 1024, 4096), (1608, 1024, 1024), (6432, 1024, 3072), (200, 1000, 256),
+                                   (64, 128, 64), (1608, 3072, 1024)])
+def test_hgemm_stream_k(tile, M, N, K):
+    """Stream-K (splits 0): runs of (tile, K step) units cut tiles anywhere (a tile may be shared by up to
+    `maxc` runs, or held whole); fewer units than CUs (64 x 128 x 64); ragged M / N. The shared tiles' partials are
+    summed in K order by their last arriver: two launches give the same bits."""
+    from radhip import _lib
+    from radhip.ops import hgemm
+    a, b, bias = _ops(M, N, K, seed=tile + K)
+    got = hgemm(a, b, bias, tile=tile, splits=0)
+    assert _rel(got, a.float() @ b.float().t() + bias.float()) < 1e-2
+    assert torch.equal(got, hgemm(a, b, bias, tile=tile, splits=0))
+    uu = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    du = hgemm(a, b, epilogue=_lib.EPI_GELU_BWD, aux=uu, tile=tile, splits=0)
+    x = uu.float()
+    grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    assert _rel(du, (a.float() @ b.float().t()).to(torch.bfloat16).float() * grad) < 2e-2

@@ -119,11 +119,12 @@ def main():
                 add(f"pg{tname}", pl)
             for tname in [x for x in args.hg.split(",") if x]:
                 parts = [int(v) for v in tname.split(":")]
-                tile, splits, gm = (parts + [1, 0])[:3] if len(parts) < 3 else parts
+                tile, splits, gm = (parts + [1, 0][len(parts) - 1:])[:3]
                 ws = cnt = None
                 nws = ncnt = 0
-                if splits > 1:
-                    nws = int(L.rdx_hgemm_ws_bytes(M, N, tile, splits))
+                if splits != 1:
+                    nws = int(L.rdx_hgemm_ws_bytes(M, N, tile, splits) if splits > 1
+                              else L.rdx_hgemm_sk_ws_bytes(M, N, K, tile))
                     ncnt = int(L.rdx_hgemm_counters(M, N, tile))
                     if nws <= 0:
                         row[f"hg{tname}"] = "no split geometry"
