@@ -826,15 +826,20 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     }
     RDX_PROBE(4);
     dg += __shfl_xor(dg, 32, 64);
-    if (kSplit) {   // partials of this part: dQ [tp][64] then d gate [tp]
+    if (kSplit) {   // partials of this part: dQ [tp][64] then d gate [tp], stored write-through (sc1)
       float* wp = ws + (bh * 2 + part) * FB_WSP;
-      if (qvalid && hh == 0) wp[AT_FUSED_MAXNT * AT_TILE * AT_DH + qi] = dg;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(wp, 0, FB_WSP * 4, 0x00020000);
+      if (qvalid && hh == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dg), rs, (AT_FUSED_MAXNT * AT_TILE * AT_DH + qi) * 4, 0,
+                                              16);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qq = qb * AT_TILE + crow(i, hh);
         if (qq < T) {
 #pragma unroll
-          for (int db = 0; db < 2; ++db) wp[qq * AT_DH + db * 32 + r] = dqacc[db][i];
+          for (int db = 0; db < 2; ++db)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dqacc[db][i]), rs, (qq * AT_DH + db * 32 + r) * 4,
+                                                  0, 16);
         }
       }
     } else {
@@ -852,14 +857,13 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     }
   }
   if (kSplit) {
-    // publish (every wave's stores retired, then one agent-scope release and the ticket); the second arriver
-    // acquires and combines (cdna_hip_programming.md Guideline 16); the ticket is left at zero
+    // publish: the partials were stored write-through, so every wave's stores retired then the ticket, with no
+    // release fence (an agent-scope release wrote the L2 back, µs per block); the second arriver acquires and
+    // combines (cdna_hip_programming.md Guideline 16, R1); the ticket is left at zero
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(L + FB_SC);   // the row-scalar area is free in phase 2
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int t = __hip_atomic_fetch_add(counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = t;
       if (t == 1) {
