@@ -45,7 +45,7 @@ KERNEL_BOUND = {"sincconv_absmaxpool": ("mfma", "fp32"), "sincconv_mfma": ("mfma
                 "sconv_fwd": ("hbm", None), "sconv_wgrad": ("hbm", None),
                 "sconv_dgrad_bnselu": ("hbm", None),
                 "fe_conv0": ("hbm", None), "fe_ln_gelu": ("hbm", None), "fe_conv_gemm": ("mfma", "bf16"),
-                "gemm": ("mfma", "bf16"), "wgemm": ("mfma", "bf16"), "pgemm": ("mfma", "bf16"), "hgemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}
+                "gemm": ("mfma", "bf16"), "wgemm": ("mfma", "bf16"), "pgemm": ("mfma", "bf16"), "hgemm": ("mfma", "bf16"), "lgemm": ("mfma", "bf16"), "sincconv_abspool1d": ("mfma", "fp32")}
 TRAIN_FLOP_PER_UTT = 0.72e12                # SURVEY.md §8d (algorithmic, FGM step)
 
 

@@ -524,6 +524,18 @@ int64_t rdx_hgemm_counters(int M, int N, int tile);
  * arrive, its fp32 partials in K order (deterministic). ws_bytes >= rdx_hgemm_sk_ws_bytes(M, N, K, tile). */
 int64_t rdx_hgemm_sk_ws_bytes(int M, int N, int K, int tile);
 
+/* ---- Small GEMMs of the detector head (csrc/lgemm.hip) -----------------------------------------------------------
+ * C[M, N] = A[M, K] W[N, K]^T for the fusion / PN-BiMamba / pooling / classifier linears (replaces F.linear and the
+ * input-gradient torch.matmul of src/models/DualStreamSEMamba.py:445-531,537-637,700-770 under the autocast of
+ * src/main.py:1049): A 16-bit, or fp32 when a_f32 (rounded to 16 bits on load: autocast's input cast); W 16-bit
+ * [N, ldw]; any K and any row strides (16-byte loads where rows are aligned). C 16-bit, or fp32 when c_f32 (the
+ * 16-bit result widened); R [M, ldr] of C's type or NULL: C = R + C (16-bit: rounded; C may alias R). RDX_EPI_BIAS: C = acc +
+ * bias (bias 16-bit [N] or NULL); RDX_EPI_BIAS_GELU (16-bit C): C = u = round(acc + bias), aux_out [M, ldao] =
+ * gelu(u); RDX_EPI_GELU_BWD: C = round(round(acc) * gelu'(aux)), aux = u [M, ldaux], no bias. */
+int rdx_lgemm(const void* A, int64_t lda, int a_f32, const void* W, int64_t ldw, void* C, int64_t ldc, int c_f32,
+              int M, int N, int K, const void* bias, int epilogue, const void* aux, int64_t ldaux, void* aux_out,
+              int64_t ldao, const void* R, int64_t ldr, void* stream);
+
 /* ---- Weight / bias gradients of the head's linears, accumulated in fp32 (csrc/wgrad.hip) ----------------
  * dW[n][k] += sum_m dY[m][n] X[m][k], db[n] += sum_m dY[m][n] (db may be NULL): bf16 dY [M, ldy] and X [M, ldx],
  * fp32 dW [N, ldw] (the flat gradient buffer's views), the token rows split over the chip in chunks of

@@ -76,6 +76,32 @@ __device__ __forceinline__ hx4v ds_tr4(const void* lds) {
   return __builtin_bit_cast(hx4v, __builtin_amdgcn_ds_read_tr16_b64_v4i16((rdx_lds_s4v*)(lds)));
 }
 
+// GELU (erf form, HF "gelu" = torch.nn.functional.gelu) for the GEMM epilogues (csrc/hgemm.hip, csrc/lgemm.hip), with erf by Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7, below the fp32 rounding the result then takes to bf16 / fp16): one reciprocal, one exp2 and
+// five FMAs instead of erff's piecewise polynomial, which made the VALU tail of a 256 x 256 FFN1 tile longer than its
+// stores. With z = x / sqrt(2) and q = P(t) exp(-z^2) = 1 - erf(|z|): 1 + erf(z) = 2 - q (z >= 0) or q (z < 0), and
+// exp(-z^2) = exp(-x^2 / 2) also gives the normal density of the GELU derivative.
+struct GeluParts {
+  float one_p_erf;   // 1 + erf(x / sqrt(2))
+  float e;           // exp(-x^2 / 2)
+};
+__device__ __forceinline__ GeluParts gelu_parts(float x) {
+  const float ax = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float y = fmaf(t, 1.061405429f, -1.453152027f);
+  y = fmaf(t, y, 1.421413741f);
+  y = fmaf(t, y, -0.284496736f);
+  y = fmaf(t, y, 0.254829592f);
+  y *= t;
+  const float e = __builtin_amdgcn_exp2f(-x * x * 0.72134752044448170f);   // exp(-x^2/2) = 2^(-x^2 log2(e) / 2)
+  const float q = y * e;
+  return GeluParts{x >= 0.f ? 2.0f - q : q, e};
+}
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * gelu_parts(x).one_p_erf; }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const GeluParts g = gelu_parts(x);
+  return fmaf(x * 0.39894228040143268f, g.e, 0.5f * g.one_p_erf);
+}
 // Storage-type adapters: all arithmetic is fp32.
 template <typename T> __device__ __forceinline__ float ld(const T* p, int64_t i);
 template <> __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }

@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
-from radhip.linear import RowLayerNorm, SideLinear
+from radhip.linear import RowLayerNorm, SideLinear, ffn_residual
 from radhip.mamba import Mamba
 from radhip.ops import layer_weighted_sum
 from radhip.sinc import CONV, Residual_block, SincNetEncoder  # noqa: F401  (re-exported like the reference)
@@ -134,9 +134,9 @@ class PN_BiMambas_Encoder(nn.Module):
 
     def forward(self, x):
         m = self.mamba.bidirectional(self.norm1(x))     # == mamba(n) + flip(mamba(flip(n)))
-        # bf16 FFN output (autocast) + fp32 residual: cast first, then a same-dtype add (ROCm's mixed-dtype
-        # add kernel took ~42 us on these [B, 201, 144] tensors; the cast and the add take ~5 us each)
-        return x + self.feed_forward(self.norm2(m)).to(x.dtype)
+        # x + feed_forward(norm2(m)).to(x.dtype): on the GPU two csrc/lgemm.hip launches each way (FFN1's bias +
+        # GELU and FFN2's bias + widening + residual add in the GEMM epilogues)
+        return ffn_residual(x, self.norm2(m), self.feed_forward[0], self.feed_forward[2])
 
 
 class SELayer(nn.Module):

@@ -133,6 +133,8 @@ SIGNATURES = {
     "rdx_hgemm": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64, c_vp,
                           c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "rdx_hgemm_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
+    "rdx_lgemm": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_int, c_vp, c_int,
+                          c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "rdx_hgemm_counters": (c_i64, [c_int, c_int, c_int]),
     "rdx_hgemm_sk_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
     "rdx_gemm_bf16_strided": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,

@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import _lib, ops
 
 _SIDE = {}
 _JOIN_QUEUED = [False]
@@ -55,6 +55,27 @@ def _cast(t, dt):
     return t.to(dt)
 
 
+def _cast_t(weight, wc):
+    """wc^T contiguous ([in, out]: the input-gradient GEMM's weight operand), through the window's cast cache like
+    _cast (the parameters do not change within a window)."""
+    cache = ops.SCONV_WCACHE
+    if cache is not None and isinstance(weight, nn.Parameter):
+        key = ("linT", id(weight), wc.dtype)
+        hit = cache.get(key)
+        if hit is not None and hit[0] is weight and hit[1].dtype == wc.dtype:
+            return hit[1]
+        c = wc.t().contiguous()
+        cache[key] = (weight, c)
+        return c
+    return wc.t().contiguous()
+
+
+def _rows(t):
+    """t as a 2-D [rows, last] view (no copy when the leading dimensions collapse), unit inner stride."""
+    t2 = t.reshape(-1, t.shape[-1])
+    return t2 if t2.stride(-1) == 1 else t2.contiguous()
+
+
 def direct_grad(p):
     """True for parameters whose gradient SideLinear accumulates into .grad itself (window.py keeps their
     .grad bound during a pass instead of handing it over through autograd)."""
@@ -65,7 +86,12 @@ class SideLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, dt):
         xc, wc, bc = x.to(dt), _cast(weight, dt), _cast(bias, dt)
-        y = F.linear(xc, wc, bc)
+        if _LGEMM and xc.is_cuda and dt in ops.HALF:
+            # csrc/lgemm.hip: one launch per head linear (hipBLASLt took 7-9 us on these narrow shapes)
+            y = torch.empty(*xc.shape[:-1], wc.shape[0], device=xc.device, dtype=dt)   # not a view: in-place
+            ops.lgemm(_rows(xc), wc, bc, out=y.view(-1, wc.shape[0]))                  # consumers (SE's ReLU)
+        else:
+            y = F.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.x_dtype = x.dtype
         ctx.params = (weight, bias)
@@ -78,46 +104,103 @@ class SideLinearFn(torch.autograd.Function):
         dy = dy.to(wc.dtype)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dy, wc).to(ctx.x_dtype)
-        need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        x2 = xc.reshape(-1, xc.shape[-1])
-        direct = (dy.is_cuda and need_w and weight.grad is not None and weight.grad.dtype == torch.float32
-                  and (not need_b or (bias.grad is not None and bias.grad.dtype == torch.float32)))
-        if not direct:
-            gw = torch.matmul(dy2.t(), x2).to(weight.dtype) if need_w else None
-            gb = dy2.sum(0, dtype=torch.float32).to(bias.dtype) if need_b else None
-            return dx, gw, gb, None
-        dev = dy.device
-        cur = torch.cuda.current_stream(dev)
-        side = _side(dev) if _MODE != "2" else cur
-        if side is not cur:
-            side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            if (_WGRAD and dy2.dtype in ops.HALF and x2.dtype == dy2.dtype and dy2.stride(-1) == 1
-                    and x2.stride(-1) == 1 and weight.grad.is_contiguous()):
-                # one split-over-tokens MFMA pass + a fixed-order reduce into .grad (csrc/wgrad.hip): hipBLASLt
-                # ran these long-K, tiny-output GEMMs on 5-27 workgroups
-                ops.wgrad_acc(dy2, x2, weight.grad, bias.grad if need_b else None)
-            elif dy2.dtype == torch.float32:
-                weight.grad.addmm_(dy2.t(), x2)
+            if _LGEMM and dy.is_cuda and wc.dtype in ops.HALF:
+                dx = ops.lgemm(_rows(dy), _cast_t(weight, wc),
+                               out_dtype=torch.float32 if ctx.x_dtype == torch.float32 else None)
+                dx = dx.to(ctx.x_dtype).view(*dy.shape[:-1], wc.shape[1])
             else:
-                torch.ops.aten.addmm.dtype_out(weight.grad, dy2.t(), x2, torch.float32, beta=1, alpha=1,
-                                               out=weight.grad)
-            if need_b and not (_WGRAD and dy2.dtype in ops.HALF and x2.dtype == dy2.dtype
-                               and dy2.stride(-1) == 1 and x2.stride(-1) == 1 and weight.grad.is_contiguous()):
-                bias.grad.add_(dy2.sum(0, dtype=torch.float32))
-        if side is cur:
-            return dx, None, None, None
+                dx = torch.matmul(dy, wc).to(ctx.x_dtype)
+        need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
+        gw, gb = _weight_grads(dy.reshape(-1, dy.shape[-1]), xc.reshape(-1, xc.shape[-1]), weight, bias, need_w, need_b)
+        return dx, gw, gb, None
+
+
+def _weight_grads(dy2, x2, weight, bias, need_w, need_b):
+    """The linear's weight / bias gradients from dy2 [M, N] and x2 [M, K]: accumulated in fp32 straight into .grad
+    when it is bound (returns None, None), else returned for autograd."""
+    direct = (dy2.is_cuda and need_w and weight.grad is not None and weight.grad.dtype == torch.float32
+              and (not need_b or (bias.grad is not None and bias.grad.dtype == torch.float32)))
+    if not direct:
+        gw = torch.matmul(dy2.t(), x2).to(weight.dtype) if need_w else None
+        gb = dy2.sum(0, dtype=torch.float32).to(bias.dtype) if need_b else None
+        return gw, gb
+    dev = dy2.device
+    cur = torch.cuda.current_stream(dev)
+    side = _side(dev) if _MODE != "2" else cur
+    if side is not cur:
+        side.wait_stream(cur)
+    fast = (_WGRAD and dy2.dtype in ops.HALF and x2.dtype == dy2.dtype and dy2.stride(-1) == 1
+            and x2.stride(-1) == 1 and weight.grad.is_contiguous())
+    with torch.cuda.stream(side):
+        if fast:
+            # one split-over-tokens MFMA pass + a fixed-order reduce into .grad (csrc/wgrad.hip): hipBLASLt
+            # ran these long-K, tiny-output GEMMs on 5-27 workgroups
+            ops.wgrad_acc(dy2, x2, weight.grad, bias.grad if need_b else None)
+        elif dy2.dtype == torch.float32:
+            weight.grad.addmm_(dy2.t(), x2)
+        else:
+            torch.ops.aten.addmm.dtype_out(weight.grad, dy2.t(), x2, torch.float32, beta=1, alpha=1,
+                                           out=weight.grad)
+        if need_b and not fast:
+            bias.grad.add_(dy2.sum(0, dtype=torch.float32))
+    if side is not cur:
         dy2.record_stream(side)
         x2.record_stream(side)
         if not _JOIN_QUEUED[0]:
             _JOIN_QUEUED[0] = True
             torch.autograd.Variable._execution_engine.queue_callback(_join(dev))
-        return dx, None, None, None
+    return None, None
+
+
+class FFNResidualFn(torch.autograd.Function):
+    """x + Linear2(GELU(Linear1(n))).to(x.dtype) (PN_BiMambas_Encoder's feed-forward and residual,
+    src/models/DualStreamSEMamba.py:467-486) in two csrc/lgemm.hip launches each way: FFN1's bias + GELU in its
+    epilogue (u kept for the backward), FFN2's bias, widening and residual add in its epilogue; backward: FFN2's
+    input gradient times gelu'(u) in one launch, FFN1's input gradient, the weight gradients as SideLinear's.
+    The roundings are autocast's: u, gelu(u), the FFN output and d u in the 16-bit dtype."""
+
+    @staticmethod
+    def forward(ctx, x, n, w1, b1, w2, b2, dt):
+        n2 = _rows(n.to(dt))
+        w1c, b1c, w2c, b2c = _cast(w1, dt), _cast(b1, dt), _cast(w2, dt), _cast(b2, dt)
+        u, h = ops.lgemm(n2, w1c, b1c, epilogue=_lib.EPI_BIAS_GELU)
+        if x.dtype == torch.float32:
+            y = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+            ops.lgemm(h, w2c, b2c, out_dtype=torch.float32, residual=_rows(x), out=y.view(-1, x.shape[-1]))
+        else:
+            y = x + ops.lgemm(h, w2c, b2c).to(x.dtype).view(x.shape)
+        ctx.save_for_backward(n2, u, h, w1c, w2c)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.n_dtype = n.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n2, u, h, w1c, w2c = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        dy2 = _rows(dy.to(w2c.dtype))
+        du = ops.lgemm(dy2, _cast_t(w2, w2c), epilogue=_lib.EPI_GELU_BWD, aux=u)
+        dn = None
+        if ctx.needs_input_grad[1]:
+            dn = ops.lgemm(du, _cast_t(w1, w1c)).to(ctx.n_dtype).view(*dy.shape[:-1], w1c.shape[1])
+        gw2, gb2 = _weight_grads(dy2, h, w2, b2, ctx.needs_input_grad[4], b2 is not None and ctx.needs_input_grad[5])
+        gw1, gb1 = _weight_grads(du, n2, w1, b1, ctx.needs_input_grad[2], b1 is not None and ctx.needs_input_grad[3])
+        return dy, dn, gw1, gb1, gw2, gb2, None
+
+
+def ffn_residual(x, n, lin1, lin2):
+    """x + lin2(gelu(lin1(n))).to(x.dtype) with FFNResidualFn on the GPU under 16-bit autocast (lgemm on), else the
+    module path."""
+    if (_LGEMM and _ON and n.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") in ops.HALF and x.dtype in (torch.float32, *ops.HALF)):
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return FFNResidualFn.apply(x, n, lin1.weight, lin1.bias, lin2.weight, lin2.bias, dt)
+    return x + lin2(F.gelu(lin1(n))).to(x.dtype)
 
 
 _WGRAD = os.environ.get("RADHIP_WGRAD", "1") != "0"     # csrc/wgrad.hip for the 16-bit weight gradients
+_LGEMM = os.environ.get("RADHIP_LGEMM", "1") != "0"     # csrc/lgemm.hip for the forward / input-gradient GEMMs
 _MODE = os.environ.get("RADHIP_SIDE_LINEAR", "2")   # "2": main stream; "1": side stream; "0": F.linear
 _ON = _MODE != "0"
 

@@ -1254,17 +1254,23 @@ def attn_keep_mask(B, T, H, p_drop, device):
 
 
 _ATTN_WS = {}
+_ATTN_NEED = {}   # device index -> (floats, counters): the largest split-backward workspace an eager launch asked for
 
 
 def _attn_split_workspace(dev, n_floats, n_counters):
     """fp32 partial dQ / d gate and the per-(b, h) tickets of the split attention backward, one per (device,
     stream): launches on one stream run one after another, launches in flight on two streams must not share them;
-    the tickets are zeroed here once and left at zero by each launch. Grown outside graph capture only."""
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    the tickets are zeroed here once and left at zero by each launch. Captured launches take the device's graph
+    workspace, reserved before capture by reserve_graph_workspace (the captured graphs replay one after another)."""
+    need = _ATTN_NEED.get(dev.index, (0, 0))
+    _ATTN_NEED[dev.index] = (max(need[0], n_floats), max(need[1], n_counters))
+    capturing = torch.cuda.is_current_stream_capturing()
+    key = (dev.index, "graph") if capturing else (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     cur = _ATTN_WS.get(key)
     if cur is None or cur[0].numel() < n_floats or cur[1].numel() < n_counters:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("radhip attention: split-backward workspace must be allocated before graph capture")
+        if capturing:
+            raise RuntimeError("radhip attention: split-backward graph workspace not reserved before capture "
+                               "(ops.reserve_graph_workspace after an eager warm-up)")
         cur = (torch.empty(max(n_floats, cur[0].numel() if cur else 0), dtype=torch.float32, device=dev),
                torch.zeros(max(n_counters, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
         _ATTN_WS[key] = cur
@@ -1281,10 +1287,10 @@ def attn_bwd_launch(q, ldq, k, ldk, v, ldv, gate, rel, mask, seed, salt, p_drop,
     if fused_bwd_enabled(T):
         if p_drop > 0 and mask is None:
             raise RuntimeError("fused attention backward with dropout needs the forward's keep mask")
-        if B * H < 256 and (B * H) % 8 == 0 and os.environ.get("RADHIP_ATTN_SPLIT", "0") == "1":
-            # opt-in: two workgroups per (b, h) over the key tiles, the second to finish combines dQ / d gate
-            # (fills the chip at B = 8, but measured 4.6 vs 4.2 ms of attention backward per step in the
-            # bench: the combine's extra dQ traffic and the halved per-workgroup key reuse cost more)
+        if B * H < 256 and (B * H) % 8 == 0 and os.environ.get("RADHIP_ATTN_SPLIT", "1") == "1":
+            # B = 8: two workgroups per (b, h) over the key tiles, the second to finish combines dQ / d gate (fills
+            # the chip; partials published write-through): 3.83 vs 4.01 ms of attention backward per step in-step
+            # (profiles/r05_ab/asplit_*.json); RADHIP_ATTN_SPLIT=0 keeps one workgroup per (b, h)
             ws, cnt = _attn_split_workspace(gate.device, int(lib().rdx_attn_bwd_split_ws(B, H)), B * H)
             return check(L.rdx_attn_bwd_fused_split(q, ldq, k, ldk, v, ldv, _p(gate), _p(rel),
                                                         _p(mask) if mask is not None else None, p_drop, 0.125, o,
@@ -1589,16 +1595,18 @@ def _wgemm_workspace(dev, ws_bytes, n_counters):
 
 
 def reserve_graph_workspace(dev):
-    """Allocate (outside capture) the graph split-K workspace at the largest size an eager launch on `dev` needed."""
+    """Allocate (outside capture) the graph workspaces (split-K GEMM, split attention backward) at the largest size
+    an eager launch on `dev` needed."""
     dev = torch.device(dev)
-    nb, nc = _WG_NEED.get(dev.index, (0, 0))
-    if nb == 0:
-        return
     key = (dev.index, "graph")
-    cur = _WG_WS.get(key)
-    if cur is None or cur[0].numel() < nb or cur[1].numel() < nc:
-        _WG_WS[key] = (torch.empty(max(nb, cur[0].numel() if cur else 0), dtype=torch.uint8, device=dev),
-                       torch.zeros(max(nc, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
+    for table, need, dt in ((_WG_WS, _WG_NEED, torch.uint8), (_ATTN_WS, _ATTN_NEED, torch.float32)):
+        nb, nc = need.get(dev.index, (0, 0))
+        if nb == 0:
+            continue
+        cur = table.get(key)
+        if cur is None or cur[0].numel() < nb or cur[1].numel() < nc:
+            table[key] = (torch.empty(max(nb, cur[0].numel() if cur else 0), dtype=dt, device=dev),
+                          torch.zeros(max(nc, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
 
 
 def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm",
@@ -1761,3 +1769,46 @@ def feature_encoder_fused(x, ops_):
                   "fe_ln_gelu")
         h, T = (out32 if last else y), To
     return h
+
+
+# ------------------------------------------------------------------- detector-head small GEMMs ----
+def lgemm(a, w, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out_dtype=None, residual=None, out=None, aux_out=None,
+          name="lgemm"):
+    """C[M, N] = a[M, K] @ w[N, K]^T (+ fused epilogue) on csrc/lgemm.hip, the head's small-GEMM kernel: a 16-bit
+    or fp32 (rounded to w's 16-bit dtype on load) 2-D view with unit inner stride and any row stride, w 16-bit.
+    out_dtype: w.dtype (default) or torch.float32 (the 16-bit result widened). residual [M, N] in the output dtype:
+    C = residual + C (rounded in 16 bits; `out` may be `residual` itself: in-place accumulation). EPI_BIAS_GELU
+    returns (u, gelu(u)); EPI_GELU_BWD multiplies by gelu'(aux)."""
+    _require_gpu(a, w)
+    if w.dtype not in HALF or a.dtype not in (w.dtype, torch.float32) or a.dim() != 2 or w.dim() != 2:
+        raise ValueError("radhip lgemm: 2-D a (16-bit or fp32) and 16-bit w required")
+    if a.stride(-1) != 1 or w.stride(-1) != 1:
+        raise ValueError("radhip lgemm: unit inner stride required")
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2:
+        raise ValueError(f"radhip lgemm: K {K} vs {K2}")
+    od = w.dtype if out_dtype is None else out_dtype
+    if od not in (w.dtype, torch.float32):
+        raise ValueError("radhip lgemm: output in w's dtype or fp32")
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=od)
+    if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
+        aux_out = torch.empty(M, N, device=a.device, dtype=w.dtype)
+    for t in (bias, aux, aux_out):
+        if t is not None and (t.dtype != w.dtype or t.stride(-1) != 1):
+            raise ValueError("radhip lgemm: bias / aux in w's dtype with unit inner stride")
+    if residual is not None and (residual.dtype != od or residual.stride(-1) != 1 or residual.shape != (M, N)):
+        raise ValueError("radhip lgemm: residual [M, N] in the output dtype with unit inner stride")
+    if out.shape != (M, N) or out.dtype != od or out.stride(-1) != 1:
+        raise ValueError("radhip lgemm: out [M, N] in the output dtype with unit inner stride")
+    with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
+        check(_L(w).rdx_lgemm(_p(a), a.stride(0), int(a.dtype == torch.float32), _p(w), w.stride(0), _p(out),
+                              out.stride(0), int(od == torch.float32), M, N, K,
+                              _p(bias) if bias is not None else None, int(epilogue),
+                              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                              _p(aux_out) if aux_out is not None else None,
+                              aux_out.stride(0) if aux_out is not None else 0,
+                              _p(residual) if residual is not None else None,
+                              residual.stride(0) if residual is not None else 0, _stream(w)), "lgemm")
+    return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
