@@ -5,12 +5,11 @@
 // The head's shapes are narrow (N, K in {1, 2, 9, 41, 64, 144, 288, 576, 1024}) over 1 608 - 12 864 token rows: each
 // GEMM is a few hundred MFLOP and its time is launch and load latency, not arithmetic (hipBLASLt took 7-9 us per
 // call on them, and the casts, GELU, residual add and bias reduction around them were launches of their own). Here a
-// 256-thread workgroup owns 32 token rows x 64 output features; it loads whole K chunks of 320 (every head K but
-// 576 and 1024 in one chunk) with all of its loads in flight at once, prefetching the next chunk into registers
-// while the MFMAs (v_mfma_f32_16x16x32, wave w: features 16 w .. 16 w + 15 of the tile, both 16-row token tiles)
-// run on the current one from LDS. Operands may be strided views with any K (the x_proj output's dt columns):
-// 16-byte loads where rows are 16-byte aligned, element loads with zero fill elsewhere. A may be fp32 (converted to
-// the 16-bit type on load, the cast F.linear's autocast does first).
+// 256-thread workgroup owns 32 token rows x 64 output features and stages K in LDS with every load of a chunk in
+// flight at once: 16-bit operands with aligned rows by LDS-DMA (buffer_load ... lds, 36 VGPRs; chunks of up to 640,
+// every head K but 1024 in one), others (fp32 A converted on load, strided views with any K such as the x_proj
+// output's dt columns) through registers with zero-filled element loads (chunks of up to 320).
+// The MFMAs are v_mfma_f32_16x16x32, wave w: features 16 w .. 16 w + 15 of the tile against both 16-row token tiles.
 //
 // Epilogues, each the rounding sequence of the unfused autocast ops:
 //   RDX_EPI_BIAS      C = half(acc + bias)                         (F.linear; bias optional)
@@ -26,13 +25,10 @@ namespace lg {
 
 constexpr int BM = 32;          // token rows per workgroup
 constexpr int BN = 64;          // output features per workgroup (16 per wave)
-constexpr int KC = 320;         // K chunk staged in LDS
-constexpr int KP = KC + 8;      // LDS row pitch (16-bit elements): 656 B, rows 36 banks apart (conflict-free b128)
 constexpr int T = 256;
-constexpr int CH = KC / 8;      // 16-byte items per row chunk
-constexpr int A_IT = BM * CH / T;   // 5
-constexpr int B_IT = BN * CH / T;   // 10
-constexpr int LDS = (BM + BN) * KP * 2;
+// K is staged in LDS in chunks, kce = the chunk rounded up to 32 elements; LDS is sized by the launch. Register-path rows are kce + 8 elements: a pitch of an odd number of
+// 16-byte bank groups, so the 16 rows one ds_read_b128 covers fall on distinct groups.
+__host__ __device__ constexpr int kce_of(int KC, int K) { return K < KC ? ((K + 31) / 32) * 32 : KC; }
 
 struct Args {
   const void* A;     // [M, K] rows at lda (16-bit storage type, or fp32 when A_F32)
@@ -49,86 +45,167 @@ struct Args {
   const void* R;     // residual [M, N] of C's type, rows at ldr, or null
   int64_t ldr;
   int M, N, K;
-  int vec_a, vec_w;  // rows 16-byte aligned (16-byte loads where 8 elements fit)
+  int vec_a, vec_w;  // rows 16-byte aligned and K % 8 == 0 (16-byte loads)
   int vec_c;         // C rows 8-byte (16-bit) / 16-byte (fp32) aligned
 };
 
-// 8 consecutive elements of row `row` from column k as packed 16-bit values, zero past nrows / K
+// 8 consecutive elements of row `row` from column k as packed 16-bit values, zero past nrows / K. Buffer loads:
+// an invalid element gets an offset past the buffer's range and reads as 0, so no load sits in a branch and every
+// load of a chunk is in flight before the first wait.
+constexpr uint32_t OOB = 0x80000000u;
 template <bool F32>
-__device__ __forceinline__ uint4 load8(const void* base, int64_t ld, int row, int nrows, int k, int K, bool vec) {
-  uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  if (row >= nrows || k >= K) return z;
-  if constexpr (F32) {
-    const float* p = reinterpret_cast<const float*>(base) + (int64_t)row * ld + k;
-    float v[8];
-    if (vec && k + 8 <= K) {
-      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+__device__ __forceinline__ uint4 load8(__amdgpu_buffer_rsrc_t rs, int64_t ld, int row, int nrows, int k, int K,
+                                       bool vec) {
+  constexpr int ES = F32 ? 4 : 2;
+  const bool rv = row < nrows;
+  const uint32_t base = (uint32_t)(((int64_t)row * ld + k) * ES);
+  if (vec) {   // rows 16-byte aligned and K % 8 == 0: whole 16-byte items
+    const uint32_t off = (rv && k + 8 <= K) ? base : OOB;
+    if constexpr (F32) {
+      const uint4 a = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      const uint4 b = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+      const float v[8] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w),
+                          __uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w)};
+      return make_uint4(hpack2(v[0], v[1]), hpack2(v[2], v[3]), hpack2(v[4], v[5]), hpack2(v[6], v[7]));
     } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = k + j < K ? p[j] : 0.f;
+      return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
-    return make_uint4(hpack2(v[0], v[1]), hpack2(v[2], v[3]), hpack2(v[4], v[5]), hpack2(v[6], v[7]));
-  } else {
-    const uint16_t* p = reinterpret_cast<const uint16_t*>(base) + (int64_t)row * ld + k;
-    if (vec && k + 8 <= K) return *reinterpret_cast<const uint4*>(p);
-    uint32_t w[4];
+  } else {     // element loads (unaligned rows: the x_proj output's dt columns, odd widths)
+    if constexpr (F32) {
+      float t[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t lo = k + 2 * j < K ? p[2 * j] : 0u, hi = k + 2 * j + 1 < K ? p[2 * j + 1] : 0u;
-      w[j] = lo | (hi << 16);
+      for (int j = 0; j < 8; ++j)
+        t[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (rv && k + j < K) ? base + 4 * j : OOB, 0, 0));
+      return make_uint4(hpack2(t[0], t[1]), hpack2(t[2], t[3]), hpack2(t[4], t[5]), hpack2(t[6], t[7]));
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b16(rs, (rv && k + 2 * j < K) ? base + 4 * j : OOB, 0, 0);
+        const uint32_t hi =
+            __builtin_amdgcn_raw_buffer_load_b16(rs, (rv && k + 2 * j + 1 < K) ? base + 4 * j + 2 : OOB, 0, 0);
+        w[j] = lo | (hi << 16);
+      }
+      return make_uint4(w[0], w[1], w[2], w[3]);
     }
-    return make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
-template <bool A_F32, bool C_F32, int EPI>
+typedef __attribute__((ext_vector_type(4))) int lg_i32x4;
+__device__ void lg_load_lds(lg_i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds, int size, int voffset,
+                            int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+__device__ __forceinline__ lg_i32x4 lg_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  lg_i32x4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)(uint32_t)(a >> 32);
+  r.z = (int)bytes;
+  r.w = 0x00020000;  // raw buffer, range-checked
+  return r;
+}
+
+// DMA: 16-bit operands with 16-byte aligned rows and K % 8 == 0 go global -> LDS by buffer_load ... lds (no
+// registers, every load of a chunk in flight at once) into chunk-major images: the 16-byte item (k chunk j, row r)
+// at 16 (j ROWS + r), so a wave instruction fills 64 consecutive items and the 16 rows one MFMA operand read covers
+// are 256 contiguous bytes (conflict-free). Otherwise (fp32 A, unaligned rows, K % 8 != 0) through registers into
+// row-major images of pitch kce + 8.
+template <bool A_F32, bool C_F32, int EPI, bool DMA>
 __global__ __launch_bounds__(T, 2) void lgemm_kernel(Args g) {
+  constexpr int KC = DMA ? 640 : 320;
+  constexpr int A_IT = DMA ? 1 : BM * (KC / 8) / T;   // 5
+  constexpr int B_IT = DMA ? 1 : BN * (KC / 8) / T;   // 10
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  uint16_t* As = reinterpret_cast<uint16_t*>(lds);   // [BM][KP]
-  uint16_t* Ws = As + BM * KP;                         // [BN][KP]
+  const int kce = kce_of(KC, g.K);
+  const int KP = kce + 8;
+  uint16_t* As = reinterpret_cast<uint16_t*>(lds);                      // register path: [BM][KP]
+  uint16_t* Ws = As + BM * KP;                                          //                [BN][KP]
+  char* Ab = lds;                                                       // DMA path: [kce / 8][BM] items
+  char* Wb = lds + (kce / 8) * BM * 16;                                 //           [kce / 8][BN] items
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int nch = (g.K + KC - 1) / KC;
-  uint4 ra[A_IT], rw[B_IT];
-  auto fetch = [&](int c) {
-    const int k0 = c * KC, kcp = min(KC, ((g.K - k0 + 31) / 32) * 32);
-#pragma unroll
-    for (int i = 0; i < A_IT; ++i) {
-      const int it = tid + T * i, row = it / CH, kk = (it % CH) * 8;
-      ra[i] = kk < kcp ? load8<A_F32>(g.A, g.lda, m0 + row, g.M, k0 + kk, g.K, g.vec_a) : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int i = 0; i < B_IT; ++i) {
-      const int it = tid + T * i, row = it / CH, kk = (it % CH) * 8;
-      rw[i] = kk < kcp ? load8<false>(g.W, g.ldw, n0 + row, g.N, k0 + kk, g.K, g.vec_w) : make_uint4(0u, 0u, 0u, 0u);
-    }
-  };
+  const uint32_t abytes = (uint32_t)(((int64_t)(g.M - 1) * g.lda + g.K) * (A_F32 ? 4 : 2));
+  const uint32_t wbytes = (uint32_t)(((int64_t)(g.N - 1) * g.ldw + g.K) * 2);
   rdx_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  fetch(0);
-  for (int c = 0; c < nch; ++c) {
-    const int k0 = c * KC, kcp = min(KC, ((g.K - k0 + 31) / 32) * 32);
-    if (c > 0) __syncthreads();   // the previous chunk's MFMA reads are done
-#pragma unroll
-    for (int i = 0; i < A_IT; ++i) {
-      const int it = tid + T * i, row = it / CH, kk = (it % CH) * 8;
-      if (kk < kcp) *reinterpret_cast<uint4*>(As + row * KP + kk) = ra[i];
+  if constexpr (DMA) {
+    const lg_i32x4 ra = lg_rsrc(g.A, abytes), rw = lg_rsrc(g.W, wbytes);
+    for (int c = 0; c < nch; ++c) {
+      const int k0 = c * KC, kcp = min(KC, ((g.K - k0 + 31) / 32) * 32), nj = kcp / 8;
+      if (c > 0) __syncthreads();   // the previous chunk's MFMA reads are done
+      for (int q = wv; q < nj / 2; q += 4) {      // A: two k chunks of 32 rows per instruction
+        const int i = 64 * q + lane, j = i / BM, r = i % BM;
+        const bool ok = m0 + r < g.M && k0 + 8 * j < g.K;
+        const int off = ok ? (int)((((int64_t)(m0 + r)) * g.lda + k0 + 8 * j) * 2) : (int)OOB;
+        lg_load_lds(ra, (__attribute__((address_space(3))) uint32_t*)(Ab + 1024 * q), 16, off, 0, 0, 0);
+      }
+      for (int q = wv; q < nj; q += 4) {          // W: one k chunk of 64 rows per instruction
+        const bool ok = n0 + lane < g.N && k0 + 8 * q < g.K;
+        const int off = ok ? (int)((((int64_t)(n0 + lane)) * g.ldw + k0 + 8 * q) * 2) : (int)OOB;
+        lg_load_lds(rw, (__attribute__((address_space(3))) uint32_t*)(Wb + 1024 * q), 16, off, 0, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      const char* wp = Wb + (16 * wv + l16) * 16 + lg * BN * 16;
+      const char* ap0 = Ab + l16 * 16 + lg * BM * 16;
+      const char* ap1 = ap0 + 16 * 16;
+      for (int ks = 0; ks < kcp; ks += 32) {     // K step = 4 chunks
+        const int j4 = ks / 8;
+        const hx8 w = *reinterpret_cast<const hx8*>(wp + j4 * BN * 16);
+        const hx8 a0 = *reinterpret_cast<const hx8*>(ap0 + j4 * BM * 16);
+        const hx8 a1 = *reinterpret_cast<const hx8*>(ap1 + j4 * BM * 16);
+        acc0 = mfma16x16x32(w, a0, acc0);
+        acc1 = mfma16x16x32(w, a1, acc1);
+      }
     }
+  } else {
+    uint4 ra[A_IT], rw[B_IT];
+    // byte ranges of the operands (the last row ends at K): offsets past them read 0
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g.A), 0, (int)abytes,
+                                                                          0x00020000);
+    const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(const_cast<hst*>(g.W), 0, (int)wbytes,
+                                                                          0x00020000);
+    // items enumerated chunk-major (item it: k chunk it / ROWS, row it % ROWS), so whether a wave's items lie inside
+    // the chunk's kcp is the same for all its lanes: items past it issue no loads at all
+    auto fetch = [&](int c) {
+      const int k0 = c * KC, nj = min(KC, ((g.K - k0 + 31) / 32) * 32) / 8;
 #pragma unroll
-    for (int i = 0; i < B_IT; ++i) {
-      const int it = tid + T * i, row = it / CH, kk = (it % CH) * 8;
-      if (kk < kcp) *reinterpret_cast<uint4*>(Ws + row * KP + kk) = rw[i];
-    }
-    __syncthreads();
-    if (c + 1 < nch) fetch(c + 1);
-    // D^T tiles: A operand = the weights (rows = features 16 wv + l16), B operand = tokens l16 / 16 + l16
-    const uint16_t* wp = Ws + (16 * wv + l16) * KP + 8 * lg;
-    const uint16_t* ap0 = As + l16 * KP + 8 * lg;
-    const uint16_t* ap1 = ap0 + 16 * KP;
-    for (int ks = 0; ks < kcp; ks += 32) {
-      const hx8 w = *reinterpret_cast<const hx8*>(wp + ks);
-      acc0 = mfma16x16x32(w, *reinterpret_cast<const hx8*>(ap0 + ks), acc0);
-      acc1 = mfma16x16x32(w, *reinterpret_cast<const hx8*>(ap1 + ks), acc1);
+      for (int i = 0; i < A_IT; ++i) {
+        const int it = tid + T * i, j = it / BM, row = it % BM;
+        ra[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (j < nj) ra[i] = load8<A_F32>(rsa, g.lda, m0 + row, g.M, k0 + 8 * j, g.K, g.vec_a);
+      }
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i) {
+        const int it = tid + T * i, j = it / BN, row = it % BN;
+        rw[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (j < nj) rw[i] = load8<false>(rsw, g.ldw, n0 + row, g.N, k0 + 8 * j, g.K, g.vec_w);
+      }
+    };
+    fetch(0);
+    for (int c = 0; c < nch; ++c) {
+      const int kcp = min(KC, ((g.K - c * KC + 31) / 32) * 32);
+      if (c > 0) __syncthreads();   // the previous chunk's MFMA reads are done
+#pragma unroll
+      for (int i = 0; i < A_IT; ++i) {
+        const int it = tid + T * i, j = it / BM, row = it % BM;
+        if (8 * j < kcp) *reinterpret_cast<uint4*>(As + row * KP + 8 * j) = ra[i];
+      }
+#pragma unroll
+      for (int i = 0; i < B_IT; ++i) {
+        const int it = tid + T * i, j = it / BN, row = it % BN;
+        if (8 * j < kcp) *reinterpret_cast<uint4*>(Ws + row * KP + 8 * j) = rw[i];
+      }
+      __syncthreads();
+      if (c + 1 < nch) fetch(c + 1);
+      // D^T tiles: A operand = the weights (rows = features 16 wv + l16), B operand = tokens l16 / 16 + l16
+      const uint16_t* wp = Ws + (16 * wv + l16) * KP + 8 * lg;
+      const uint16_t* ap0 = As + l16 * KP + 8 * lg;
+      const uint16_t* ap1 = ap0 + 16 * KP;
+      for (int ks = 0; ks < kcp; ks += 32) {
+        const hx8 w = *reinterpret_cast<const hx8*>(wp + ks);
+        acc0 = mfma16x16x32(w, *reinterpret_cast<const hx8*>(ap0 + ks), acc0);
+        acc1 = mfma16x16x32(w, *reinterpret_cast<const hx8*>(ap1 + ks), acc1);
+      }
     }
   }
   // lane holds features n = n0 + 16 wv + 4 lg + i (i < 4) of token m0 + l16 (acc0) and m0 + 16 + l16 (acc1)
@@ -191,19 +268,27 @@ __global__ __launch_bounds__(T, 2) void lgemm_kernel(Args g) {
   }
 }
 
-template <bool A_F32, bool C_F32, int EPI>
-int launch(const Args& g, hipStream_t st) {
+template <bool A_F32, bool C_F32, int EPI, bool DMA>
+int launch_dma(const Args& g, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lgemm_kernel<A_F32, C_F32, EPI>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lgemm_kernel<A_F32, C_F32, EPI, DMA>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             DMA ? (BM + BN) * 640 * 2 : (BM + BN) * (320 + 8) * 2);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  hipLaunchKernelGGL((lgemm_kernel<A_F32, C_F32, EPI>), dim3((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM)),
-                     dim3(T), LDS, st, g);
+  const int lds = DMA ? (BM + BN) * kce_of(640, g.K) * 2 : (BM + BN) * (kce_of(320, g.K) + 8) * 2;
+  hipLaunchKernelGGL((lgemm_kernel<A_F32, C_F32, EPI, DMA>),
+                     dim3((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM)), dim3(T), lds, st, g);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
+}
+template <bool A_F32, bool C_F32, int EPI>
+int launch(const Args& g, hipStream_t st) {
+  if constexpr (!A_F32)
+    if (g.vec_a && g.vec_w) return launch_dma<false, C_F32, EPI, true>(g, st);
+  return launch_dma<A_F32, C_F32, EPI, false>(g, st);
 }
 
 }  // namespace lg
@@ -222,8 +307,8 @@ extern "C" int rdx_lgemm(const void* A, int64_t lda, int a_f32, const void* W, i
   RDX_REQUIRE(!R || ldr >= N);
   lg::Args g{A, lda, (const hst*)W, ldw, C, ldc, (const hst*)bias, (const hst*)aux, ldaux, (hst*)aux_out, ldao,
              R, ldr, M, N, K, 0, 0, 0};
-  g.vec_a = (((uintptr_t)A & 15) == 0 && (lda % (a_f32 ? 4 : 8)) == 0) ? 1 : 0;
-  g.vec_w = (((uintptr_t)W & 15) == 0 && (ldw % 8) == 0) ? 1 : 0;
+  g.vec_a = (((uintptr_t)A & 15) == 0 && (lda % (a_f32 ? 4 : 8)) == 0 && K % 8 == 0) ? 1 : 0;
+  g.vec_w = (((uintptr_t)W & 15) == 0 && (ldw % 8) == 0 && K % 8 == 0) ? 1 : 0;
   g.vec_c = c_f32 ? ((((uintptr_t)C & 15) == 0 && (ldc % 4) == 0) ? 1 : 0)
                   : ((((uintptr_t)C & 7) == 0 && (ldc % 4) == 0) ? 1 : 0);
   const hipStream_t st = as_stream(stream);

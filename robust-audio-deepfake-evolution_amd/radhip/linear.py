@@ -70,10 +70,21 @@ def _cast_t(weight, wc):
     return wc.t().contiguous()
 
 
+LG_MAX_K = 320     # csrc/lgemm.hip stages K <= 320 in one LDS chunk; its per-CU operand ingest loses to hipBLASLt above
+
+
+def _lg_ok(t, K):
+    """csrc/lgemm.hip for a plain (unfused) head GEMM with contraction length K."""
+    return _LGEMM and t.is_cuda and t.dtype in ops.HALF and K <= LG_MAX_K
+
+
 def _rows(t):
     """t as a 2-D [rows, last] view (no copy when the leading dimensions collapse), unit inner stride."""
     t2 = t.reshape(-1, t.shape[-1])
-    return t2 if t2.stride(-1) == 1 else t2.contiguous()
+    M, K = t2.shape
+    if (K > 1 and t2.stride(-1) != 1) or (M > 1 and t2.stride(0) < K):   # e.g. an expanded [M, 1] gradient
+        t2 = t2.clone(memory_format=torch.contiguous_format)
+    return t2
 
 
 def direct_grad(p):
@@ -86,8 +97,9 @@ class SideLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, dt):
         xc, wc, bc = x.to(dt), _cast(weight, dt), _cast(bias, dt)
-        if _LGEMM and xc.is_cuda and dt in ops.HALF:
-            # csrc/lgemm.hip: one launch per head linear (hipBLASLt took 7-9 us on these narrow shapes)
+        if _lg_ok(xc, wc.shape[1]):
+            # csrc/lgemm.hip at K <= 320 (3.5-5 us in a graph vs hipBLASLt's 4.4-6.5; longer K stays on hipBLASLt:
+            # tools/bench_lgemm.py, profiles/r05_bench_lgemm.jsonl)
             y = torch.empty(*xc.shape[:-1], wc.shape[0], device=xc.device, dtype=dt)   # not a view: in-place
             ops.lgemm(_rows(xc), wc, bc, out=y.view(-1, wc.shape[0]))                  # consumers (SE's ReLU)
         else:
@@ -104,7 +116,7 @@ class SideLinearFn(torch.autograd.Function):
         dy = dy.to(wc.dtype)
         dx = None
         if ctx.needs_input_grad[0]:
-            if _LGEMM and dy.is_cuda and wc.dtype in ops.HALF:
+            if _lg_ok(dy, wc.shape[0]):
                 dx = ops.lgemm(_rows(dy), _cast_t(weight, wc),
                                out_dtype=torch.float32 if ctx.x_dtype == torch.float32 else None)
                 dx = dx.to(ctx.x_dtype).view(*dy.shape[:-1], wc.shape[1])
@@ -181,8 +193,9 @@ class FFNResidualFn(torch.autograd.Function):
         dy2 = _rows(dy.to(w2c.dtype))
         du = ops.lgemm(dy2, _cast_t(w2, w2c), epilogue=_lib.EPI_GELU_BWD, aux=u)
         dn = None
-        if ctx.needs_input_grad[1]:
-            dn = ops.lgemm(du, _cast_t(w1, w1c)).to(ctx.n_dtype).view(*dy.shape[:-1], w1c.shape[1])
+        if ctx.needs_input_grad[1]:   # K = 4 d_model: hipBLASLt (see LG_MAX_K)
+            dn = (ops.lgemm(du, _cast_t(w1, w1c)) if _lg_ok(du, w1c.shape[0]) else torch.mm(du, w1c))
+            dn = dn.to(ctx.n_dtype).view(*dy.shape[:-1], w1c.shape[1])
         gw2, gb2 = _weight_grads(dy2, h, w2, b2, ctx.needs_input_grad[4], b2 is not None and ctx.needs_input_grad[5])
         gw1, gb1 = _weight_grads(du, n2, w1, b1, ctx.needs_input_grad[2], b1 is not None and ctx.needs_input_grad[3])
         return dy, dn, gw1, gb1, gw2, gb2, None

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import ops
 from ._lib import check, lib
-from .linear import SideLinear, _LGEMM, _ON, _cast, _cast_t, _rows, _weight_grads, side_linear
+from .linear import SideLinear, _LGEMM, _ON, _cast, _cast_t, _lg_ok, _rows, _weight_grads, side_linear
 from .ops import BiGate, DWConvBidir, SelectiveScan, SplitLast
 
 
@@ -201,6 +201,7 @@ class MambaBiFn(torch.autograd.Function):
         gw_in, _ = _weight_grads(dxz, n2, w_in, None, need[1], False)
         dx = None
         if need[0]:
-            dx = ops.lgemm(dxz, _cast_t(w_in, wi)).to(ctx.x_dtype).view(B, L, Dm)
+            dx = ops.lgemm(dxz, _cast_t(w_in, wi)) if _lg_ok(dxz, 2 * Di) else torch.mm(dxz, wi)   # K = 2 Di
+            dx = dx.to(ctx.x_dtype).view(B, L, Dm)
         return (dx, gw_in, totc[:Di * K].view(conv_w.shape), totc[Di * K:], gw_x, gw_dt, tot[Di * N + Di:],
                 tot[:Di * N].view(Di, N), tot[Di * N:Di * N + Di], gw_out, None)

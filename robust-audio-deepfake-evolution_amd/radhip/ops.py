@@ -1782,7 +1782,7 @@ def lgemm(a, w, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out_dtype=None, res
     _require_gpu(a, w)
     if w.dtype not in HALF or a.dtype not in (w.dtype, torch.float32) or a.dim() != 2 or w.dim() != 2:
         raise ValueError("radhip lgemm: 2-D a (16-bit or fp32) and 16-bit w required")
-    if a.stride(-1) != 1 or w.stride(-1) != 1:
+    if not ((a.stride(-1) == 1 or a.shape[1] == 1) and (w.stride(-1) == 1 or w.shape[1] == 1)):
         raise ValueError("radhip lgemm: unit inner stride required")
     M, K = a.shape
     N, K2 = w.shape
@@ -1795,20 +1795,26 @@ def lgemm(a, w, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out_dtype=None, res
         out = torch.empty(M, N, device=a.device, dtype=od)
     if epilogue == _lib.EPI_BIAS_GELU and aux_out is None:
         aux_out = torch.empty(M, N, device=a.device, dtype=w.dtype)
+    def unit(t):
+        return t.stride(-1) == 1 or t.shape[-1] == 1
     for t in (bias, aux, aux_out):
-        if t is not None and (t.dtype != w.dtype or t.stride(-1) != 1):
+        if t is not None and (t.dtype != w.dtype or not unit(t)):
             raise ValueError("radhip lgemm: bias / aux in w's dtype with unit inner stride")
-    if residual is not None and (residual.dtype != od or residual.stride(-1) != 1 or residual.shape != (M, N)):
+    if residual is not None and (residual.dtype != od or not unit(residual) or residual.shape != (M, N)):
         raise ValueError("radhip lgemm: residual [M, N] in the output dtype with unit inner stride")
-    if out.shape != (M, N) or out.dtype != od or out.stride(-1) != 1:
+    if out.shape != (M, N) or out.dtype != od or not unit(out):
         raise ValueError("radhip lgemm: out [M, N] in the output dtype with unit inner stride")
+    def ld(t, cols):   # row stride as the kernel reads it (any value for a single row)
+        return t.stride(0) if t.shape[0] > 1 else cols
+    if ld(a, K) < K or ld(w, K) < K or ld(out, N) < N:
+        raise ValueError("radhip lgemm: overlapping rows")
     with _timed(name, a, gemm_flops(M, N, K), shape=(M, N, K)):
-        check(_L(w).rdx_lgemm(_p(a), a.stride(0), int(a.dtype == torch.float32), _p(w), w.stride(0), _p(out),
-                              out.stride(0), int(od == torch.float32), M, N, K,
+        check(_L(w).rdx_lgemm(_p(a), ld(a, K), int(a.dtype == torch.float32), _p(w), ld(w, K), _p(out),
+                              ld(out, N), int(od == torch.float32), M, N, K,
                               _p(bias) if bias is not None else None, int(epilogue),
-                              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0,
+                              _p(aux) if aux is not None else None, ld(aux, N) if aux is not None else 0,
                               _p(aux_out) if aux_out is not None else None,
-                              aux_out.stride(0) if aux_out is not None else 0,
+                              ld(aux_out, N) if aux_out is not None else 0,
                               _p(residual) if residual is not None else None,
-                              residual.stride(0) if residual is not None else 0, _stream(w)), "lgemm")
+                              ld(residual, N) if residual is not None else 0, _stream(w)), "lgemm")
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out

@@ -1,6 +1,6 @@
 """csrc/lgemm.hip against torch (hipBLASLt F.linear / matmul, plus the torch GELU / cast / add launches the fused
 epilogues replace) at the detector head's GEMM shapes, fp16. Operands rotate over 4 copies; per shape the median of
-7 interleaved rounds of 50 calls. One JSON line per shape.
+7 rounds of a captured HIP graph of 50 calls (kernel time plus the in-graph launch gap). One JSON line per shape.
 
   python tools/bench_lgemm.py
 """
@@ -26,16 +26,29 @@ CASES = [("in_proj", 1608, 576, 144, "mm"), ("x_proj", 3216, 41, 288, "mm"), ("d
 
 
 def timeit(fns, rounds=7, reps=50):
-    out = {k: [] for k in fns}
-    for f in fns.values():
+    """per-call time of each variant from a captured HIP graph of `reps` calls (no host launch cost)"""
+    graphs = {}
+    for k, f in fns.items():
         f(0)
-    torch.cuda.synchronize()
-    for _ in range(rounds):
-        for k, f in fns.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i in range(2):
+                f(i)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
             for i in range(reps):
                 f(i)
+        graphs[k] = g
+    out = {k: [] for k in fns}
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k, g in graphs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
             e1.record()
             torch.cuda.synchronize()
             out[k].append(e0.elapsed_time(e1) / reps * 1e3)
