@@ -1261,19 +1261,14 @@ def _attn_split_workspace(dev, n_floats, n_counters):
     """fp32 partial dQ / d gate and the per-(b, h) tickets of the split attention backward, one per (device,
     stream): launches on one stream run one after another, launches in flight on two streams must not share them;
     the tickets are zeroed here once and left at zero by each launch. Captured launches take the device's graph
-    workspace, reserved before capture by reserve_graph_workspace (the captured graphs replay one after another)."""
+    workspace (reserve_graph_workspace sizes it before capture; a capture that needs more grows it in the capture)."""
     need = _ATTN_NEED.get(dev.index, (0, 0))
     _ATTN_NEED[dev.index] = (max(need[0], n_floats), max(need[1], n_counters))
     capturing = torch.cuda.is_current_stream_capturing()
     key = (dev.index, "graph") if capturing else (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     cur = _ATTN_WS.get(key)
     if cur is None or cur[0].numel() < n_floats or cur[1].numel() < n_counters:
-        if capturing:
-            raise RuntimeError("radhip attention: split-backward graph workspace not reserved before capture "
-                               "(ops.reserve_graph_workspace after an eager warm-up)")
-        cur = (torch.empty(max(n_floats, cur[0].numel() if cur else 0), dtype=torch.float32, device=dev),
-               torch.zeros(max(n_counters, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
-        _ATTN_WS[key] = cur
+        cur = _grow_workspace(_ATTN_WS, key, cur, n_floats, n_counters, torch.float32, dev)
     return cur
 
 
@@ -1574,24 +1569,33 @@ def _wgemm_workspace(dev, ws_bytes, n_counters):
     once here; the last arriver re-zeroes its ticket). Eager launches take one per (device, stream): launches on one
     stream run one after another, while two launches in flight at once on different streams (the SincNet side
     stream, SideLinear's) must not share slabs or tickets. Launches captured into HIP graphs take the device's graph
-    workspace, reserved before capture (reserve_graph_workspace) at the largest size the eager warm-up asked for:
-    the graphs' split-K GEMMs (the WavLM layers') are captured on one stream and replayed one graph after another."""
+    workspace, reserved before capture (reserve_graph_workspace) at the largest size the eager warm-up asked for, and
+    grown inside a capture that needs more: the graphs' split-K GEMMs (the WavLM layers') are captured on one stream
+    and replayed one graph after another."""
     need = _WG_NEED.get(dev.index, (0, 0))
     _WG_NEED[dev.index] = (max(need[0], ws_bytes), max(need[1], n_counters))
-    if torch.cuda.is_current_stream_capturing():
-        cur = _WG_WS.get((dev.index, "graph"))
-        if cur is None or cur[0].numel() < ws_bytes or cur[1].numel() < n_counters:
-            raise RuntimeError("radhip split-K GEMM: graph workspace not reserved before capture "
-                               "(ops.reserve_graph_workspace after an eager warm-up)")
-        return cur
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    capturing = torch.cuda.is_current_stream_capturing()
+    key = (dev.index, "graph") if capturing else (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     cur = _WG_WS.get(key)
     if cur is None or cur[0].numel() < ws_bytes or cur[1].numel() < n_counters:
-        nb = max(ws_bytes, cur[0].numel() if cur else 0)
-        nc = max(n_counters, cur[1].numel() if cur else 0)
-        cur = (torch.empty(nb, dtype=torch.uint8, device=dev), torch.zeros(nc, dtype=torch.int32, device=dev))
-        _WG_WS[key] = cur
+        cur = _grow_workspace(_WG_WS, key, cur, ws_bytes, n_counters, torch.uint8, dev)
     return cur
+
+
+_WS_KEEP = []   # every workspace pair ever handed out: captured graphs hold raw pointers into them
+
+
+def _grow_workspace(table, key, cur, n, n_counters, dtype, dev):
+    """A larger (slab, zeroed tickets) workspace for `key`. During a capture the allocation comes from the graph's
+    memory pool and the tickets' zero fill is a node of the graph (the tickets are zero whenever a replay reaches
+    it: each launch leaves them at zero); the pair it replaces stays referenced (_WS_KEEP), since graphs captured
+    earlier keep its addresses."""
+    n = max(n, cur[0].numel() if cur else 0)
+    nc = max(n_counters, cur[1].numel() if cur else 0)
+    new = (torch.empty(n, dtype=dtype, device=dev), torch.zeros(nc, dtype=torch.int32, device=dev))
+    _WS_KEEP.append(new)
+    table[key] = new
+    return new
 
 
 def reserve_graph_workspace(dev):
@@ -1605,8 +1609,7 @@ def reserve_graph_workspace(dev):
             continue
         cur = table.get(key)
         if cur is None or cur[0].numel() < nb or cur[1].numel() < nc:
-            table[key] = (torch.empty(max(nb, cur[0].numel() if cur else 0), dtype=dt, device=dev),
-                          torch.zeros(max(nc, cur[1].numel() if cur else 0), dtype=torch.int32, device=dev))
+            _grow_workspace(table, key, cur, nb, nc, dt, dev)
 
 
 def wgemm(a, b, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out=None, aux_out=None, tile=-1, name="wgemm",

@@ -24,6 +24,19 @@ class AdamW(torch.optim.AdamW):
         # (RADHIP_ADAMW=0) keeps the fused form, the one that takes GradScaler's grad_scale / found_inf
         super().__init__(params, fused=True, **kw)
 
+    def load_state_dict(self, state_dict):
+        """torch's load, then this optimizer's own form: the groups keep torch's fused flags (a state_dict of torch's
+        non-fused AdamW brings fused=False), and every step count becomes a device fp32 scalar of its own (torch's
+        load keeps a CPU step tensor as the very object of the source state_dict, shared with its optimizer)."""
+        super().load_state_dict(state_dict)
+        for group in self.param_groups:
+            group["fused"] = True
+            group["foreach"] = None
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and torch.is_tensor(st.get("step")) and p.is_cuda:
+                    st["step"] = st["step"].detach().to(device=p.device, dtype=torch.float32, copy=True)
+
     def _covered(self, group, ps):
         return (all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
                     and p.grad.is_contiguous() and not p.grad.is_sparse for p in ps)
