@@ -26,16 +26,22 @@ class AdamW(torch.optim.AdamW):
 
     def load_state_dict(self, state_dict):
         """torch's load, then this optimizer's own form: the groups keep torch's fused flags (a state_dict of torch's
-        non-fused AdamW brings fused=False), and every step count becomes a device fp32 scalar of its own (torch's
-        load keeps a CPU step tensor as the very object of the source state_dict, shared with its optimizer)."""
+        non-fused AdamW brings fused=False), every step count a device fp32 scalar, and every state tensor a copy of
+        its own (torch's load keeps a tensor already of the right device and dtype as the very object of the source
+        state_dict, so an optimizer loaded from another live one would share its moments and step counts)."""
         super().load_state_dict(state_dict)
         for group in self.param_groups:
             group["fused"] = True
             group["foreach"] = None
             for p in group["params"]:
                 st = self.state.get(p)
-                if st and torch.is_tensor(st.get("step")) and p.is_cuda:
-                    st["step"] = st["step"].detach().to(device=p.device, dtype=torch.float32, copy=True)
+                if not st:
+                    continue
+                for k, v in list(st.items()):
+                    if torch.is_tensor(v):
+                        st[k] = v.detach().clone()
+                if torch.is_tensor(st.get("step")) and p.is_cuda:
+                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
 
     def _covered(self, group, ps):
         return (all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
