@@ -511,7 +511,9 @@ int rdx_pgemm_prof(const void* A, int64_t lda, const void* B, int64_t ldb, void*
  * a ring of 8 KB slabs refilled one phase after they are read (counted vmcnt, never drained in the loop). tile codes
  * (csrc/hgemm.hip hg::geometry): 0 = 256 x 256, 1 = 256 x 192, 2 = 128 x 256, 3 = 128 x 192, 4 = 128 x 128,
  * 5 = 256 x 128; + 100: s_setprio(1) around every MFMA segment, + 200: static priority 1 for the second row group.
- * group_m: XCD-contiguous runs ordered group_m row tiles x every column tile (0 = column-panel order). splits > 1:
+ * group_m: XCD-contiguous runs ordered group_m row tiles x every column tile (0 = column-panel order); -R (R = 1, 2,
+ * 4, 8): the tiles cut into an R x 8/R grid of blocks, one per XCD (each XCD's L2 sees 1/R of A's rows and R/8 of
+ * B's panels). splits > 1:
  * split-K with an in-launch last-arriver sum in split order (deterministic); ws / counters as rdx_wgemm_bf16_ex
  * (rdx_hgemm_ws_bytes, rdx_hgemm_counters), one workspace per stream. */
 int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,

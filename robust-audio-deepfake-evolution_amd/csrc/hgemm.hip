@@ -149,6 +149,32 @@ __device__ __forceinline__ void tile_coords(const Args& g, int tile, int& mt, in
   }
 }
 
+// group_m < 0: the tiles as an R x (8 / R) grid of rectangular blocks (R = -group_m row groups, 8 / R column groups),
+// one per XCD, laid out block after block: each XCD's L2 takes only the A rows of its row group and the B panels of
+// its column group (over the chip A is fetched 8 / R times instead of 8 in column-panel order, B R times instead of
+// once). Position t of that order -> (tile row, tile column, split); the XCD
+// deal below hands each XCD a contiguous run of positions, so where the blocks' sizes differ by a few work ids the
+// excess lands on a neighbour's XCD (a locality loss, never a correctness one).
+__device__ __forceinline__ void grid_coords(const Args& g, int t, int spl, int& mt, int& nt, int& split) {
+  const int R = -g.group_m, C = 8 / R;
+  int pos = t;
+  mt = nt = split = 0;
+  for (int x = 0; x < 8; ++x) {
+    const int rg = x / C, cg = x - rg * C;
+    const int r0 = rg * g.tiles_m / R, r1 = (rg + 1) * g.tiles_m / R;
+    const int c0 = cg * g.tiles_n / C, c1 = (cg + 1) * g.tiles_n / C;
+    const int sz = (r1 - r0) * (c1 - c0) * spl;
+    if (pos < sz) {
+      const int tl = pos / spl, w = c1 - c0;
+      split = pos - tl * spl;
+      mt = r0 + tl / w;
+      nt = c0 + tl % w;
+      return;
+    }
+    pos -= sz;
+  }
+}
+
 // bijective deal of n work ids onto the 8 XCDs in contiguous runs (blocks b and b + 8 share an XCD)
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
   const int xcd = bid & 7, q = n >> 3, r = n & 7;
@@ -462,9 +488,14 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
   if constexpr (SK == 0) {
     const int SPL = g.splits;
     const int t = xcd_remap(blockIdx.x, tiles * SPL);
-    const int tile = t / SPL, split = t - tile * SPL;
+    int tile = t / SPL, split = t - tile * SPL;
     int mt, nt;
-    tile_coords(g, tile, mt, nt);
+    if (g.group_m < 0) {
+      grid_coords(g, t, SPL, mt, nt, split);
+      tile = nt * g.tiles_m + mt;     // the tile's id for its split-K slots and ticket (column-panel numbering)
+    } else {
+      tile_coords(g, tile, mt, nt);
+    }
     const int kb = split * nk_all / SPL, nk = (split + 1) * nk_all / SPL - kb;
     run_segment<BM, BN, NPA, NPB, U, EPI, PRIO, ABL>(g, lds, mt, nt, tile, kb, nk, split, SPL, SPL);
     return;
@@ -631,7 +662,7 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
   const bool probe = tile >= 1000;
   RDX_REQUIRE(probe ? (tile < 4000 && epilogue == RDX_EPI_BIAS && splits == 1)
                     : (tile >= 0 && tile < 300 && hg::geometry(tile, &bm, &bn)));
-  RDX_REQUIRE(group_m >= 0);
+  RDX_REQUIRE(group_m >= 0 || ((group_m == -1 || group_m == -2 || group_m == -4 || group_m == -8) && splits != 0));
   RDX_REQUIRE(splits >= 0 && splits <= 16 && splits <= K / 64);
   RDX_REQUIRE(splits >= 1 || !probe);
   if (splits != 1) {

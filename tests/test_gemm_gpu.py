@@ -264,11 +264,14 @@ HG_TILES = [0, 1, 2, 3, 4, 5, 100, 202]
 @pytest.mark.parametrize("M,N,K,splits,gm", [(1608, 1024, 1024, 1, 4), (333, 3072, 1024, 1, 0),
                                              (1608, 4096, 128, 1, 2), (64, 768, 4096, 1, 1),
                                              (6432, 1024, 192, 1, 8), (1608, 1024, 4096, 2, 0),
-                                             (200, 1000, 1024, 3, 0), (130, 260, 128, 2, 1)])
+                                             (200, 1000, 1024, 3, 0), (130, 260, 128, 2, 1),
+                                             (1608, 1024, 4096, 2, -2), (1608, 3072, 1024, 1, -4),
+                                             (6432, 4096, 256, 1, -2), (333, 260, 256, 3, -8), (130, 1000, 128, 1, -1)])
 def test_hgemm_bias_every_tile(tile, M, N, K, splits, gm):
     """Row tails (rows past M read as zeros through the buffer range), ragged column tiles (N % 8 == 4 takes the
     8-byte row phase), K of 2-3 steps (shorter than the ring: the refills past the last step take the zero-record
-    descriptor) up to deep K, split-K with the last-arriver sum, every group order."""
+    descriptor) up to deep K, split-K with the last-arriver sum, every group order (gm < 0: the R x 8/R XCD grid,
+    with empty and uneven blocks)."""
     from radhip.ops import hgemm
     a, b, bias = _ops(M, N, K, seed=tile + gm + splits)
     got = hgemm(a, b, bias, tile=tile, splits=splits, group_m=gm)
