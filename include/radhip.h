@@ -526,6 +526,12 @@ int64_t rdx_hgemm_counters(int M, int N, int tile);
  * arrive, its fp32 partials in K order (deterministic). ws_bytes >= rdx_hgemm_sk_ws_bytes(M, N, K, tile). */
 int64_t rdx_hgemm_sk_ws_bytes(int M, int N, int K, int tile);
 
+/* Column sums of fp32 row-partial buffers, up to 4 problems per launch: out_k[c] = sum_r in_k[r * ld_k + c] (rows
+ * in order, fixed-order combine: deterministic). Replaces the torch reductions of the scan / depthwise-conv backward
+ * partials (csrc/layersum.hip). */
+int rdx_colsum_many(int n, const float* const* in, const int* rows, const int* cols, const int64_t* ld,
+                    float* const* out, void* stream);
+
 /* ---- Small GEMMs of the detector head (csrc/lgemm.hip) -----------------------------------------------------------
  * C[M, N] = A[M, K] W[N, K]^T for the fusion / PN-BiMamba / pooling / classifier linears (replaces F.linear and the
  * input-gradient torch.matmul of src/models/DualStreamSEMamba.py:445-531,537-637,700-770 under the autocast of

@@ -227,3 +227,65 @@ extern "C" int rdx_cast_f32_many(int n, const float* const* src, void* const* ds
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
+
+// ---- Column sums of row-partial buffers: out[c] = sum_r in[r * ld + c] for up to CS_MAXP problems per launch (the
+// per-(direction, utterance, chunk) partial rows of the scan backward and of the depthwise conv backward: one launch
+// instead of a torch reduction each). A 256-thread block owns 32 columns x 8 row groups; a thread sums every 8th row
+// in row order, the 8 group sums are added in group order (fixed order: deterministic).
+namespace rdx {
+constexpr int CS_MAXP = 4;
+struct ColSumTable {
+  const float* in[CS_MAXP];
+  float* out[CS_MAXP];
+  int64_t ld[CS_MAXP];
+  int rows[CS_MAXP];
+  int cols[CS_MAXP];
+};
+__global__ __launch_bounds__(256) void colsum_many_kernel(ColSumTable t) {
+  __shared__ float red[8][33];
+  const int pb = blockIdx.y;
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5;
+  if (blockIdx.x * 32 >= t.cols[pb]) return;   // block-uniform
+  const float* in = t.in[pb];
+  const int rows = t.rows[pb];
+  const int64_t ld = t.ld[pb];
+  float s = 0.f;
+  if (c < t.cols[pb]) {
+    int r = g;
+    for (; r + 24 < rows; r += 32) {   // four rows of this group in flight per step, added in row order
+      const float a0 = in[(int64_t)r * ld + c], a1 = in[(int64_t)(r + 8) * ld + c];
+      const float a2 = in[(int64_t)(r + 16) * ld + c], a3 = in[(int64_t)(r + 24) * ld + c];
+      s = (((s + a0) + a1) + a2) + a3;
+    }
+    for (; r < rows; r += 8) s += in[(int64_t)r * ld + c];
+  }
+  red[g][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (g == 0 && c < t.cols[pb]) {
+    float tot = red[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) tot += red[k][threadIdx.x];
+    t.out[pb][c] = tot;
+  }
+}
+}  // namespace rdx
+
+extern "C" int rdx_colsum_many(int n, const float* const* in, const int* rows, const int* cols, const int64_t* ld,
+                               float* const* out, void* stream) {
+  RDX_REQUIRE(n > 0 && n <= rdx::CS_MAXP && in && rows && cols && ld && out);
+  rdx::ColSumTable t{};
+  int maxc = 0;
+  for (int k = 0; k < n; ++k) {
+    RDX_REQUIRE(in[k] && out[k] && rows[k] > 0 && cols[k] > 0 && ld[k] >= cols[k]);
+    t.in[k] = in[k];
+    t.out[k] = out[k];
+    t.ld[k] = ld[k];
+    t.rows[k] = rows[k];
+    t.cols[k] = cols[k];
+    maxc = cols[k] > maxc ? cols[k] : maxc;
+  }
+  hipLaunchKernelGGL(rdx::colsum_many_kernel, dim3((unsigned)((maxc + 31) / 32), (unsigned)n), dim3(256), 0,
+                     as_stream(stream), t);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}

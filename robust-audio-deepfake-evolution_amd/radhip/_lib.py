@@ -133,6 +133,7 @@ SIGNATURES = {
     "rdx_hgemm": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_i64, c_vp,
                           c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "rdx_hgemm_ws_bytes": (c_i64, [c_int, c_int, c_int, c_int]),
+    "rdx_colsum_many": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rdx_lgemm": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp, c_i64, c_int, c_int, c_int, c_int, c_vp, c_int,
                           c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "rdx_hgemm_counters": (c_i64, [c_int, c_int, c_int]),

@@ -185,7 +185,6 @@ class MambaBiFn(torch.autograd.Function):
                                    ops._p(dy), 0, ops._p(du), ops._p(ddelta), ops._p(dBC), ctypes.c_void_p(base),
                                    ctypes.c_void_p(base + 4 * Di * N), ctypes.c_void_p(base + 4 * (Di * N + Di)),
                                    Di * N + 2 * Di, ops._p(gloc), B, L, Di, N, 2, st), "scan2_bwd")
-        tot = part.sum(0)
         dxdbl = torch.empty(2 * M, ldbc, device=dev, dtype=dt)
         dxdbl[:, R:].copy_(dBC)
         ops.lgemm(ddelta, _cast_t(w_dt, wdt), out=dxdbl[:, :R])       # d dt
@@ -197,7 +196,9 @@ class MambaBiFn(torch.autograd.Function):
         check(Lb.rdx_dwconv_bidir_bwd(code, ops._p(xz), 2 * Di, ops._p(cw), ops._p(cb), ops._p(du), ops._p(dxz),
                                       2 * Di, ops._p(partc), ctypes.c_void_p(partc.data_ptr() + 4 * Di * K),
                                       Di * K + Di, B, L, Di, K, 2, st), "dwconv_bidir_bwd")
-        totc = partc.sum(0)
+        tot = torch.empty(part.shape[1], device=dev, dtype=torch.float32)
+        totc = torch.empty(partc.shape[1], device=dev, dtype=torch.float32)
+        ops.colsum_many([(part, tot), (partc, totc)])     # the scan's and the conv's parameter-gradient partials
         gw_in, _ = _weight_grads(dxz, n2, w_in, None, need[1], False)
         dx = None
         if need[0]:

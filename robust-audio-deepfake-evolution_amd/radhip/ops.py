@@ -1821,3 +1821,21 @@ def lgemm(a, w, bias=None, epilogue=_lib.EPI_BIAS, aux=None, out_dtype=None, res
                               _p(residual) if residual is not None else None,
                               ld(residual, N) if residual is not None else 0, _stream(w)), "lgemm")
     return (out, aux_out) if epilogue == _lib.EPI_BIAS_GELU else out
+
+
+def colsum_many(pairs):
+    """out[c] = sum over rows of part[r, c] for each (part [rows, cols] fp32, unit inner stride, out fp32 [cols]) in
+    `pairs` (up to 4): one csrc/layersum.hip launch, rows in order (deterministic)."""
+    n = len(pairs)
+    if not 0 < n <= 4:
+        raise ValueError("radhip colsum_many: 1-4 problems")
+    for part, out in pairs:
+        _require_gpu(part, out)
+        if (part.dtype != torch.float32 or out.dtype != torch.float32 or part.dim() != 2 or part.stride(1) != 1
+                or out.shape != (part.shape[1],) or not out.is_contiguous()):
+            raise ValueError("radhip colsum_many: fp32 [rows, cols] parts and [cols] outputs")
+    ints = lambda v: (ctypes.c_int * n)(*v)
+    check(lib().rdx_colsum_many(n, ptr_array([p.data_ptr() for p, _ in pairs]), ints([p.shape[0] for p, _ in pairs]),
+                                ints([p.shape[1] for p, _ in pairs]),
+                                (ctypes.c_int64 * n)(*[p.stride(0) for p, _ in pairs]),
+                                ptr_array([o.data_ptr() for _, o in pairs]), _stream(pairs[0][0])), "colsum_many")

@@ -44,3 +44,20 @@ def test_mamba_fused_bitwise_equals_module_path(B, L, dt, monkeypatch):
     for k in g0:
         assert _rel(g1[k], g0[k]) < tol, k
     assert all(torch.isfinite(v).all() for v in g1.values())
+
+
+def test_colsum_many_matches_torch_sum():
+    """ops.colsum_many (csrc/layersum.hip): the fused node's partial-row reductions, against torch's sum in fp64,
+    ragged row / column counts, a strided part, two launches bitwise equal (fixed order)."""
+    from radhip.ops import colsum_many
+    g = torch.Generator(device="cpu").manual_seed(7)
+    parts = [torch.randn(208, 5184, generator=g).to(DEV), torch.randn(56, 1440, generator=g).to(DEV),
+             torch.randn(7, 33, generator=g).to(DEV), torch.randn(301, 100, generator=g).to(DEV)[:, 3:70]]
+    outs = [torch.empty(p.shape[1], device=DEV) for p in parts]
+    colsum_many(list(zip(parts, outs)))
+    for p, o in zip(parts, outs):
+        ref = p.double().sum(0)
+        assert float((o.double() - ref).abs().max()) <= 1e-5 * float(p.abs().sum(0).max())
+    again = [torch.empty_like(o) for o in outs]
+    colsum_many(list(zip(parts, again)))
+    assert all(torch.equal(a, b) for a, b in zip(outs, again))
