@@ -929,8 +929,20 @@ def _conv2_grad_to_c(da, out1, c, wd2, w2_shape, bn5, f32):
 
 
 def _bn_rows(conv_bias, mean, invstd, gamma, beta):
-    f32 = [t.detach().contiguous().float() for t in (conv_bias, mean, invstd, gamma, beta)]
+    """The frozen-BN record rows [conv bias | mean | invstd * gamma | beta | invstd] of a block; within an
+    accumulation window (ops.SCONV_WCACHE set) made once and shared by the window's passes (the parameters and
+    running statistics do not change inside a window)."""
+    src = (conv_bias, mean, invstd, gamma, beta)
+    cache = SCONV_WCACHE
+    key = ("bn5",) + tuple(id(t) for t in src)
+    if cache is not None:
+        hit = cache.get(key)
+        if hit is not None and all(a is b for a, b in zip(hit[0], src)):
+            return hit[1], hit[2]
+    f32 = [t.detach().contiguous().float() for t in src]
     bn5 = torch.stack([f32[0], f32[1], f32[2] * f32[3], f32[4], f32[2]]).contiguous()
+    if cache is not None:
+        cache[key] = (src, f32, bn5)
     return f32, bn5
 
 

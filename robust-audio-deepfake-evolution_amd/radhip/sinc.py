@@ -129,7 +129,7 @@ class Residual_block(nn.Module):
             # 32/64-channel convolutions run on csrc/sconv.hip (conv1 with the BN+SELU in its epilogue).
             bn = self.bn2
             bf = _half_autocast(x)
-            invstd = torch.rsqrt(bn.running_var + bn.eps)
+            invstd = _frozen_invstd(bn)
             bnp = (self.conv1.bias, bn.running_mean, invstd, bn.weight, bn.bias)
             w2 = self.conv2.weight
             # conv1 -> bn2 -> selu -> conv2 as one autograd op on csrc/sconv.hip (its backward reaches conv1's
@@ -185,6 +185,21 @@ class Residual_block(nn.Module):
         out = self.conv2(out)
         identity = self.conv_downsample(x) if self.downsample else x
         return self.mp(out + identity)
+
+
+def _frozen_invstd(bn):
+    """rsqrt(running_var + eps) of a frozen BatchNorm, once per accumulation window (ops.SCONV_WCACHE)."""
+    from . import ops as _ops
+    cache = _ops.SCONV_WCACHE
+    if cache is None:
+        return torch.rsqrt(bn.running_var + bn.eps)
+    key = ("invstd", id(bn.running_var))
+    hit = cache.get(key)
+    if hit is not None and hit[0] is bn.running_var:
+        return hit[1]
+    v = torch.rsqrt(bn.running_var + bn.eps)
+    cache[key] = (bn.running_var, v)
+    return v
 
 
 class SincNetEncoder(nn.Module):
