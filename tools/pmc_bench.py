@@ -24,7 +24,7 @@ OPS = {
     "sconv_wgrad": r"sconv_wgrad_kernel<", "attn_fwd": r"attn_fwd_kernel<", "attn_bwd": r"attn_bwd_fused_kernel<",
     "selective_scan_fwd": r"scan_fwd_seg_kernel<|s2::fwd_chunk_kernel<|s2::carry_kernel<0>|s2::fwd_out_kernel<",
     "selective_scan_bwd": r"[^_]scan_bwd_kernel<|s2::bwd_chunk_kernel<|s2::carry_kernel<1>|s2::bwd_out_kernel<",
-    "pgemm": r"pgemm_kernel<", "hgemm": r"hgemm_kernel<", "sincconv_mfma": r"sincconv_mfma_kernel",
+    "pgemm": r"pgemm_kernel<", "hgemm": r"hgemm_kernel<", "lgemm": r"lgemm_kernel<", "sincconv_mfma": r"sincconv_mfma_kernel",
     "wgrad_acc": r"wgrad_part_kernel|wgrad_reduce_kernel", "wgrad_many": r"wgrad_part_many_kernel|wgrad_reduce_many_kernel", "posconv_fwd": r"posconv2?_kernel<false>",
     "posconv_bwd": r"posconv2?_kernel<true>", "fe_conv0": r"fe_conv0_kernel", "fe_ln_gelu": r"fe_ln_gelu_kernel", "sincconv_absmaxpool": r"sincconv_absmaxpool_kernel",
     "fe_conv_gemm": r"gemm_nt_kernel|strided_gemm", "layer_wsum_fwd": r"lws_fwd_kernel", "layer_wsum_bwd": r"lws_bwd_kernel",
