@@ -1436,8 +1436,9 @@ WGEMM_POLICY_R4 = {
 }
 # tile orders (group_m) chosen by L2 fill traffic: rocprofv3 FETCH_SIZE per launch under column-panel order (0),
 # 4-row-tile groups (4) and the XCD grid (-R), profiles/r05_pmc_hgemm_order.jsonl (e.g. B = 32 FFN1 9.2x the A + B
-# bytes in column order, 4.0x at -2; B = 8 FFN2 5.9x -> 4.2x at 4); in-step A/B 469.7 vs 461.0 utt/s
-# (profiles/r05_ab/fo_*.json)
+# bytes in column order, 4.7x at 4; B = 8 FFN2 5.9x -> 4.2x at 4) and by time (standalone sweep of the orders,
+# profiles/r05_hgemm_orders.jsonl: 4 fastest for every shape but the B = 8 FFN1 pair, 0); in-step A/B of the first
+# such table 469.7 vs 461.0 utt/s (profiles/r05_ab/fo_*.json)
 WGEMM_POLICY_R5A = {
     "b8": {"qkv": ("hg", 3, 1, 0), "out": ("hg", 4, 1, 0), "d_out": ("hg", 4, 1, 0), "ffn1": ("hg", 202, 1, 0),
            "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 4, 2, 0), "d_ffn1": ("hg", 4, 2, 0), "d_qkv": ("hg", 4, 2, 0)},
@@ -1445,10 +1446,10 @@ WGEMM_POLICY_R5A = {
             "d_ffn2": ("hg", 0, 1, 0), "ffn2": ("hg", 2, 1, 0), "d_ffn1": ("hg", 2, 1, 0), "d_qkv": ("hg", 2, 1, 0)},
 }
 WGEMM_POLICY = {
-    "b8": {"qkv": ("hg", 3, 1, 0), "out": ("hg", 4, 1, 4), "d_out": ("hg", 4, 1, 4), "ffn1": ("hg", 202, 1, 0),
+    "b8": {"qkv": ("hg", 3, 1, 4), "out": ("hg", 4, 1, 4), "d_out": ("hg", 4, 1, 4), "ffn1": ("hg", 202, 1, 0),
            "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 4, 2, 4), "d_ffn1": ("hg", 4, 2, 4), "d_qkv": ("hg", 4, 2, 4)},
-    "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, -2),
-            "d_ffn2": ("hg", 0, 1, -2), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
+    "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
+            "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
 }
 
 
