@@ -164,6 +164,10 @@ int rdx_layer_wsum_bwd(int dtype, int nl, const void* const* hs, const float* w,
  * i < numel[k] (round to nearest even). The accumulation window casts the detector head's fp32 linear weights to the
  * autocast dtype once per window with it (radhip/window.py; autocast's own cast cache: one launch per tensor). */
 int rdx_cast_f32_many(int n, const float* const* src, void* const* dst, const int64_t* numel, void* stream);
+/* dst[k][i] += src[k][i] (copy = 0) or dst[k][i] = src[k][i] (copy = 1), i < numel[k], over n <= 64 fp32 tensors in
+ * one launch (4096 elements per workgroup). Replaces torch._foreach_add_ / _foreach_copy_ in the window's gradient
+ * hand-over (radhip/window.py; the reference accumulates each .grad by autograd, src/main.py:1077-1108). */
+int rdx_add_f32_many(int n, void* const* dst, const float* const* src, const int64_t* numel, int copy, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * RawBoost, batched over utterances with host-drawn parameters. Replaces RawBoost.process and

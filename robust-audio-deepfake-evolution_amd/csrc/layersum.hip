@@ -228,6 +228,69 @@ extern "C" int rdx_cast_f32_many(int n, const float* const* src, void* const* ds
   return RDX_OK;
 }
 
+// ---- dst[k] += src[k] (or dst[k] = src[k]) over up to RDX_ADDM_MAX fp32 tensors in one launch: the window's per-pass
+// hand-over of autograd's parameter gradients into the flat gradient buffer and the feature_projection copies
+// (radhip/window.py). torch's multi-tensor add gives each workgroup a 64 K-element chunk, so a pass's few hundred
+// thousand elements run on a dozen workgroups at ~0.15 TB/s; here a workgroup owns 4096 elements (16 per lane, every
+// load of the lane issued before its stores) and the tensors' chunks are laid end to end over the grid.
+constexpr int RDX_ADDM_MAX = 64;
+constexpr int RDX_ADDM_CHUNK = 4096;
+struct AddManyTable {
+  float* dst[RDX_ADDM_MAX];
+  const float* src[RDX_ADDM_MAX];
+  int64_t n[RDX_ADDM_MAX];
+  int start[RDX_ADDM_MAX + 1];  // first workgroup of each tensor; start[nt] = the grid size
+};
+
+template <bool kCopy>
+__global__ __launch_bounds__(256) void add_many_kernel(AddManyTable t, int nt) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < nt && t.start[k + 1] <= b) ++k;   // workgroup-uniform
+  const int64_t base = (int64_t)(b - t.start[k]) * RDX_ADDM_CHUNK + threadIdx.x;
+  const int64_t n = t.n[k];
+  float* __restrict__ d = t.dst[k];
+  const float* __restrict__ s = t.src[k];
+  constexpr int kPer = RDX_ADDM_CHUNK / 256;
+  float a[kPer], c[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = base + j * 256;
+    a[j] = i < n ? s[i] : 0.f;
+    if (!kCopy) c[j] = i < n ? d[i] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = base + j * 256;
+    if (i < n) d[i] = kCopy ? a[j] : c[j] + a[j];
+  }
+}
+
+extern "C" int rdx_add_f32_many(int n, void* const* dst, const float* const* src, const int64_t* numel, int copy,
+                                void* stream) {
+  RDX_REQUIRE(n >= 0 && (n == 0 || (src && dst && numel)) && (copy == 0 || copy == 1));
+  if (n > RDX_ADDM_MAX) return RDX_EUNSUPPORTED;
+  AddManyTable t{};
+  int64_t blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    RDX_REQUIRE(numel[k] >= 0 && (numel[k] == 0 || (src[k] && dst[k])));
+    t.dst[k] = reinterpret_cast<float*>(dst[k]);
+    t.src[k] = src[k];
+    t.n[k] = numel[k];
+    t.start[k] = (int)blocks;
+    blocks += (numel[k] + RDX_ADDM_CHUNK - 1) / RDX_ADDM_CHUNK;
+    if (blocks > (int64_t)INT32_MAX) return RDX_EUNSUPPORTED;
+  }
+  t.start[n] = (int)blocks;
+  if (blocks == 0) return RDX_OK;
+  if (copy)
+    hipLaunchKernelGGL(add_many_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), t, n);
+  else
+    hipLaunchKernelGGL(add_many_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), t, n);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
 // ---- Column sums of row-partial buffers: out[c] = sum_r in[r * ld + c] for up to CS_MAXP problems per launch (the
 // per-(direction, utterance, chunk) partial rows of the scan backward and of the depthwise conv backward: one launch
 // instead of a torch reduction each). A 256-thread block owns 32 columns x 8 row groups; a thread sums every 8th row

@@ -80,6 +80,8 @@ SIGNATURES = {
     "rdx_layer_wsum_fwd": (c_int, [c_int, c_int, ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_vp]),
     "rdx_layer_wsum_nblk": (c_int, [c_i64]),
     "rdx_cast_f32_many": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
+    "rdx_add_f32_many": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_int,
+                                 c_vp]),
     "rdx_layer_wsum_bwd": (c_int, [c_int, c_int, ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.POINTER(c_vp), c_vp,
                                    c_i64, c_vp]),
     "rdx_rawboost_workspace_bytes": (c_i64, [c_int, c_i64]),

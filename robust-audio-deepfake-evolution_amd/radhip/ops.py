@@ -575,6 +575,25 @@ def cast_many(srcs, dsts):
               "cast_f32_many")
 
 
+def add_many(dsts, srcs, copy=False):
+    """dsts[k] += srcs[k] (copy: dsts[k] = srcs[k]) for contiguous fp32 tensors, one launch per 64 pairs
+    (csrc/layersum.hip rdx_add_f32_many; the same fp32 adds as torch._foreach_add_)."""
+    if len(dsts) != len(srcs):
+        raise ValueError("radhip add_many: one source per destination")
+    if not dsts:
+        return
+    _require_gpu(*dsts)
+    for d, s in zip(dsts, srcs):
+        if (d.dtype != torch.float32 or s.dtype != torch.float32 or d.numel() != s.numel() or not d.is_contiguous()
+                or not s.is_contiguous() or d.device != s.device):
+            raise ValueError("radhip add_many: contiguous fp32 tensors of equal size on one device")
+    for i in range(0, len(dsts), 64):
+        d, s = dsts[i:i + 64], srcs[i:i + 64]
+        check(lib().rdx_add_f32_many(len(d), ptr_array([t.data_ptr() for t in d]), ptr_array([t.data_ptr() for t in s]),
+                                     (ctypes.c_int64 * len(d))(*[t.numel() for t in d]), int(bool(copy)),
+                                     _stream(d[0])), "add_f32_many")
+
+
 # ------------------------------------------------------------------------------------ FGM ----
 def fgm_attack(params, grads, backups, eps):
     """backup <- p; p += eps * g / ||g|| per tensor (skip when the norm is 0 or NaN). fp32 tensors."""

@@ -29,6 +29,19 @@ from .train import MAX_LEN, _PinnedRing, check_graph_memset_replay, layerdrop_dr
 from .wavlm import compute_time_mask
 
 
+def _add_many(dsts, srcs, copy=False):
+    """dsts[k] += srcs[k] (copy: =) in one HIP launch per 64 tensors on the GPU (ops.add_many); torch's multi-tensor
+    ops for the CPU runs of the window (the gloo tests of the host logic)."""
+    if not dsts:
+        return
+    if dsts[0].is_cuda:
+        ops.add_many(dsts, srcs, copy=copy)
+    elif copy:
+        torch._foreach_copy_(dsts, srcs)
+    else:
+        torch._foreach_add_(dsts, srcs)
+
+
 def window_eligible(trainer):
     """True when batching the window's clean passes is exact: no BatchNorm computes batch statistics
     (freeze_bn, or a model without BatchNorm)."""
@@ -217,7 +230,7 @@ class WindowStep:
         finally:
             got = [(v, p.grad) for p, v in zip(self.handed, views) if p.grad is not None]
             if got:
-                torch._foreach_add_([v for v, _ in got], [g for _, g in got])
+                _add_many([v for v, _ in got], [g for _, g in got])
             for p, v in zip(self.handed, views):
                 p.grad = v
 
@@ -278,7 +291,7 @@ class WindowStep:
         if self.sinc_batched:
             self._sinc_adv_forward()
         with torch.no_grad():
-            torch._foreach_copy_(self._flat_copies, self._flat_real)
+            _add_many(self._flat_copies, self._flat_real, copy=True)
             self.fp_grad.zero_()
         core.fp_groups = self.fp_copies
         core.cnn_reuse = "store"
@@ -341,7 +354,7 @@ class WindowStep:
         is frozen (no .grad) and the copies' gradients are never used."""
         if not self.adv:
             return
-        torch._foreach_add_([p.grad for p in self.fp_real], list(self.fp_copies[k][i].grad for i in range(4)))
+        _add_many([p.grad for p in self.fp_real], [self.fp_copies[k][i].grad for i in range(4)])
 
     def _adv_step(self, k):
         """Micro-batch k's FGM chain link: its clean gradient into feature_projection.grad, the attack on the
