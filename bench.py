@@ -480,8 +480,19 @@ def main():
         from torch.profiler import ProfilerActivity, profile
         prof = profile(activities=[ProfilerActivity.CPU], record_shapes=True)
         prof.__enter__()
+    cprof = None
+    if os.environ.get("RADHIP_CPROFILE"):          # tools: where the host spends a step (python-level)
+        import cProfile
+        cprof = cProfile.Profile()
+        cprof.enable()
     for _ in range(args.steps):
         step()
+    if cprof is not None:
+        cprof.disable()
+        import pstats
+        with open(os.environ["RADHIP_CPROFILE"], "w") as f:
+            pstats.Stats(cprof, stream=f).sort_stats("tottime").print_stats(60)
+            pstats.Stats(cprof, stream=f).sort_stats("cumulative").print_stats(60)
     if prof is not None:
         prof.__exit__(None, None, None)
         with open(os.environ["RADHIP_TORCH_PROFILE"], "w") as f:
@@ -490,6 +501,7 @@ def main():
                                                                          max_name_column_width=40,
                                                                          max_shapes_column_width=120))
     ev1.record(stream)
+    host_submit = time.perf_counter() - t0      # the host has issued every step (diagnostic: host- vs GPU-bound)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -548,6 +560,8 @@ def main():
             # the dominant kernel per (kernel, shape): every shape sampled in every graph (GraphTimer keys)
             "kernel_shapes": shape_table(shape_rows, roof["kernel"] if roof else None, args.steps),
             "final_loss": round(loss, 6),
+            # host time to issue the K steps (no sync inside): close to ms_per_step means the GPU waited on the host
+            "host_submit_ms_per_step": round(1000 * host_submit / args.steps, 3),
         }
         if ws == 1 and not args.no_cpu_baseline:
             hb.set("cpu baseline")
