@@ -30,6 +30,7 @@ class AdamW(torch.optim.AdamW):
         its own (torch's load keeps a tensor already of the right device and dtype as the very object of the source
         state_dict, so an optimizer loaded from another live one would share its moments and step counts)."""
         super().load_state_dict(state_dict)
+        self._tables = {}
         for group in self.param_groups:
             group["fused"] = True
             group["foreach"] = None
@@ -49,6 +50,45 @@ class AdamW(torch.optim.AdamW):
                 and not group["amsgrad"] and not group["maximize"] and not group.get("differentiable", False)
                 and not torch.is_tensor(group["lr"]))
 
+    def _launch_table(self, gi, group, ps):
+        """Per group: the step counters as views of one flat fp32 device tensor (the increment and GradScaler's
+        rollback are one launch each, where torch's per-tensor _foreach_add_ / _foreach_sub_ over a few hundred
+        scalars cost ~0.6 ms of host time apiece) and the kernel's pointer arrays, rebuilt only when the group's
+        parameters, gradients or state tensors change (a loaded state_dict, a .grad re-bound)."""
+        # the table keeps every keyed object alive (ids cannot be reused while it holds them)
+        key = tuple((id(p), id(p.grad), p.data_ptr(), p.grad.data_ptr()) for p in ps)
+        tab = self._tables.get(gi)
+        if tab is not None and tab["key"] == key and all(
+                self.state[p].get("step") is s for p, s in zip(ps, tab["ss"])):
+            return tab
+        ms, vs, ss = [], [], []
+        for p in ps:
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            ms.append(st["exp_avg"])
+            vs.append(st["exp_avg_sq"])
+            # a loaded state_dict may hold the step as a CPU scalar (torch's non-fused AdamW, or
+            # map_location="cpu"); the kernel reads it on the device, as torch's fused step does
+            ss.append(st["step"].to(device=p.device, dtype=torch.float32).reshape(()))
+        flat = torch.stack(ss)
+        for i, p in enumerate(ps):
+            self.state[p]["step"] = flat[i]
+        ss = [self.state[p]["step"] for p in ps]
+        mx = int(lib().rdx_adamw_many_max())
+        chunks = []
+        for i in range(0, len(ps), mx):
+            sl = slice(i, i + mx)
+            n = len(ps[sl])
+            chunks.append((n, ptr_array([p.data_ptr() for p in ps[sl]]), ptr_array([p.grad.data_ptr() for p in ps[sl]]),
+                           ptr_array([t.data_ptr() for t in ms[sl]]), ptr_array([t.data_ptr() for t in vs[sl]]),
+                           ptr_array([t.data_ptr() for t in ss[sl]]), (ctypes.c_int64 * n)(*[p.numel() for p in ps[sl]])))
+        tab = {"key": key, "ss": ss, "flat": flat, "chunks": chunks, "keep": (ps, [p.grad for p in ps], ms, vs)}
+        self._tables[gi] = tab
+        return tab
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -57,47 +97,27 @@ class AdamW(torch.optim.AdamW):
                 loss = closure()
         grad_scale = getattr(self, "grad_scale", None)
         found_inf = getattr(self, "found_inf", None)
-        for group in self.param_groups:
+        if not hasattr(self, "_tables"):
+            self._tables = {}
+        for gi, group in enumerate(self.param_groups):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
             if not self._covered(group, ps):
                 self._torch_step(group, ps, grad_scale, found_inf)
                 continue
-            ms, vs, ss = [], [], []
-            for p in ps:
-                st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                elif not (st["step"].is_cuda and st["step"].device == p.device
-                          and st["step"].dtype == torch.float32):
-                    # a loaded state_dict may hold the step as a CPU scalar (torch's non-fused AdamW, or
-                    # map_location="cpu"); the kernel reads it on the device, as torch's fused step does
-                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
-                ms.append(st["exp_avg"])
-                vs.append(st["exp_avg_sq"])
-                ss.append(st["step"])
-            torch._foreach_add_(ss, 1)
+            tab = self._launch_table(gi, group, ps)
+            tab["flat"].add_(1)
             b1, b2 = group["betas"]
             stream = torch.cuda.current_stream(ps[0].device).cuda_stream
             gsp = grad_scale.data_ptr() if grad_scale is not None else None
             fip = found_inf.data_ptr() if found_inf is not None else None
-            mx = int(lib().rdx_adamw_many_max())
-            for i in range(0, len(ps), mx):
-                sl = slice(i, i + mx)
-                n = len(ps[sl])
-                check(lib().rdx_adamw_many(n, ptr_array([p.data_ptr() for p in ps[sl]]),
-                                           ptr_array([p.grad.data_ptr() for p in ps[sl]]),
-                                           ptr_array([t.data_ptr() for t in ms[sl]]),
-                                           ptr_array([t.data_ptr() for t in vs[sl]]),
-                                           ptr_array([t.data_ptr() for t in ss[sl]]),
-                                           (ctypes.c_int64 * n)(*[p.numel() for p in ps[sl]]),
-                                           float(group["lr"]), float(b1), float(b2), float(group["weight_decay"]),
-                                           float(group["eps"]), gsp, fip, stream), "adamw_many")
+            for n, pp, gp, mp, vp, sp, numel in tab["chunks"]:
+                check(lib().rdx_adamw_many(n, pp, gp, mp, vp, sp, numel, float(group["lr"]), float(b1), float(b2),
+                                           float(group["weight_decay"]), float(group["eps"]), gsp, fip, stream),
+                      "adamw_many")
             if found_inf is not None:
-                torch._foreach_sub_(ss, [found_inf] * len(ss))
+                tab["flat"].sub_(found_inf)
         return loss
 
     def _torch_step(self, group, ps, grad_scale, found_inf):

@@ -140,12 +140,15 @@ class EMA:
 
     def refresh_names(self):
         self.names = [n for n, p in self.model.named_parameters() if p.requires_grad]
+        self._cur_params = None
         self.shadow = None if self.n_averaged == 0 else self.shadow
 
     @torch.no_grad()
     def update(self):
-        params = dict(self.model.named_parameters())
-        cur = [params[n].detach() for n in self.names]
+        cur = getattr(self, "_cur_params", None)
+        if cur is None:    # the name walk (~9000 modules) once; parameters are updated in place, refresh_names rebinds
+            named = dict(self.model.named_parameters())
+            cur = self._cur_params = [named[n].detach() for n in self.names]
         if self.shadow is None or self.n_averaged == 0:
             self.shadow = [c.clone() for c in cur]
         else:
@@ -480,12 +483,19 @@ class Trainer:
         return 1.0, None
 
     def train_mode(self):
-        """model.train() + freeze_batch_norm_stats (main.py:44-51,1016-1018)."""
+        """model.train() + freeze_batch_norm_stats (main.py:44-51,1016-1018). Walking the model's ~9000 modules
+        costs ~6 ms of host time, once per window in front of its graph replays; when the model is still as the
+        last call left it (top module training, every frozen BatchNorm in eval: any model.train() / eval() since
+        flips those) the walk is skipped."""
+        sent = getattr(self, "_mode_sentinel", None)
+        if sent is not None and self.model.training and not any(m.training for m in sent):
+            return
         self.model.train()
         if self.freeze_bn:
             for m in self.model.modules():
                 if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
                     m.eval()
+        self._mode_sentinel = [m for m in self.model.modules() if not m.training]
 
     def cnn_reuse(self, mode, drop=False):
         """FGM's adversarial pass reuses the frozen WavLM CNN features of the clean pass (identical input,
