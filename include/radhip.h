@@ -514,7 +514,7 @@ int rdx_pgemm_prof(const void* A, int64_t lda, const void* B, int64_t ldb, void*
  * groups one barrier apart so each SIMD pairs one wave's MFMA segment with its partner's LDS reads and LDS-DMA issue,
  * a ring of 8 KB slabs refilled one phase after they are read (counted vmcnt, never drained in the loop). tile codes
  * (csrc/hgemm.hip hg::geometry): 0 = 256 x 256, 1 = 256 x 192, 2 = 128 x 256, 3 = 128 x 192, 4 = 128 x 128,
- * 5 = 256 x 128; + 100: s_setprio(1) around every MFMA segment, + 200: static priority 1 for the second row group.
+ * 5 = 256 x 128, 6 = 64 x 128, 7 = 64 x 256; + 100: s_setprio(1) around every MFMA segment, + 200: static priority 1 for the second row group.
  * group_m: XCD-contiguous runs ordered group_m row tiles x every column tile (0 = column-panel order); -R (R = 1, 2,
  * 4, 8): the tiles cut into an R x 8/R grid of blocks, one per XCD (each XCD's L2 sees 1/R of A's rows and R/8 of
  * B's panels). splits > 1:

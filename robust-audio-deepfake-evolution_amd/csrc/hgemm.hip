@@ -559,6 +559,8 @@ static int dispatch(const Args& g, int tile, hipStream_t st) {
     case 3: return launch<128, 192, 2, 1, 3, EPI, PRIO>(g, st);   // 15 slabs
     case 4: return launch<128, 128, 1, 1, 4, EPI, PRIO>(g, st);   // 16 slabs
     case 5: return launch<256, 128, 2, 1, 3, EPI, PRIO>(g, st);   // 18 slabs
+    case 6: return launch<64, 128, 1, 1, 4, EPI, PRIO>(g, st);    // 12 slabs: twice the tiles of 128 x 128
+    case 7: return launch<64, 256, 1, 1, 3, EPI, PRIO>(g, st);    // 15 slabs
     default: return RDX_EINVAL;
   }
 }
@@ -588,6 +590,8 @@ static bool geometry(int tile, int* bm, int* bn) {
     case 3: *bm = 128; *bn = 192; return true;
     case 4: *bm = 128; *bn = 128; return true;
     case 5: *bm = 256; *bn = 128; return true;
+    case 6: *bm = 64; *bn = 128; return true;
+    case 7: *bm = 64; *bn = 256; return true;
     default: return false;
   }
 }

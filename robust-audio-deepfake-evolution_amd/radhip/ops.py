@@ -1464,9 +1464,18 @@ WGEMM_POLICY_R5A = {
     "b32": {"qkv": ("hg", 1, 1, 0), "out": ("hg", 2, 1, 0), "d_out": ("hg", 2, 1, 0), "ffn1": ("hg", 0, 1, 0),
             "d_ffn2": ("hg", 0, 1, 0), "ffn2": ("hg", 2, 1, 0), "d_ffn1": ("hg", 2, 1, 0), "d_qkv": ("hg", 2, 1, 0)},
 }
-WGEMM_POLICY = {
+WGEMM_POLICY_R5G = {
     "b8": {"qkv": ("hg", 3, 1, 4), "out": ("hg", 4, 1, 4), "d_out": ("hg", 4, 1, 4), "ffn1": ("hg", 202, 1, 0),
            "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 4, 2, 4), "d_ffn1": ("hg", 4, 2, 4), "d_qkv": ("hg", 4, 2, 4)},
+    "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
+            "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
+}
+# 64 x 128 tiles (code 6) for the B = 8 N = 1024 shapes: 208 tiles on 256 CUs instead of 104, no split-K
+# (tools/bench_hgemm.py, profiles/r05_hgemm_tile64.jsonl, us: out / d_out 11.1 -> 9.2, FFN2 24.0 -> 22.7,
+# FFN1's input gradient 24.1 -> 22.4, q/k/v's input gradient 20.8 -> 18.4)
+WGEMM_POLICY = {
+    "b8": {"qkv": ("hg", 3, 1, 4), "out": ("hg", 6, 1, 4), "d_out": ("hg", 6, 1, 4), "ffn1": ("hg", 202, 1, 0),
+           "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 6, 1, 4), "d_ffn1": ("hg", 6, 1, 4), "d_qkv": ("hg", 6, 1, 4)},
     "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
             "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
 }
@@ -1482,9 +1491,9 @@ def wgemm_policy(name, M, N, K):
         return None
     table = WGEMM_POLICY
     env = os.environ.get("RADHIP_WGEMM_POLICY")
-    if env:
+    if env:     # a JSON table, or the name of one of this module's tables (R4, R5A, R5G)
         import json
-        table = json.loads(env)
+        table = json.loads(env) if env.lstrip().startswith("{") else globals()["WGEMM_POLICY_" + env.upper()]
     ent = table.get("b8" if M <= 2048 else "b32", {}).get(name)
     if ent is None:
         return None

@@ -257,7 +257,7 @@ def test_pgemm_probe_stamps():
 
 
 # ---- csrc/hgemm.hip: the 8-wave ping-pong GEMM with the slab ring (every tile, split-K, group orders) ----
-HG_TILES = [0, 1, 2, 3, 4, 5, 100, 202]
+HG_TILES = [0, 1, 2, 3, 4, 5, 6, 7, 100, 202, 206]
 
 
 @pytest.mark.parametrize("tile", HG_TILES)
@@ -280,7 +280,7 @@ def test_hgemm_bias_every_tile(tile, M, N, K, splits, gm):
     assert _rel(hgemm(a, b, tile=tile, splits=splits, group_m=gm), a.float() @ b.float().t()) < 1e-2
 
 
-@pytest.mark.parametrize("tile,splits", [(0, 1), (2, 1), (3, 1), (4, 2), (1, 1)])
+@pytest.mark.parametrize("tile,splits", [(0, 1), (2, 1), (3, 1), (4, 2), (1, 1), (6, 1), (7, 2)])
 def test_hgemm_epilogues_match_wgemm(tile, splits):
     """The bias / bias + GELU / GELU-backward epilogues round where csrc/wgemm.hip's do (bf16 rounding of C, the
     aux output gelu(u) of the stored u); split-K sums in split order, so two launches give the same bits."""
