@@ -1470,12 +1470,20 @@ WGEMM_POLICY_R5G = {
     "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
             "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
 }
-# 64 x 128 tiles (code 6) for the B = 8 N = 1024 shapes: 208 tiles on 256 CUs instead of 104, no split-K
-# (tools/bench_hgemm.py, profiles/r05_hgemm_tile64.jsonl, us: out / d_out 11.1 -> 9.2, FFN2 24.0 -> 22.7,
-# FFN1's input gradient 24.1 -> 22.4, q/k/v's input gradient 20.8 -> 18.4)
-WGEMM_POLICY = {
+# 64 x 128 tiles (code 6) for the B = 8 N = 1024 shapes: 208 tiles on 256 CUs instead of 104, no split-K.
+# Standalone (tools/bench_hgemm.py, profiles/r05_hgemm_tile64.jsonl, us) every such shape gained: out / d_out
+# 11.1 -> 9.2, FFN2 24.0 -> 22.7, FFN1's input gradient 24.1 -> 22.4, q/k/v's 20.8 -> 18.4; in the step
+# (profiles/r05_ab/t6_*, per-shape graph timings) only the K = 1024 pair did (13.05 -> 11.2), the K = 4096 pair lost
+# (26.1 -> 27.5) and K = 3072 was even: the long-K shapes keep 128 x 128 with split-K 2
+WGEMM_POLICY_T6 = {
     "b8": {"qkv": ("hg", 3, 1, 4), "out": ("hg", 6, 1, 4), "d_out": ("hg", 6, 1, 4), "ffn1": ("hg", 202, 1, 0),
            "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 6, 1, 4), "d_ffn1": ("hg", 6, 1, 4), "d_qkv": ("hg", 6, 1, 4)},
+    "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
+            "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
+}
+WGEMM_POLICY = {
+    "b8": {"qkv": ("hg", 3, 1, 4), "out": ("hg", 6, 1, 4), "d_out": ("hg", 6, 1, 4), "ffn1": ("hg", 202, 1, 0),
+           "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 4, 2, 4), "d_ffn1": ("hg", 4, 2, 4), "d_qkv": ("hg", 4, 2, 4)},
     "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
             "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
 }
