@@ -530,6 +530,59 @@ int64_t rdx_hgemm_counters(int M, int N, int tile);
  * arrive, its fp32 partials in K order (deterministic). ws_bytes >= rdx_hgemm_sk_ws_bytes(M, N, K, tile). */
 int64_t rdx_hgemm_sk_ws_bytes(int M, int N, int K, int tile);
 
+/* ---- Split-precision ("x3") GEMM for the fp32 scoring pass (csrc/hgemm.hip) ------------------------------------
+ * The reference scores in fp32 without autocast (src/main.py:958-995, comment at :974-975) and the north star holds the
+ * logits to 1e-3 of its CPU path. gfx950 has no TF32 and its fp32 MFMA runs at 1/16 of the bf16 rate, so an fp32
+ * operand x is carried as two bf16 planes, hi = bf16(x) and lo = bf16(x - hi) (|x - hi - lo| <= 2^-17 |x|), and
+ *   C = A . B^T ~= Ahi . Bhi^T + Alo . Bhi^T + Ahi . Blo^T      (the dropped Alo . Blo^T is <= 2^-16 |A||B|)
+ * runs as one ping-pong launch of rdx_hgemm whose K loop makes three passes over the planes (3K/64 steps, fp32
+ * accumulation throughout). A / A_lo [M, lda], B / B_lo [N, ldb] (the frozen weight's planes), same strides; batch
+ * > 1: blockIdx.y walks `batch` problems, A planes advanced by sa and C / C_lo by sc elements (the WavLM CNN's
+ * per-utterance strided convolutions), splits must then be 1. bias fp32 [N] or NULL.
+ * epilogue RDX_EPI_F32: C fp32 [M, ldc] = acc + bias (C_lo unused);
+ *          RDX_EPI_F32_GELU_SPLIT: v = gelu(acc + bias) (erf form), C = bf16(v), C_lo = bf16(v - C) (the planes of the
+ *          next GEMM's A: FFN1 -> FFN2).
+ * tile 0-5 as rdx_hgemm; splits >= 1 with rdx_hgemm_ws_bytes / rdx_hgemm_counters workspaces. libradhip.so only
+ * (libradhip_f16.so returns RDX_EINVAL: fp16 lo planes of small values fall into fp16's subnormal range). */
+#define RDX_EPI_F32 4
+#define RDX_EPI_F32_GELU_SPLIT 5
+int rdx_hgemm_x3(const void* A, const void* A_lo, int64_t lda, int64_t sa, const void* B, const void* B_lo,
+                 int64_t ldb, void* C, void* C_lo, int64_t ldc, int64_t sc, int M, int N, int K, int batch,
+                 const float* bias, int epilogue, int tile, int splits, int group_m, void* ws, int64_t ws_bytes,
+                 int* counters, int64_t n_counters, void* stream);
+
+/* ---- The rest of the fp32 scoring pass's WavLM stream on the x3 planes (csrc/x3.hip; libradhip.so only) ---------
+ * Planes: hi = bf16(x), lo = bf16(x - hi), same shape and strides. Reference: HF WavLMModel under
+ * WavLMFrontend.forward (src/models/DualStreamSEMamba.py:392-439) as the fp32 eval runs it (src/main.py:958-995).
+ *   rdx_x3_split: x fp32 [rows, cols] (row stride ldx) -> hi / lo [rows, ldo]; cols % 4 == 0.
+ *   rdx_x3_ln_split: x = a (+ b when b != NULL; x written to sum_out when != NULL: the residual stream), rows of E = 512
+ *     or 1024 fp32; y = LayerNorm(x; gamma, beta, eps) -> planes hi / lo [M, ldo] and / or fp32 y32 [M, E]. wg != NULL
+ *     (E = 1024, 64-dim heads): the HF WavLMAttention gate of y, gate[m, h] = ga (gb gconst[h] - 1) + 2 with (ga, gb)
+ *     = sigmoid of the two 4-sums of gru_rel_pos_linear(y_head) (wg [8, 64], bg [8]), gate fp32 [M, H].
+ *   rdx_x3_attn_fwd: o = softmax(scaling q k^T + gate[b, i, h] rel[h, j - i + T - 1]) v per (utterance, head) in fp32
+ *     (v_mfma_f32_16x16x4_f32), q / k / v fp32 [B*T, ld] column blocks of 64 per head, rel the [H, 2T - 1] table of
+ *     the relative position bias (radhip.ops.rel_bias_table), output planes [B*T, ldo]; T <= 256; qsplit workgroups
+ *     per (utterance, head) share its query tiles.
+ *   rdx_x3_posconv_fwd: out = h + gelu(conv1d(h, W, bias, padding 64, groups 16)[:, :T]) (HF
+ *     WavLMPositionalConvEmbedding + the encoder's residual add), h / out fp32 [B, T, 1024] (out != h); wk_hi / wk_lo
+ *     the bf16 planes of W in rdx_posconv_fwd's [16][128][64][64] layout, bias fp32 [1024].
+ *   rdx_x3_fe_conv0: CNN layer 0 of rdx_fe_conv0 in fp32 (unrounded waveform and weights w fp32 [512, 10], bias fp32
+ *     [512] or NULL) + LayerNorm(512) + GELU -> planes [B, T0, 512].
+ *   rdx_x3_fe_ln_gelu: LayerNorm(512) + GELU of in fp32 [rows, 512] (+ bias fp32 [512] when != NULL) -> planes
+ *     [rows, 512], or fp32 out32 when != NULL (the last layer). */
+int rdx_x3_split(const float* x, int64_t ldx, int64_t rows, int cols, void* hi, void* lo, int64_t ldo, void* stream);
+int rdx_x3_ln_split(const float* a, const float* b, float* sum_out, const float* gamma, const float* beta, float eps,
+                    void* hi, void* lo, int64_t ldo, float* y32, const float* wg, const float* bg, const float* gconst,
+                    float* gate, int64_t M, int E, void* stream);
+int rdx_x3_attn_fwd(const float* q, const float* k, const float* v, int64_t ld, const float* gate, const float* rel,
+                    float scaling, void* ohi, void* olo, int64_t ldo, int B, int T, int H, int qsplit, void* stream);
+int rdx_x3_posconv_fwd(const float* h, const void* wk_hi, const void* wk_lo, const float* bias, float* out, int B,
+                       int T, void* stream);
+int rdx_x3_fe_conv0(const float* x, int64_t batch, int64_t len, const float* w, const float* bias, const float* gamma,
+                    const float* beta, float eps, int ksize, int stride, void* out_hi, void* out_lo, void* stream);
+int rdx_x3_fe_ln_gelu(const float* in, int64_t rows, const float* bias, const float* gamma, const float* beta,
+                      float eps, void* out_hi, void* out_lo, float* out32, void* stream);
+
 /* Column sums of fp32 row-partial buffers, up to 4 problems per launch: out_k[c] = sum_r in_k[r * ld_k + c] (rows
  * in order, fixed-order combine: deterministic). Replaces the torch reductions of the scan / depthwise-conv backward
  * partials (csrc/layersum.hip). */

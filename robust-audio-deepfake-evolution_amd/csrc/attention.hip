@@ -864,6 +864,11 @@ __global__ __launch_bounds__(AT_FUSED_MAXNT * 64) void attn_bwd_fused_kernel(
     __syncthreads();
     int* flag = reinterpret_cast<int*>(L + FB_SC);   // the row-scalar area is free in phase 2
     if (threadIdx.x == 0) {
+#if !defined(__gfx950__) && !defined(__gfx942__)
+      // the fence-free publish relies on gfx94x / gfx950's write-through (sc1) store encoding; any other target
+      // releases the partials explicitly
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
       const int t = __hip_atomic_fetch_add(counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = t;
       if (t == 1) {

@@ -84,6 +84,11 @@ struct Args {
   float* ws;         // split-K partial slabs [tile][split][FM*FN][512][4] fp32
   int* counters;     // split-K arrival tickets, one per tile, zero between launches
   int wide;          // C / aux / aux_out rows 16-byte aligned: 16-byte row-phase accesses
+  // split-precision (X3) form, csrc/hgemm.hip rdx_hgemm_x3: A = A + A2, B = B + B2 (bf16 hi / lo planes of fp32
+  // operands, same strides); the K loop runs 3 K passes, (A, B), (A2, B), (A, B2)
+  const hst* A2;
+  const hst* B2;
+  int64_t sa, sc;    // batch strides (elements) of A / A2 and of C / aux_out (blockIdx.y = batch index)
 };
 
 // The phase / slab plan of a BM x BN tile with its A part split NPA ways and its B part NPB ways.
@@ -184,9 +189,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 // One output tile's K steps [kb, kb + nk): the ring, the phases, then either the epilogue (nc == 1) or this
 // contribution's fp32 partial in slot `slot` of the tile's nc and, for the last of them to arrive, the sum of the nc
 // partials in slot order and the epilogue.
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL>
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL, int X3 = 0>
 __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, int nt, int tile, int kb, int nk,
                                             int slot, int nc, int maxc) {
+  // X3 batched form: blockIdx.y selects the problem (A planes advanced by sa, C / aux_out by sc elements)
+  const int64_t yb = X3 ? (int64_t)blockIdx.y : 0;
   using P = Plan<BM, BN, NPA, NPB>;
   constexpr int FM = P::FM, FN = P::FN, WTM = P::WTM, WTN = P::WTN, FMP = P::FMP, FNP = P::FNP;
   constexpr int NPH = P::NPH, SPK = P::SPK, S = U * SPK;
@@ -204,6 +211,15 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
   const i32x4 ra = rsrc(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)(rows_a - 1) * lda_b + (int64_t)K * 2));
   const i32x4 rb = rsrc(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(rows_b - 1) * ldb_b + (int64_t)K * 2));
   const i32x4 rnull = rsrc(g.A, 0u);
+  // X3: the planes' base addresses (64-bit scalars: the descriptor of a refill is built from the pass's base, so
+  // no descriptor is selected through memory), their buffer ranges, and the K steps per pass
+  const uint64_t xa0 = (uint64_t)(g.A + yb * g.sa + (int64_t)m0 * g.lda);
+  const uint64_t xa1 = X3 ? (uint64_t)(g.A2 + yb * g.sa + (int64_t)m0 * g.lda) : xa0;
+  const uint64_t xb0 = (uint64_t)(g.B + (int64_t)n0 * g.ldb);
+  const uint64_t xb1 = X3 ? (uint64_t)(g.B2 + (int64_t)n0 * g.ldb) : xb0;
+  const uint32_t xra = (uint32_t)((int64_t)(rows_a - 1) * lda_b + (int64_t)K * 2);
+  const uint32_t xrb = (uint32_t)((int64_t)(rows_b - 1) * ldb_b + (int64_t)K * 2);
+  const int nkp = K / 64;
 
   // loop-invariant DMA source offsets of this lane, one per slab of a K step: image row ir = 8 * wave + lane / 8,
   // position lane % 8 holding source chunk swz(ir, lane % 8)
@@ -225,8 +241,19 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
     constexpr int j = decltype(JC)::value;
     constexpr int isb = P::slab_isb(j);
     const bool live = kst < nk;
-    const i32x4 rs = live ? (isb ? rb : ra) : rnull;
-    const int kbytes = live ? (kb + kst) * 128 : 0;
+    i32x4 rs;
+    int kbytes;
+    if constexpr (X3) {
+      // pass p of global K step ks: (A, B), (A2, B), (A, B2)
+      const int ks = kb + kst;
+      const int p = (ks >= nkp) + (ks >= 2 * nkp);
+      const uint64_t base = isb ? (p == 2 ? xb1 : xb0) : (p == 1 ? xa1 : xa0);
+      rs = rsrc((const void*)base, live ? (isb ? xrb : xra) : 0u);
+      kbytes = __builtin_amdgcn_readfirstlane(live ? (ks - p * nkp) * 128 : 0);   // uniform: keep it scalar
+    } else {
+      rs = live ? (isb ? rb : ra) : rnull;
+      kbytes = live ? (kb + kst) * 128 : 0;
+    }
     buffer_load_lds(rs, (__attribute__((address_space(3))) uint32_t*)(lds + (pos * SPK + j) * SLAB + wave * 1024),
                     16, voff[j], kbytes, 0, 0);
   };
@@ -249,7 +276,8 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
   constexpr int BIAS_OFF = (S * SLAB > BM * (BN * 2 + 16) ? S * SLAB : BM * (BN * 2 + 16));
   constexpr int FLAG_OFF = BIAS_OFF + BN * 2;     // the split / stream-K arrival broadcast
   static_assert(FLAG_OFF + 16 <= 160 * 1024, "bias slot");
-  const bool has_bias = EPI != RDX_EPI_GELU_BWD && g.bias != nullptr;
+  constexpr bool F32EPI = EPI == RDX_EPI_F32 || EPI == RDX_EPI_F32_GELU_SPLIT;
+  const bool has_bias = EPI != RDX_EPI_GELU_BWD && !F32EPI && g.bias != nullptr;
   uint2 bias4 = make_uint2(0u, 0u);
   if (has_bias && tid < BN / 4 && n0 + 4 * tid < N) bias4 = *reinterpret_cast<const uint2*>(g.bias + n0 + 4 * tid);
   __builtin_amdgcn_sched_barrier(0);
@@ -363,6 +391,11 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
     __syncthreads();
     int* flag = reinterpret_cast<int*>(lds + FLAG_OFF);
     if (tid == 0) {
+#if !defined(__gfx950__) && !defined(__gfx942__)
+      // the fence-free publish relies on gfx94x / gfx950's write-through (sc1) store encoding; any other target
+      // releases the partials explicitly
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
       const int ticket = __hip_atomic_fetch_add(g.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = ticket;
       if (ticket == nc - 1) {
@@ -397,6 +430,88 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
   // epilogue: acc[i][j][e] = C[m0 + wm*WTM + i*16 + fr][n0 + wn*WTN + j*16 + 4*fq + e], through an LDS image
   // (fp32 acc + bias rounded once, as the unfused layer rounds), then whole rows, 16 bytes per lane
   constexpr int PITCH = BN * 2 + 16;
+  if constexpr (F32EPI) {
+    // split-precision epilogues: fp32 bias; RDX_EPI_F32 stores C fp32 from the registers (16 bytes per lane, 64-byte
+    // row pieces); RDX_EPI_F32_GELU_SPLIT forms v = gelu(acc + bias) and leaves it as the bf16 pair hi = bf16(v)
+    // (C), lo = bf16(v - hi) (aux_out), each through the LDS image and whole-row stores
+    const float* biasf = reinterpret_cast<const float*>(g.bias);
+    f32x4 bv[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = n0 + wn * WTN + j * 16 + 4 * fq;
+      bv[j] = (biasf != nullptr && c < N) ? *reinterpret_cast<const f32x4*>(biasf + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (EPI == RDX_EPI_F32) {
+      float* Cf = reinterpret_cast<float*>(g.C) + yb * g.sc;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = m0 + wm * WTM + i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = n0 + wn * WTN + j * 16 + 4 * fq;
+          if (r < M && c < N) *reinterpret_cast<f32x4*>(Cf + (int64_t)r * g.ldc + c) = acc[i][j] + bv[j];
+        }
+      }
+      return;
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = gelu(acc[i][j][e] + bv[j][e]);
+      constexpr int CPR = BN / 8, ITER = BM * CPR / 512;
+      static_assert((BM * CPR) % 512 == 0, "row phase");
+      char* img = lds;
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        __syncthreads();                          // the ring (pass 0) / the previous pass's row phase is done
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r = wm * WTM + i * 16 + fr;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int c = wn * WTN + j * 16 + 4 * fq;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = pass == 0 ? acc[i][j][e] : acc[i][j][e] - hround(acc[i][j][e]);
+            *reinterpret_cast<uint2*>(img + r * PITCH + c * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          }
+        }
+        __syncthreads();
+        hst* dst = (pass == 0 ? g.C : g.aux_out) + yb * g.sc;
+        const int64_t ld = pass == 0 ? g.ldc : g.ldao;
+        if (m0 + BM <= M && n0 + BN <= N && g.wide) {
+          uint4 qv[ITER];
+#pragma unroll
+          for (int it = 0; it < ITER; ++it) {
+            const int idx = tid + it * 512, r = idx / CPR, c = (idx - r * CPR) * 8;
+            qv[it] = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
+          }
+#pragma unroll
+          for (int it = 0; it < ITER; ++it) {
+            const int idx = tid + it * 512, r = idx / CPR, c = (idx - r * CPR) * 8;
+            *reinterpret_cast<uint4*>(dst + (int64_t)(m0 + r) * ld + n0 + c) = qv[it];
+          }
+        } else {
+          for (int idx = tid; idx < BM * CPR; idx += 512) {
+            const int r = idx / CPR, c = (idx - r * CPR) * 8;
+            const int m = m0 + r, n = n0 + c;
+            if (m >= M || n >= N) continue;
+            const uint4 q = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
+            hst* o = dst + (int64_t)m * ld + n;
+            if (n + 8 <= N && g.wide) {
+              *reinterpret_cast<uint4*>(o) = q;
+            } else {
+              *reinterpret_cast<uint2*>(o) = make_uint2(q.x, q.y);
+              if (n + 8 <= N) *reinterpret_cast<uint2*>(o + 4) = make_uint2(q.z, q.w);
+            }
+          }
+        }
+      }
+      return;
+    }
+  }
   static_assert(BM * PITCH <= 160 * 1024, "epilogue image");
   char* img = lds;
   uint2 bb[FN];
@@ -480,10 +595,11 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
 // splits >= 1: work id (XCD-dealt) = tile * splits + split; splits == 0 (stream-K): the grid's workgroups take
 // equal contiguous runs of the (tile, K step) units in tile order, a tile shared by several runs summed by the last
 // of them to arrive (its partial slots in K order).
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0, int SK = 0>
-__global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0, int SK = 0, int X3 = 0>
+__global__ __launch_bounds__(512, 1) void hgemm_kernel(const Args g) {
   extern __shared__ __attribute__((aligned(1024))) char lds[];
-  const int nk_all = g.K / 64;
+  const int nk_all = (X3 ? 3 : 1) * (g.K / 64);
+
   const int tiles = g.tiles_m * g.tiles_n;
   if constexpr (SK == 0) {
     const int SPL = g.splits;
@@ -497,7 +613,7 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
       tile_coords(g, tile, mt, nt);
     }
     const int kb = split * nk_all / SPL, nk = (split + 1) * nk_all / SPL - kb;
-    run_segment<BM, BN, NPA, NPB, U, EPI, PRIO, ABL>(g, lds, mt, nt, tile, kb, nk, split, SPL, SPL);
+    run_segment<BM, BN, NPA, NPB, U, EPI, PRIO, ABL, X3>(g, lds, mt, nt, tile, kb, nk, split, SPL, SPL);
     return;
   }
   if (g.splits != 0) return;
@@ -519,14 +635,14 @@ __global__ __launch_bounds__(512, 1) void hgemm_kernel(Args g) {
   }
 }
 
-template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0, int SK = 0>
-static int launch(Args g, hipStream_t st) {
+template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL = 0, int SK = 0, int X3 = 0>
+static int launch(Args g, hipStream_t st, int batch = 1) {
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   constexpr int ring = U * (BM / 64 + BN / 64) * 8192, image = BM * (BN * 2 + 16);
   constexpr int lds = (ring > image ? ring : image) + BN * 2 + 16;   // + the bias slot and the arrival flag
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO, ABL, SK>;
+  auto kern = &hgemm_kernel<BM, BN, NPA, NPB, U, EPI, PRIO, ABL, SK, X3>;
   static bool lds_ok = false;
   if (!lds_ok) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -535,7 +651,7 @@ static int launch(Args g, hipStream_t st) {
     lds_ok = true;
   }
   const unsigned grid = g.splits >= 1 ? (unsigned)(g.tiles_m * g.tiles_n * g.splits) : (unsigned)g.grid_sk;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, g);
+  hipLaunchKernelGGL(kern, dim3(grid, batch), dim3(512), lds, st, g);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -564,6 +680,22 @@ static int dispatch(const Args& g, int tile, hipStream_t st) {
     default: return RDX_EINVAL;
   }
 }
+
+#ifndef RDX_F16
+// split-precision (X3) launches: the eval tiles (bf16 planes only)
+template <int EPI>
+static int dispatch_x3(const Args& g, int tile, int batch, hipStream_t st) {
+  switch (tile) {
+    case 0: return launch<256, 256, 2, 2, 2, EPI, 0, 0, 0, 1>(g, st, batch);
+    case 1: return launch<256, 192, 2, 1, 2, EPI, 0, 0, 0, 1>(g, st, batch);
+    case 2: return launch<128, 256, 1, 2, 3, EPI, 0, 0, 0, 1>(g, st, batch);
+    case 3: return launch<128, 192, 2, 1, 3, EPI, 0, 0, 0, 1>(g, st, batch);
+    case 4: return launch<128, 128, 1, 1, 4, EPI, 0, 0, 0, 1>(g, st, batch);
+    case 5: return launch<256, 128, 2, 1, 3, EPI, 0, 0, 0, 1>(g, st, batch);
+    default: return RDX_EINVAL;
+  }
+}
+#endif
 
 // timing probes (bias epilogue, wrong results by design): 1000 + tile without refills in the K loop, 2000 + tile
 // without MFMA, 3000 + tile without the epilogue
@@ -700,6 +832,8 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
   }
   g.ws = (float*)ws;
   g.counters = counters;
+  g.A2 = g.B2 = nullptr;
+  g.sa = g.sc = 0;
   g.wide = al(C, 16) && ldc % 8 == 0;
   if (epilogue == RDX_EPI_BIAS_GELU) g.wide = g.wide && al(aux_out, 16) && ldao % 8 == 0;
   if (epilogue == RDX_EPI_GELU_BWD) g.wide = g.wide && al(aux, 16) && ldaux % 8 == 0;
@@ -719,4 +853,67 @@ extern "C" int rdx_hgemm(const void* A, int64_t lda, const void* B, int64_t ldb,
            : prio == 1 ? hg::dispatch<RDX_EPI_GELU_BWD, 1>(g, base, st)
                        : hg::dispatch<RDX_EPI_GELU_BWD, 2>(g, base, st);
   }
+}
+
+extern "C" int rdx_hgemm_x3(const void* A, const void* A_lo, int64_t lda, int64_t sa, const void* B, const void* B_lo,
+                            int64_t ldb, void* C, void* C_lo, int64_t ldc, int64_t sc, int M, int N, int K, int batch,
+                            const float* bias, int epilogue, int tile, int splits, int group_m, void* ws,
+                            int64_t ws_bytes, int* counters, int64_t n_counters, void* stream) {
+#ifdef RDX_F16
+  (void)A; (void)A_lo; (void)lda; (void)sa; (void)B; (void)B_lo; (void)ldb; (void)C; (void)C_lo; (void)ldc; (void)sc;
+  (void)M; (void)N; (void)K; (void)batch; (void)bias; (void)epilogue; (void)tile; (void)splits; (void)group_m;
+  (void)ws; (void)ws_bytes; (void)counters; (void)n_counters; (void)stream;
+  return RDX_EINVAL;                              // bf16 planes only (libradhip.so)
+#else
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  RDX_REQUIRE(A && A_lo && B && B_lo && C && M > 0 && N > 0 && K > 0 && batch >= 1);
+  RDX_REQUIRE(al(A, 16) && al(A_lo, 16) && al(B, 16) && al(B_lo, 16) && al(C, 16));
+  // A rows may overlap (lda < K: a strided convolution's im2col rows, never materialised)
+  RDX_REQUIRE(K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda > 0 && ldb >= K && N % 4 == 0 && ldc >= N);
+  RDX_REQUIRE(((int64_t)(M - 1) * lda + K) * 2 < 0x7fffffffLL && (int64_t)N * ldb * 2 < 0x7fffffffLL);
+  RDX_REQUIRE(batch == 1 || (sa % 8 == 0 && sc % 8 == 0 && sa >= 0 && sc >= 0 && splits == 1));
+  RDX_REQUIRE(!bias || al(bias, 16));
+  RDX_REQUIRE(epilogue == RDX_EPI_F32 || epilogue == RDX_EPI_F32_GELU_SPLIT);
+  if (epilogue == RDX_EPI_F32) RDX_REQUIRE(ldc % 4 == 0);
+  else RDX_REQUIRE(C_lo && al(C_lo, 16) && ldc % 8 == 0);
+  int bm, bn;
+  RDX_REQUIRE(tile >= 0 && tile <= 5 && hg::geometry(tile, &bm, &bn));
+  RDX_REQUIRE(group_m >= 0 || ((group_m == -1 || group_m == -2 || group_m == -4 || group_m == -8) && splits != 0));
+  RDX_REQUIRE(splits >= 1 && splits <= 16 && splits <= 3 * (K / 64));
+  if (splits > 1) {
+    const int64_t need = rdx_hgemm_ws_bytes(M, N, tile, splits);
+    const int64_t nc = rdx_hgemm_counters(M, N, tile);
+    RDX_REQUIRE(need > 0 && ws && al(ws, 16) && ws_bytes >= need && counters && n_counters >= nc);
+  }
+  hg::Args g;
+  g.A = (const hst*)A;
+  g.A2 = (const hst*)A_lo;
+  g.lda = lda;
+  g.B = (const hst*)B;
+  g.B2 = (const hst*)B_lo;
+  g.ldb = ldb;
+  g.C = (hst*)C;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.bias = (const hst*)bias;                      // fp32 [N], read as such by the F32 epilogues
+  g.aux = nullptr;
+  g.ldaux = 0;
+  g.aux_out = (hst*)C_lo;
+  g.ldao = ldc;
+  g.tiles_m = g.tiles_n = 0;
+  g.group_m = group_m;
+  g.splits = splits;
+  g.maxc = splits;
+  g.grid_sk = 0;
+  g.ws = (float*)ws;
+  g.counters = counters;
+  g.sa = sa;
+  g.sc = sc;
+  g.wide = ldc % 8 == 0 && (batch == 1 || sc % 8 == 0);
+  hipStream_t st = as_stream(stream);
+  return epilogue == RDX_EPI_F32 ? hg::dispatch_x3<RDX_EPI_F32>(g, tile, batch, st)
+                                 : hg::dispatch_x3<RDX_EPI_F32_GELU_SPLIT>(g, tile, batch, st);
+#endif
 }

@@ -305,6 +305,9 @@ extern "C" int rdx_lgemm(const void* A, int64_t lda, int a_f32, const void* W, i
   RDX_REQUIRE(epilogue != RDX_EPI_BIAS_GELU || (aux_out && ldao >= N && !c_f32));
   RDX_REQUIRE(epilogue != RDX_EPI_GELU_BWD || (aux && ldaux >= N && !bias));
   RDX_REQUIRE(!R || ldr >= N);
+  // 32-bit buffer ranges and element offsets (the OOB sentinel 0x80000000 must lie outside every operand's range)
+  RDX_REQUIRE(((int64_t)(M - 1) * lda + K) * (a_f32 ? 4 : 2) < 0x7fffffffLL &&
+              ((int64_t)(N - 1) * ldw + K) * 2 < 0x7fffffffLL);
   lg::Args g{A, lda, (const hst*)W, ldw, C, ldc, (const hst*)bias, (const hst*)aux, ldaux, (hst*)aux_out, ldao,
              R, ldr, M, N, K, 0, 0, 0};
   g.vec_a = (((uintptr_t)A & 15) == 0 && (lda % (a_f32 ? 4 : 8)) == 0 && K % 8 == 0) ? 1 : 0;

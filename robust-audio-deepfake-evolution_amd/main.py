@@ -195,7 +195,7 @@ class Runner:
         ds = ds_cls(keys, base_dir)
         bs = int(self.config.get("test_config", {}).get("batch_size", self.config["batch_size"]))
         feeder = EvalFeeder(ds, bs, threads=self.threads, zero_on_error=zero_on_error)
-        eval_amp = None if self.args.eval_amp == "fp32" else AMP[self.args.eval_amp]
+        eval_amp = {"fp32": None, "x3": "x3"}.get(self.args.eval_amp) or AMP[self.args.eval_amp]
         produce_evaluation_file_sharded(ds, model, self.device, save_path, trial_path, batch_size=bs,
                                         criterion=self.criterion, batches=feeder.batches, fmt=fmt, amp=eval_amp)
         self.barrier()
@@ -517,8 +517,11 @@ def parse_args(argv=None):
     parser.add_argument("--pretrained_weights", type=str, default=None, help="pretrained weights for fine-tuning")
     parser.add_argument("--model", type=str, default=None, help="override the model architecture")
     parser.add_argument("--amp", default="fp16", choices=sorted(AMP), help="autocast dtype (reference: fp16)")
-    parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "bf16", "fp16"],
-                        help="scoring precision: fp32 as the reference scores (default), or bf16 / fp16 autocast, which "
+    parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "x3", "bf16", "fp16"],
+                        help="scoring precision: fp32 as the reference scores (default); x3, the reference's fp32 "
+                             "scoring with the WavLM stream on the hand-written split-precision kernels "
+                             "(radhip/wavlm_x3.py: bf16 hi/lo planes, three MFMA products per GEMM, fp32 attention; "
+                             "logits within 1e-3 of fp32); or bf16 / fp16 autocast, which "
                              "runs the hand-written HIP encoder / SincNet path (tools/bench_eval.py: throughput and "
                              "score deviation). 16-bit scores are parity-unpinned against the reference (no fixture "
                              "pins its EER); with --eval_amp bf16 / fp16 they also drive the dev-set best-model "

@@ -16,6 +16,7 @@ LIB16_PATH = os.environ.get("RADHIP_LIB16", os.path.join(_HERE, "libradhip_f16.s
 RDX_F32 = 0
 RDX_BF16 = 1
 EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_RESID_DROP = 0, 1, 2, 3
+EPI_F32, EPI_F32_GELU_SPLIT = 4, 5          # rdx_hgemm_x3
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -192,6 +193,16 @@ SIGNATURES = {
     "rdx_focal_mixup_fwd": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_int,
                                     c_f32, c_vp, c_vp, c_vp]),
     "rdx_focal_mixup_bwd": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
+    "rdx_hgemm_x3": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_int,
+                             c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "rdx_x3_split": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
+    "rdx_x3_ln_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                c_i64, c_int, c_vp]),
+    "rdx_x3_attn_fwd": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_int, c_int, c_int,
+                                c_int, c_vp]),
+    "rdx_x3_posconv_fwd": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
+    "rdx_x3_fe_conv0": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_int, c_int, c_vp, c_vp, c_vp]),
+    "rdx_x3_fe_ln_gelu": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
     "rdx_fgm_attack": (c_int, [c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                ctypes.POINTER(c_i64), c_f32, c_vp, c_vp]),
 }

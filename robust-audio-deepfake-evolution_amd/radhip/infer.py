@@ -22,8 +22,15 @@ import torch.nn.functional as F
 
 
 def _scores(model, batch_x, criterion=None, amp=None):
-    """amp: None (fp32, the reference's eval) or a dtype to autocast the forward to (bf16: the fused HIP path)."""
-    ctx = torch.autocast("cuda", dtype=amp) if amp is not None and batch_x.is_cuda else contextlib.nullcontext()
+    """amp: None (fp32, the reference's eval), "x3" (fp32 eval with the WavLM stream on the split-precision kernels,
+    radhip/wavlm_x3.py) or a dtype to autocast the forward to (bf16 / fp16: the fused 16-bit HIP path)."""
+    if amp == "x3":
+        from . import wavlm_x3
+        ctx = wavlm_x3.scoring()
+    elif amp is not None and batch_x.is_cuda:
+        ctx = torch.autocast("cuda", dtype=amp)
+    else:
+        ctx = contextlib.nullcontext()
     with ctx:
         feats, out = model(batch_x)
     feats, out = feats.float(), out.float()

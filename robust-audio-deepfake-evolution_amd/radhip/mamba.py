@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import ops
 from ._lib import check, lib
-from .linear import SideLinear, _LGEMM, _ON, _cast, _cast_t, _lg_ok, _rows, _weight_grads, side_linear
+from .linear import LG_MAX_K, SideLinear, _LGEMM, _ON, _cast, _cast_t, _lg_ok, _rows, _weight_grads, side_linear
 from .ops import BiGate, DWConvBidir, SelectiveScan, SplitLast
 
 
@@ -83,7 +83,11 @@ class Mamba(nn.Module):
         if (_FUSED and _LGEMM and _ON and x.is_cuda and x.dim() == 3 and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") in ops.HALF and ops.scan2_enabled() and self.d_state == 16
                 and self.in_proj.bias is None and self.x_proj.bias is None and self.out_proj.bias is None
-                and self.conv1d.bias is not None):
+                and self.conv1d.bias is not None
+                # every GEMM of the node runs on csrc/lgemm.hip with K = d_model, d_inner or dt_rank: within the K
+                # its single-chunk LDS staging is built for (radhip/linear.py LG_MAX_K; larger widths take the
+                # module path, whose linears fall back to hipBLASLt)
+                and max(x.shape[-1], self.in_proj.weight.shape[0] // 2, self.dt_proj.weight.shape[1]) <= LG_MAX_K):
             dt = torch.get_autocast_dtype("cuda")
             with torch.autocast("cuda", enabled=False):
                 return MambaBiFn.apply(x, self.in_proj.weight, self.conv1d.weight, self.conv1d.bias,

@@ -1641,20 +1641,36 @@ def _wgemm_workspace(dev, ws_bytes, n_counters):
     return cur
 
 
-_WS_KEEP = []   # every workspace pair ever handed out: captured graphs hold raw pointers into them
+_WS_KEEP = []         # every graph workspace pair ever handed out: captured graphs hold raw pointers into them
+_CAPTURE_TICKETS = []  # tickets allocated inside a capture: zeroed eagerly by finalize_graph_workspace
 
 
 def _grow_workspace(table, key, cur, n, n_counters, dtype, dev):
     """A larger (slab, zeroed tickets) workspace for `key`. During a capture the allocation comes from the graph's
-    memory pool and the tickets' zero fill is a node of the graph (the tickets are zero whenever a replay reaches
-    it: each launch leaves them at zero); the pair it replaces stays referenced (_WS_KEEP), since graphs captured
-    earlier keep its addresses."""
+    memory pool and its zero fill is only a node of the capturing graph: another graph captured later on the same
+    (device, "graph") key could replay first and find the tickets uninitialised. So the tickets grown in a capture are
+    also zeroed eagerly once the capture has ended (finalize_graph_workspace, called by every capture site before
+    any replay). A graph workspace it replaces stays referenced (_WS_KEEP): graphs captured earlier keep its
+    addresses. An eager per-stream workspace it replaces is freed (no graph points into it)."""
     n = max(n, cur[0].numel() if cur else 0)
     nc = max(n_counters, cur[1].numel() if cur else 0)
     new = (torch.empty(n, dtype=dtype, device=dev), torch.zeros(nc, dtype=torch.int32, device=dev))
-    _WS_KEEP.append(new)
+    if key[1] == "graph":
+        _WS_KEEP.append(new)
+        if torch.cuda.is_current_stream_capturing():
+            _CAPTURE_TICKETS.append(new[1])
     table[key] = new
     return new
+
+
+def finalize_graph_workspace(dev=None):
+    """After a capture (before any replay): zero, eagerly, every split-K / split-attention ticket array a capture
+    allocated, then synchronise."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("finalize_graph_workspace inside a capture")
+    while _CAPTURE_TICKETS:
+        _CAPTURE_TICKETS.pop().zero_()
+    torch.cuda.synchronize(dev)
 
 
 def reserve_graph_workspace(dev):

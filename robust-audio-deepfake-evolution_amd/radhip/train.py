@@ -826,7 +826,7 @@ class GraphedMicroStep:
                 self._fgm()
         if self.adv:
             self._restore()
-        torch.cuda.synchronize(tr.device)
+        ops.finalize_graph_workspace(tr.device)     # tickets grown inside a capture: zero before any replay
         self._unbind()
         # the graphs hold the "store"/"use" branches; eager calls (eval, tools) must recompute the CNN.
         # The stored feature tensor stays referenced: graph 1 reads it on every replay.

@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import wavlm_fused
+from . import wavlm_fused, wavlm_x3
 from .ops import HALF, GatedAttention, PosConv, fe_conv_weights, feature_encoder_fused, half_dtype, posconv_weights
 
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
@@ -519,6 +519,10 @@ class WavLMEncoderModel(nn.Module):
 
     def forward(self, input_values, output_hidden_states=True, layerdrop=None):
         x = input_values
+        if wavlm_x3.eligible(self, x):
+            # the fp32 scoring pass on the split-precision kernels (radhip/wavlm_x3.py)
+            self.encoder.state_defer = None
+            return wavlm_x3.forward(self, x)
         frozen = self._cnn_frozen()
         if frozen and self.cnn_feats_given is not None:
             feats = self.cnn_feats_given

@@ -437,7 +437,7 @@ class WindowStep:
                     for p, v in zip(self.fp_real, fp_saved):
                         p.copy_(v)
                 tr.fgm.backup = {}
-        torch.cuda.synchronize(tr.device)
+        ops.finalize_graph_workspace(tr.device)     # tickets grown inside a capture: zero before any replay
         self._unbind()
         tr.grads.zero()
         self.fp_grad.zero_()
