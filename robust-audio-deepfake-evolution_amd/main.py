@@ -517,11 +517,12 @@ def parse_args(argv=None):
     parser.add_argument("--pretrained_weights", type=str, default=None, help="pretrained weights for fine-tuning")
     parser.add_argument("--model", type=str, default=None, help="override the model architecture")
     parser.add_argument("--amp", default="fp16", choices=sorted(AMP), help="autocast dtype (reference: fp16)")
-    parser.add_argument("--eval_amp", default="fp32", choices=["fp32", "x3", "bf16", "fp16"],
-                        help="scoring precision: fp32 as the reference scores (default); x3, the reference's fp32 "
-                             "scoring with the WavLM stream on the hand-written split-precision kernels "
+    parser.add_argument("--eval_amp", default="x3", choices=["x3", "fp32", "bf16", "fp16"],
+                        help="scoring precision: x3 (default), the reference's fp32 scoring (src/main.py:958-995, no "
+                             "autocast) with the WavLM stream on the hand-written split-precision kernels "
                              "(radhip/wavlm_x3.py: bf16 hi/lo planes, three MFMA products per GEMM, fp32 attention; "
-                             "logits within 1e-3 of fp32); or bf16 / fp16 autocast, which "
+                             "scores within 2e-6 of fp32, 2.2x its rate: tools/bench_eval.py); fp32, the same forward "
+                             "with the WavLM stream on torch SDPA + hipBLASLt fp32; or bf16 / fp16 autocast, which "
                              "runs the hand-written HIP encoder / SincNet path (tools/bench_eval.py: throughput and "
                              "score deviation). 16-bit scores are parity-unpinned against the reference (no fixture "
                              "pins its EER); with --eval_amp bf16 / fp16 they also drive the dev-set best-model "
