@@ -529,6 +529,12 @@ int64_t rdx_hgemm_counters(int M, int N, int tile);
  * the (tile, 64-deep K step) units in tile order, and a tile shared by several runs is summed by the last of them to
  * arrive, its fp32 partials in K order (deterministic). ws_bytes >= rdx_hgemm_sk_ws_bytes(M, N, K, tile). */
 int64_t rdx_hgemm_sk_ws_bytes(int M, int N, int K, int tile);
+/* Batched form (RDX_EPI_BIAS, splits 1): `batch` problems C_y [M, ldc] = A_y . B^T + bias in one launch, A_y = A + y sa
+ * (rows may overlap, lda < K: a token-major activation read as a strided convolution's im2col matrix), C_y = C + y sc.
+ * The frozen WavLM CNN's layers 1-6 (HF WavLMFeatureEncoder, src/models/DualStreamSEMamba.py:392-439; csrc/featconv.hip
+ * layout). tile 0-7 as rdx_hgemm, group_m >= 0. */
+int rdx_hgemm_batched(const void* A, int64_t lda, int64_t sa, const void* B, int64_t ldb, void* C, int64_t ldc,
+                      int64_t sc, int M, int N, int K, int batch, const void* bias, int tile, int group_m, void* stream);
 
 /* ---- Split-precision ("x3") GEMM for the fp32 scoring pass (csrc/hgemm.hip) ------------------------------------
  * The reference scores in fp32 without autocast (src/main.py:958-995, comment at :974-975) and the north star holds the

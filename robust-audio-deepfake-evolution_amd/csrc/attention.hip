@@ -315,10 +315,16 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
   if (qvalid) {
     const float inv = 1.f / l;
     hst* orow = o + ((int64_t)b * T + qi) * ldo + col0;
+    // registers 4k .. 4k + 3 hold the 4 consecutive columns crow(4k, hh) .. + 3 of the lane's row: one 8-byte store
+    // each (ldo and col0 keep them 8-byte aligned: rdx_attn_fwd requires ldo % 4 == 0)
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) orow[db * 32 + crow(i, hh)] = f2h(oacc[db][i] * inv);
+      for (int k4 = 0; k4 < 4; ++k4) {
+        *reinterpret_cast<uint2*>(orow + db * 32 + crow(4 * k4, hh)) =
+            make_uint2(hpack2(oacc[db][4 * k4] * inv, oacc[db][4 * k4 + 1] * inv),
+                       hpack2(oacc[db][4 * k4 + 2] * inv, oacc[db][4 * k4 + 3] * inv));
+      }
     if (hh == 0) lse[bh * T + qi] = (m + __log2f(l)) * 0.69314718055994531f;  // natural-log LSE
   }
 }
@@ -999,6 +1005,7 @@ extern "C" int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t l
                             int salt, float p_drop, float scale, void* o, int64_t ldo, float* lse,
                             uint32_t* keep_mask, int B, int T, int H, int head_dim, void* stream) {
   RDX_REQUIRE(attn_ok(q, ldq, k, ldk, v, ldv, B, T, H) && gate && rel_bias && o && lse && ldo >= (int64_t)H * AT_DH);
+  RDX_REQUIRE(ldo % 4 == 0 && ((uintptr_t)o & 7) == 0);   // 8-byte output stores
   RDX_REQUIRE(p_drop >= 0.f && p_drop < 1.f && (p_drop == 0.f || seed_dev));
   if (head_dim != AT_DH || T > AT_MAXNT * AT_TILE) return RDX_EUNSUPPORTED;
   const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, rel_bias, seed_dev, salt, p_drop, scale, B, T, H);

@@ -20,7 +20,7 @@
 namespace rdx {
 
 constexpr int FE_C = 512;            // conv_dim of every layer
-constexpr int FE_TOK = 16;           // output tokens per 256-thread block (4 per wave)
+constexpr int FE_TOK = 64;           // output tokens per 256-thread block (16 per wave: the 80 weights per lane loaded once per 64 tokens)
 
 __device__ __forceinline__ float fe_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 

@@ -192,8 +192,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 template <int BM, int BN, int NPA, int NPB, int U, int EPI, int PRIO, int ABL, int X3 = 0>
 __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, int nt, int tile, int kb, int nk,
                                             int slot, int nc, int maxc) {
-  // X3 batched form: blockIdx.y selects the problem (A planes advanced by sa, C / aux_out by sc elements)
-  const int64_t yb = X3 ? (int64_t)blockIdx.y : 0;
+  // batched form (rdx_hgemm_batched, rdx_hgemm_x3): blockIdx.y selects the problem, A (and A2) advanced by sa and
+  // C / aux / aux_out by sc elements (gridDim.y == 1 otherwise)
+  const int64_t yb = (int64_t)blockIdx.y;
   using P = Plan<BM, BN, NPA, NPB>;
   constexpr int FM = P::FM, FN = P::FN, WTM = P::WTM, WTN = P::WTN, FMP = P::FMP, FNP = P::FNP;
   constexpr int NPH = P::NPH, SPK = P::SPK, S = U * SPK;
@@ -208,7 +209,7 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
 
   const int64_t lda_b = g.lda * 2, ldb_b = g.ldb * 2;
   const int rows_a = min(BM, M - m0), rows_b = min(BN, N - n0);
-  const i32x4 ra = rsrc(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)(rows_a - 1) * lda_b + (int64_t)K * 2));
+  const i32x4 ra = rsrc(g.A + yb * g.sa + (int64_t)m0 * g.lda, (uint32_t)((int64_t)(rows_a - 1) * lda_b + (int64_t)K * 2));
   const i32x4 rb = rsrc(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)(rows_b - 1) * ldb_b + (int64_t)K * 2));
   const i32x4 rnull = rsrc(g.A, 0u);
   // X3: the planes' base addresses (64-bit scalars: the descriptor of a refill is built from the pass's base, so
@@ -555,15 +556,15 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int idx = tid + it * 512, r = idx / CPR, c = (idx - r * CPR) * 8;
-      if (EPI == RDX_EPI_GELU_BWD) ux[it] = *reinterpret_cast<const uint4*>(g.aux + (int64_t)(m0 + r) * g.ldaux + n0 + c);
+      if (EPI == RDX_EPI_GELU_BWD) ux[it] = *reinterpret_cast<const uint4*>(g.aux + yb * g.sc + (int64_t)(m0 + r) * g.ldaux + n0 + c);
       qv[it] = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
     }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int idx = tid + it * 512, r = idx / CPR, c = (idx - r * CPR) * 8;
       const uint4 q = EPI == RDX_EPI_GELU_BWD ? gelu_bwd8(qv[it], ux[it]) : qv[it];
-      *reinterpret_cast<uint4*>(g.C + (int64_t)(m0 + r) * g.ldc + n0 + c) = q;
-      if (EPI == RDX_EPI_BIAS_GELU) *reinterpret_cast<uint4*>(g.aux_out + (int64_t)(m0 + r) * g.ldao + n0 + c) = gelu8(q);
+      *reinterpret_cast<uint4*>(g.C + yb * g.sc + (int64_t)(m0 + r) * g.ldc + n0 + c) = q;
+      if (EPI == RDX_EPI_BIAS_GELU) *reinterpret_cast<uint4*>(g.aux_out + yb * g.sc + (int64_t)(m0 + r) * g.ldao + n0 + c) = gelu8(q);
     }
     return;
   }
@@ -586,9 +587,9 @@ __device__ __forceinline__ void run_segment(const Args& g, char* lds, int mt, in
       if (full) *reinterpret_cast<uint2*>(dst + 4) = make_uint2(v.z, v.w);
     };
     uint4 qv = *reinterpret_cast<const uint4*>(img + r * PITCH + c * 2);
-    if (EPI == RDX_EPI_GELU_BWD) qv = gelu_bwd8(qv, ld8(g.aux + (int64_t)m * g.ldaux + n));
-    st8(g.C + (int64_t)m * g.ldc + n, qv);
-    if (EPI == RDX_EPI_BIAS_GELU) st8(g.aux_out + (int64_t)m * g.ldao + n, gelu8(qv));
+    if (EPI == RDX_EPI_GELU_BWD) qv = gelu_bwd8(qv, ld8(g.aux + yb * g.sc + (int64_t)m * g.ldaux + n));
+    st8(g.C + yb * g.sc + (int64_t)m * g.ldc + n, qv);
+    if (EPI == RDX_EPI_BIAS_GELU) st8(g.aux_out + yb * g.sc + (int64_t)m * g.ldao + n, gelu8(qv));
   }
 }
 
@@ -659,7 +660,7 @@ static int launch(Args g, hipStream_t st, int batch = 1) {
 // tile codes (BM x BN, A / B parts, ring K steps); + 100: s_setprio(1) around each MFMA segment; + 200: static
 // priority 1 for row group 1
 template <int EPI, int PRIO>
-static int dispatch(const Args& g, int tile, hipStream_t st) {
+static int dispatch(const Args& g, int tile, hipStream_t st, int batch = 1) {
   if (g.splits == 0) {                           // stream-K: the ingest-bound tiles of the N = 1024 shapes
     switch (tile) {
       case 2: return launch<128, 256, 1, 2, 3, EPI, PRIO, 0, 1>(g, st);
@@ -669,14 +670,14 @@ static int dispatch(const Args& g, int tile, hipStream_t st) {
     }
   }
   switch (tile) {
-    case 0: return launch<256, 256, 2, 2, 2, EPI, PRIO>(g, st);   // 16 slabs, 128 KB
-    case 1: return launch<256, 192, 2, 1, 2, EPI, PRIO>(g, st);   // 14 slabs
-    case 2: return launch<128, 256, 1, 2, 3, EPI, PRIO>(g, st);   // 18 slabs
-    case 3: return launch<128, 192, 2, 1, 3, EPI, PRIO>(g, st);   // 15 slabs
-    case 4: return launch<128, 128, 1, 1, 4, EPI, PRIO>(g, st);   // 16 slabs
-    case 5: return launch<256, 128, 2, 1, 3, EPI, PRIO>(g, st);   // 18 slabs
-    case 6: return launch<64, 128, 1, 1, 4, EPI, PRIO>(g, st);    // 12 slabs: twice the tiles of 128 x 128
-    case 7: return launch<64, 256, 1, 1, 3, EPI, PRIO>(g, st);    // 15 slabs
+    case 0: return launch<256, 256, 2, 2, 2, EPI, PRIO>(g, st, batch);   // 16 slabs, 128 KB
+    case 1: return launch<256, 192, 2, 1, 2, EPI, PRIO>(g, st, batch);   // 14 slabs
+    case 2: return launch<128, 256, 1, 2, 3, EPI, PRIO>(g, st, batch);   // 18 slabs
+    case 3: return launch<128, 192, 2, 1, 3, EPI, PRIO>(g, st, batch);   // 15 slabs
+    case 4: return launch<128, 128, 1, 1, 4, EPI, PRIO>(g, st, batch);   // 16 slabs
+    case 5: return launch<256, 128, 2, 1, 3, EPI, PRIO>(g, st, batch);   // 18 slabs
+    case 6: return launch<64, 128, 1, 1, 4, EPI, PRIO>(g, st, batch);    // 12 slabs: twice the tiles of 128 x 128
+    case 7: return launch<64, 256, 1, 1, 3, EPI, PRIO>(g, st, batch);    // 15 slabs
     default: return RDX_EINVAL;
   }
 }
@@ -916,4 +917,49 @@ extern "C" int rdx_hgemm_x3(const void* A, const void* A_lo, int64_t lda, int64_
   return epilogue == RDX_EPI_F32 ? hg::dispatch_x3<RDX_EPI_F32>(g, tile, batch, st)
                                  : hg::dispatch_x3<RDX_EPI_F32_GELU_SPLIT>(g, tile, batch, st);
 #endif
+}
+
+// Batched 16-bit form: `batch` problems C_y = A_y . B^T (+ bias) in one launch (blockIdx.y), A_y = A + y sa with rows
+// that may overlap (lda < K: the token-major input of a strided convolution read as its im2col matrix), C_y = C + y sc.
+// The frozen WavLM CNN's layers 1-6 (csrc/featconv.hip's token-major layout) run here.
+extern "C" int rdx_hgemm_batched(const void* A, int64_t lda, int64_t sa, const void* B, int64_t ldb, void* C,
+                                 int64_t ldc, int64_t sc, int M, int N, int K, int batch, const void* bias, int tile,
+                                 int group_m, void* stream) {
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  RDX_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0 && batch >= 1 && batch <= 65535);
+  RDX_REQUIRE(al(A, 16) && al(B, 16) && al(C, 8) && (!bias || al(bias, 8)));
+  RDX_REQUIRE(K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda > 0 && ldb >= K && N % 4 == 0 && ldc >= N &&
+              ldc % 4 == 0 && sa >= 0 && sa % 8 == 0 && sc >= 0 && sc % 4 == 0);
+  RDX_REQUIRE(((int64_t)(M - 1) * lda + K) * 2 < 0x7fffffffLL && (int64_t)N * ldb * 2 < 0x7fffffffLL);
+  RDX_REQUIRE(batch == 1 || (sc >= (int64_t)(M - 1) * ldc + N));    // the problems' outputs do not overlap
+  int bm, bn;
+  RDX_REQUIRE(tile >= 0 && tile < 8 && hg::geometry(tile, &bm, &bn));
+  RDX_REQUIRE(group_m >= 0);
+  hg::Args g;
+  g.A = (const hst*)A;
+  g.lda = lda;
+  g.B = (const hst*)B;
+  g.ldb = ldb;
+  g.C = (hst*)C;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.bias = (const hst*)bias;
+  g.aux = nullptr;
+  g.ldaux = 0;
+  g.aux_out = nullptr;
+  g.ldao = 0;
+  g.tiles_m = g.tiles_n = 0;
+  g.group_m = group_m;
+  g.splits = 1;
+  g.maxc = 1;
+  g.grid_sk = 0;
+  g.ws = nullptr;
+  g.counters = nullptr;
+  g.A2 = g.B2 = nullptr;
+  g.sa = sa;
+  g.sc = sc;
+  g.wide = al(C, 16) && ldc % 8 == 0 && sc % 8 == 0;
+  return hg::dispatch<RDX_EPI_BIAS, 0>(g, tile, as_stream(stream), batch);
 }

@@ -195,6 +195,8 @@ SIGNATURES = {
     "rdx_focal_mixup_bwd": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "rdx_hgemm_x3": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                              c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "rdx_hgemm_batched": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
+                                  c_vp, c_int, c_int, c_vp]),
     "rdx_x3_split": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_i64, c_vp]),
     "rdx_x3_ln_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                 c_i64, c_int, c_vp]),

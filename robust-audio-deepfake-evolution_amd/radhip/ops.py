@@ -1817,6 +1817,10 @@ def fe_conv_weights(layers, hd=torch.bfloat16):
     return out
 
 
+# hgemm tile of the frozen CNN's strided convolutions (rdx_hgemm_batched); -1: csrc/gemm.hip's strided GEMM (round 2-5)
+FE_HGEMM_TILE = int(os.environ.get("RADHIP_FE_TILE", "2"))
+
+
 def feature_encoder_fused(x, ops_):
     """Frozen WavLM CNN, x [B, L] fp32 -> [B, T, 512] fp32 token-major (HF WavLMFeatureEncoder, "layer" norm):
     conv0+LN+GELU in one kernel, then per layer the implicit GEMM (rdx_gemm_bf16_strided, rows of the
@@ -1838,8 +1842,16 @@ def feature_encoder_fused(x, ops_):
         To = (T - k) // s + 1
         y = torch.empty(B, To, 512, device=x.device, dtype=hd)
         with _timed("fe_conv_gemm", x, gemm_flops(B * To, 512, k * 512), shape=(B, T, k)):
-            check(Lb.rdx_gemm_bf16_strided(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To, B, To, 512,
-                                              k * 512, _p(b) if b is not None else None, _stream(x)), "gemm_bf16_strided")
+            if FE_HGEMM_TILE >= 0 and (k * 512) % 64 == 0:
+                # csrc/hgemm.hip batched over the utterances (blockIdx.y), the token-major input read as the
+                # im2col matrix (rows overlapping at stride * 512)
+                check(Lb.rdx_hgemm_batched(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To * 512, To,
+                                           512, k * 512, B, _p(b) if b is not None else None, FE_HGEMM_TILE, 0,
+                                           _stream(x)), "hgemm_batched")
+            else:
+                check(Lb.rdx_gemm_bf16_strided(_p(h), s * 512, T * 512, _p(w), w.stride(0), _p(y), 512, To, B, To,
+                                               512, k * 512, _p(b) if b is not None else None, _stream(x)),
+                      "gemm_bf16_strided")
         last = i == len(ops_) - 1
         out32 = torch.empty(B, To, 512, device=x.device, dtype=torch.float32) if last else None
         with _timed("fe_ln_gelu", x, (2.0 + (4.0 if last else 2.0)) * B * To * 512, shape=(B, To)):

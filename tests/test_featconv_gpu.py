@@ -1,4 +1,5 @@
-"""Fused frozen WavLM CNN feature encoder (csrc/featconv.hip + rdx_gemm_bf16_strided) against the module path.
+"""Fused frozen WavLM CNN feature encoder (csrc/featconv.hip + rdx_hgemm_batched; rdx_gemm_bf16_strided before round 6)
+against the module path.
 
 The WavLM-Large geometry (7 conv layers of 512 channels, kernels 10,3,3,3,3,2,2, strides 5,2,...,2,
 LayerNorm-over-channels + GELU after every conv), with seeded weights, on full-length and ragged inputs.
@@ -68,3 +69,23 @@ def test_strided_gemm_is_the_token_major_conv(K, s, T, B):
     ref = torch.nn.functional.conv1d(x.float().transpose(1, 2), w.float(), bias.float(), stride=s).transpose(1, 2)
     np.testing.assert_allclose(y.float().cpu().numpy(), ref.cpu().numpy(), rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
     assert _lib is not None
+
+
+@pytest.mark.parametrize("tile", [0, 2, 4])
+@pytest.mark.parametrize("K,s,T,B", [(3, 2, 101, 3), (2, 2, 64, 2), (3, 2, 6459, 2), (2, 2, 403, 5)])
+def test_batched_hgemm_is_the_token_major_conv(K, s, T, B, tile):
+    """rdx_hgemm_batched (csrc/hgemm.hip, blockIdx.y over the utterances, A rows overlapping at stride * C): the CNN
+    layers' product since round 6 (radhip.ops.FE_HGEMM_TILE)."""
+    from radhip._lib import check, lib
+    from radhip.ops import _p, _stream
+    C = 512
+    x = torch.from_numpy(seeded_array(f"sg{K}{T}", (B, T, C), scale=0.5)).to(torch.bfloat16).to(DEV)
+    w = torch.from_numpy(seeded_array(f"sgw{K}", (C, C, K), scale=0.05)).to(torch.bfloat16).to(DEV)
+    bias = torch.from_numpy(seeded_array(f"sgb{K}", (C,), scale=0.1)).to(torch.bfloat16).to(DEV)
+    To = (T - K) // s + 1
+    wk = w.permute(0, 2, 1).reshape(C, K * C).contiguous()
+    y = torch.full((B, To, C), float("nan"), device=DEV, dtype=torch.bfloat16)
+    check(lib().rdx_hgemm_batched(_p(x), s * C, T * C, _p(wk), K * C, _p(y), C, To * C, To, C, K * C, B, _p(bias), tile,
+                                  0, _stream(x)), "hgemm_batched")
+    ref = torch.nn.functional.conv1d(x.float().transpose(1, 2), w.float(), bias.float(), stride=s).transpose(1, 2)
+    np.testing.assert_allclose(y.float().cpu().numpy(), ref.cpu().numpy(), rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
