@@ -1817,8 +1817,10 @@ def fe_conv_weights(layers, hd=torch.bfloat16):
     return out
 
 
-# hgemm tile of the frozen CNN's strided convolutions (rdx_hgemm_batched); -1: csrc/gemm.hip's strided GEMM (round 2-5)
-FE_HGEMM_TILE = int(os.environ.get("RADHIP_FE_TILE", "2"))
+# hgemm tile of the frozen CNN's strided convolutions (rdx_hgemm_batched); -1: csrc/gemm.hip's strided GEMM (round 2-5).
+# Whole CNN at the window's 32 x 64600 clean batch (tools/bench_fe.py, profiles/r06_bench_fe.jsonl, fp16 / bf16 ms):
+# gemm.hip 1.69 / 1.53, hgemm 256 x 256 1.25 / 1.20, 128 x 256 1.29 / 1.24, 128 x 128 1.47 / 1.42
+FE_HGEMM_TILE = int(os.environ.get("RADHIP_FE_TILE", "0"))
 
 
 def feature_encoder_fused(x, ops_):

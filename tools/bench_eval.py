@@ -1,7 +1,8 @@
 """Eval (scoring) throughput of the Phase-6 model (BASELINE configs 3 and 5: the ASVspoof 2019-LA / 2021-DF score
 passes of main.py --eval), synthetic utterances of the scoring length (64 600 samples), batch 32 as the reference's
 test loader: the reference's fp32 forward, and the bf16-autocast forward that runs the hand-written HIP path (fused
-WavLM encoder layers, attention, SincNet block 0 / sconv). Random-init weights (no checkpoint); the score is
+WavLM encoder layers, attention, SincNet block 0 / sconv), and x3: the fp32 forward with the WavLM stream on the
+split-precision kernels (radhip/wavlm_x3.py). Random-init weights (no checkpoint); the score is
 logits[:, 1] exactly as radhip.infer._scores takes it. Prints one JSON line: utt/s and ms/utt per precision, and
 the bf16 scores' deviation from the fp32 scores of the same weights and inputs.
 
@@ -24,7 +25,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--batches", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--modes", default="fp32,x3,bf16,fp16", help="comma list of fp32 / x3 / bf16 / fp16")
     a = ap.parse_args()
+    modes = {"fp32": None, "x3": "x3", "bf16": torch.bfloat16, "fp16": torch.float16}
     from radhip.build import apply_lora_to_wavlm, get_model, load_config
     from radhip.infer import _scores
     dev = torch.device("cuda", 0)
@@ -38,7 +41,8 @@ def main():
            "batches": a.batches}
     scores = {}
     with torch.no_grad():
-        for name, amp in (("fp32", None), ("bf16", torch.bfloat16)):
+        for name in a.modes.split(","):
+            amp = modes[name]
             for i in range(a.warmup):
                 _scores(model, xs[i % len(xs)], None, amp)
             torch.cuda.synchronize()
@@ -50,11 +54,15 @@ def main():
             scores[name] = torch.cat(out).double()
             res[name] = {"utt_s": round(n / dt, 2), "ms_per_utt": round(dt / n * 1e3, 3),
                          "ms_per_batch": round(dt / a.batches * 1e3, 2)}
-    d = (scores["bf16"] - scores["fp32"]).abs()
-    res["bf16_vs_fp32"] = {"max_abs_score_diff": float(d.max()), "mean_abs_score_diff": float(d.mean()),
-                           "fp32_score_std": float(scores["fp32"].std()),
-                           "rank_corr": float(np.corrcoef(scores["fp32"].cpu().numpy().argsort().argsort(),
-                                                          scores["bf16"].cpu().numpy().argsort().argsort())[0, 1])}
+    for name in scores:
+        if name == "fp32" or "fp32" not in scores:
+            continue
+        d = (scores[name] - scores["fp32"]).abs()
+        res[name + "_vs_fp32"] = {
+            "max_abs_score_diff": float(d.max()), "mean_abs_score_diff": float(d.mean()),
+            "fp32_score_std": float(scores["fp32"].std()),
+            "rank_corr": float(np.corrcoef(scores["fp32"].cpu().numpy().argsort().argsort(),
+                                           scores[name].cpu().numpy().argsort().argsort())[0, 1])}
     res["reference_published"] = "~40 ms per utterance at batch 32 (reference README.md:101-105; other hardware)"
     print(json.dumps(res), flush=True)
 

@@ -3,6 +3,8 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-x3c}
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_graph_ws_gpu.py tests/test_x3_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
 timeout -k 10 400 python -u tools/bench_eval.py --batches 6 --modes x3 > $O/eval.json 2> $O/eval.err
 cat $O/eval.json
 RADHIP_PROBE_NO_SINC=1 timeout -k 10 400 python -u tools/bench_eval.py --batches 6 --modes x3 > $O/eval_nosinc.json 2> $O/eval_nosinc.err

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--micro", type=int, default=8)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--accum", type=int, default=4, help="micro-batches per step (with --before)")
     ap.add_argument("--before", default=None,
                     help="end the window at the first launch whose name contains this (bench.py: 'ts_acc_kernel', "
                          "the first clock stamp of the kernel-timing replay, so the window is the timed region)")
@@ -55,6 +56,13 @@ def main():
             raise SystemExit(f"no launch named {a.before}")
         rows = rows[:first]
     marks = [i for i, r in enumerate(rows) if "pad_mixup_kernel" in r[2]]
+    if a.before:
+        # the kernel-timing replay's first step stages its micro-batches (their pad_mixup launches) before its
+        # first stamped graph: the timed region ends at the first of those
+        if len(marks) < a.accum:
+            raise SystemExit("too few micro-batch markers")
+        rows = rows[:marks[-a.accum]]
+        marks = marks[:-a.accum]
     if len(marks) < a.micro + 1:
         raise SystemExit(f"only {len(marks)} micro-batch markers")
     lo = marks[-a.micro - 1] if len(marks) > a.micro else marks[0]
