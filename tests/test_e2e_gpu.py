@@ -48,6 +48,17 @@ GRAD_REL_BF16 = {"reference": {"layer_weights": 0.09, "feature_projection": 0.05
                             "fusion": 0.16, "backbone": 0.18, "head": 0.12}}
 
 
+PROFILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+
+
+def _record(name, obj):
+    """Keep a test's error table under profiles/ (the suite run's record of the measured ratios)."""
+    import json
+    os.makedirs(PROFILES, exist_ok=True)
+    with open(os.path.join(PROFILES, name), "w") as f:
+        json.dump(obj, f, indent=1)
+
+
 FLOOR_RATIOS = {}      # {amp: product error / fp16 reference-floor error}, filled by the reference-mode runs
 _FLOOR = {}            # the floor itself (logits max abs error, per-group gradient rel L2), computed once
 FLOOR_MAX_RATIO_FP16 = 2.0
@@ -301,6 +312,12 @@ def test_bench_path_window_vs_fp64_oracle(lora_mode, amp):
     print(f"[e2e {lora_mode} {amp}] clean loss product {losses[0]:.6f} (replay 2: {losses[1]:.6f}) "
           f"oracle {o_loss:.6f}")
     print(f"[e2e {lora_mode} {amp}] grad rel L2: " + ", ".join(f"{g} {e:.3e}" for g, e in sorted(errs.items())))
+    rec = {"eval_logits_16bit_max_abs_err": e16, "eval_logits_fp32_max_abs_err": e32, "clean_loss": losses[0],
+           "oracle_loss": o_loss, "grad_rel_l2": errs}
+    if lora_mode == "reference":
+        rec["fp16_floor"] = {"logits": _FLOOR["floor"][0], "grad_rel_l2": _FLOOR["floor"][1]}
+        rec["ratio_to_floor"] = FLOOR_RATIOS[amp]
+    _record(f"r06_e2e_{lora_mode}_{amp}.json", rec)
     assert e32 < 1e-3, e32
     assert e16 < LOGIT_ATOL_BF16, e16
     assert abs(losses[0] - o_loss) < LOSS_RTOL_BF16 * abs(o_loss), (losses[0], o_loss)
@@ -412,6 +429,7 @@ def test_bench_config_fp16_k4_window_vs_fp64_oracle():
     print(f"\n[e2e fp16 K=4] grad rel L2 product: " + ", ".join(f"{g} {e:.3e}" for g, e in sorted(errs.items())))
     print(f"[e2e fp16 K=4] reference floor: " + ", ".join(f"{g} {e:.3e}" for g, e in sorted(floor.items())))
     print(f"[e2e fp16 K=4] product / floor: " + ", ".join(f"{g} {r:.2f}x" for g, r in sorted(ratios.items())))
+    _record("r06_e2e_fp16_k4_window.json", {"grad_rel_l2": errs, "fp16_floor": floor, "ratio_to_floor": ratios})
     assert set(errs) == set(GRAD_REL_BF16["reference"]), errs
     for g, r in ratios.items():
         assert r <= FLOOR_MAX_RATIO_FP16, (g, r, ratios)
