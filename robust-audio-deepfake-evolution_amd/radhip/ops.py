@@ -1481,12 +1481,17 @@ WGEMM_POLICY_T6 = {
     "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
             "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
 }
+# B = 32 long-K shapes (ffn2, d_ffn1, d_qkv: N = 1024 at K = 4096 / 3072) on 256 x 128 tiles (code 5) instead of
+# 128 x 128: in-step A/B 6 of 6 interleaved rounds faster, 485.3 / 486.9 / 485.1 / 484.9 / 484.5 / 485.5 vs
+# 484.9 / 485.2 / 484.5 / 484.9 / 484.1 / 483.1 utt/s (tools/gpu_policy_ab.sh, profiles/r06_policy_ab.jsonl); the
+# other variants tried there (B = 8 ffn1 on code 7, long-K on 64 x 128, qkv on code 7) were 1.5-4 % slower
 WGEMM_POLICY = {
     "b8": {"qkv": ("hg", 3, 1, 4), "out": ("hg", 6, 1, 4), "d_out": ("hg", 6, 1, 4), "ffn1": ("hg", 202, 1, 0),
            "d_ffn2": ("hg", 202, 1, 0), "ffn2": ("hg", 4, 2, 4), "d_ffn1": ("hg", 4, 2, 4), "d_qkv": ("hg", 4, 2, 4)},
     "b32": {"qkv": ("hg", 1, 1, 4), "out": ("hg", 2, 1, 4), "d_out": ("hg", 2, 1, 4), "ffn1": ("hg", 0, 1, 4),
-            "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 2, 1, 4), "d_ffn1": ("hg", 2, 1, 4), "d_qkv": ("hg", 2, 1, 4)},
+            "d_ffn2": ("hg", 0, 1, 4), "ffn2": ("hg", 5, 1, 4), "d_ffn1": ("hg", 5, 1, 4), "d_qkv": ("hg", 5, 1, 4)},
 }
+WGEMM_POLICY_R6A = {"b8": WGEMM_POLICY["b8"], "b32": WGEMM_POLICY_R5G["b32"]}   # the default before that A/B
 
 
 def wgemm_policy(name, M, N, K):
@@ -1499,7 +1504,7 @@ def wgemm_policy(name, M, N, K):
         return None
     table = WGEMM_POLICY
     env = os.environ.get("RADHIP_WGEMM_POLICY")
-    if env:     # a JSON table, or the name of one of this module's tables (R4, R5A, R5G)
+    if env:     # a JSON table, or the name of one of this module's tables (R4, R5A, R5G, T6, R6A)
         import json
         table = json.loads(env) if env.lstrip().startswith("{") else globals()["WGEMM_POLICY_" + env.upper()]
     ent = table.get("b8" if M <= 2048 else "b32", {}).get(name)
