@@ -34,7 +34,7 @@ constexpr int BX_IR = 136;      // out1 image rows: positions q0 - 1 .. q0 + 128
 constexpr int BX_XW = 132;      // staged x positions q0 - 2 .. q0 + 129
 constexpr int BX_SP = 36;       // fp32 pitch of the pre-pool row (32 channels + 4: spreads the row stores)
 constexpr int BX_IMG = BX_IR * 64;
-constexpr int BX_LDS = 192 * 64 + 3 * BX_IMG + 4 * BX_XW * 4 + 128 * BX_SP * 4 + 32 * 16;
+constexpr int BX_LDS = 3 * BX_IMG + 4 * BX_XW * 4 + 128 * BX_SP * 4 + 32 * 16;   // conv2 weights: registers
 
 __device__ __forceinline__ float bx_selu(float u) {
   return BX_SELU_SCALE * (u > 0.f ? u : BX_SELU_ALPHA * (__expf(u) - 1.0f));
@@ -99,8 +99,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   long long pf_t = clock64();
 #endif
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* ws = lds;                                           // conv2 weights: rows tap * 32 + co
-  char* os = ws + 192 * 64;                                 // out1 ring: 3 slots
+  char* os = lds;                                           // out1 ring: 3 slots
   float* xr = reinterpret_cast<float*>(os + 3 * BX_IMG);    // x ring: 4 rows of BX_XW
   float* ss = xr + 4 * BX_XW;                               // s = a + idn + bias of the current row
   float4* prec = reinterpret_cast<float4*>(ss + 128 * BX_SP);   // [32] {wd[co][0..2], bias[co]}
@@ -110,10 +109,14 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
   const int H = a.H, W = a.W;
   const int h0 = blockIdx.z * a.rows_per, h1 = min(H, h0 + a.rows_per);
   if (h0 >= h1) return;
-  for (int i = tid; i < 192 * 4; i += BX_T) {
-    const int row = i >> 2, ch = i & 3;
-    *reinterpret_cast<uint4*>(ws + bx_img(row, ch)) = *reinterpret_cast<const uint4*>(a.w2 + row * BX_C + ch * 8);
-  }
+  // conv2's A operand (the weights, rows co = lane & 31) for all 6 taps x 2 K steps, held in registers for the whole
+  // walk (48 VGPRs): read from LDS per row they were half of the conv2 phase's LDS traffic (12 of 24 KB per wave)
+  hx8 wreg[6][2];
+#pragma unroll
+  for (int t = 0; t < 6; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      wreg[t][s] = *reinterpret_cast<const hx8*>(a.w2 + (t * BX_C + (tid & 31)) * BX_C + (2 * s + ((tid >> 5) & 1)) * 8);
   if (tid < 32) prec[tid] = make_float4(a.wd[tid * 3], a.wd[tid * 3 + 1], a.wd[tid * 3 + 2], a.bias[tid]);
   // this thread's out1 channels: 8 * g8 .. + 7 (its items it = tid + 256 k all have it & 3 == tid & 3)
   const int g8 = tid & 3;
@@ -213,8 +216,7 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_fwd_kernel(BxFwdArgs a) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const hx8 xf = *reinterpret_cast<const hx8*>(xk + bx_img(pw + kw, 2 * s + hh));
-          const hx8 wf = *reinterpret_cast<const hx8*>(ws + bx_img((kh * 3 + kw) * BX_C + r, 2 * s + hh));
-          acc = mfma32x32x16(wf, xf, acc);   // Y^T: rows co, columns positions
+          acc = mfma32x32x16(wreg[kh * 3 + kw][s], xf, acc);   // Y^T: rows co, columns positions
         }
     }
     BXF_STAMP(0);

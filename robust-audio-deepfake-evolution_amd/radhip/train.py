@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib, ops
 from .augment import CODEC_RATES, draw_rawboost
-from .ops import fgm_attack, pad_mixup, rawboost_batch, resample_batch, resample_kernel
+from .ops import add_many, fgm_attack, pad_mixup, rawboost_batch, resample_batch, resample_kernel
 from .wavlm import compute_time_mask
 
 MAX_LEN = 64600
@@ -116,9 +116,14 @@ class FGM:
             self.backup[n] = b
 
     def restore(self):
-        for n, p in self.model.named_parameters():
-            if p.requires_grad and self.emb_name in n and n in self.backup:
-                p.data.copy_(self.backup[n])
+        pairs = [(p.data, self.backup[n]) for n, p in self.model.named_parameters()
+                 if p.requires_grad and self.emb_name in n and n in self.backup]
+        if pairs and all(d.is_cuda and d.dtype == torch.float32 and d.is_contiguous() and b.is_contiguous()
+                         for d, b in pairs):
+            add_many([d for d, _ in pairs], [b for _, b in pairs], copy=True)   # one launch for every target
+        else:
+            for d, b in pairs:
+                d.copy_(b)
         self.backup = {}
 
 

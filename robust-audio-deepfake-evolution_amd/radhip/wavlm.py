@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import wavlm_fused, wavlm_x3
+from . import featproj, wavlm_fused, wavlm_x3
 from .ops import HALF, GatedAttention, PosConv, fe_conv_weights, feature_encoder_fused, half_dtype, posconv_weights
 
 # microsoft/wavlm-large architecture (published config.json; dropout / SpecAugment values are
@@ -498,6 +498,8 @@ class WavLMEncoderModel(nn.Module):
         c = self.config
         self.feature_extractor = FeatureEncoder(c)
         self.feature_projection = FeatureProjection(c)
+        for p in self.feature_projection.parameters():   # radhip/featproj.py accumulates their gradients into .grad
+            p._radhip_direct_grad = True
         if c.mask_time_prob > 0 or c.mask_feature_prob > 0:
             self.masked_spec_embed = nn.Parameter(torch.Tensor(c.hidden_size).uniform_())
         self.encoder = Encoder(c)
@@ -538,7 +540,9 @@ class WavLMEncoderModel(nn.Module):
         else:
             feats = self.feature_extractor(x)
         feats = feats.transpose(1, 2)
-        if self.fp_groups is not None:
+        if featproj.eligible(self.feature_projection, feats, self.fp_groups):
+            h = featproj.feature_projection(self.feature_projection, feats, self.fp_groups)
+        elif self.fp_groups is not None:
             fp = self.feature_projection
             K = len(self.fp_groups)
             parts = []

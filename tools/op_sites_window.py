@@ -39,7 +39,11 @@ class Sites(TorchDispatchMode):
             return out
         st = [f for f in traceback.extract_stack()[:-1]
               if ("/radhip/" in f.filename or "/models/" in f.filename) and "op_sites" not in f.filename]
-        loc = f"{st[-1].filename.split('/')[-1]}:{st[-1].lineno}" if st else "<autograd>"
+        if st:
+            loc = f"{st[-1].filename.split('/')[-1]}:{st[-1].lineno}"
+        else:   # issued by the autograd engine: name the backward node running it
+            node = torch._C._current_autograd_node()
+            loc = f"<autograd {node.name()}>" if node is not None else "<autograd>"
         shp = tuple(t0.shape) if t0 is not None else ()
         dts = str(t0.dtype)[6:] if t0 is not None else ""
         self.c[(name, dts, shp, loc)] += 1
