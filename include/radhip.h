@@ -372,7 +372,9 @@ int rdx_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* k
  * seed_dev disables one.
  * rdx_wl_ln1_fwd: x1 = LN1(h) -> bf16 x1[:, 0:E] (row stride ldx); gate[m, h] = ga (gb c_h - 1) + 2 with
  *   (ga, gb) = sigmoid of the 4-sums of wg [8, 64] x1_head + bg (gconst = c [H]); with lora_aq/lora_av
- *   [r, E] (r = 8) also x1[:, E + k] = sum_e A_k[e] drop_k(x1)[e] (k < r: q adapter, else v); mean/rstd [M] saved.
+ *   [r, E] (r = 8; in the library's 16-bit storage type, the value autocast's cast gives lora_A's fp32 weight;
+ *   16-byte aligned) also x1[:, E + k] = sum_e A_k[e] drop_k(x1)[e] (k < r: q adapter, else v); mean/rstd [M]
+ *   saved. The LN1 backward entries take lora_aq/lora_av the same way.
  * rdx_wl_add_ln_fwd: h2 = h + drop(delta) (fp32 out), x = LN(h2) bf16, mean/rstd saved.
  * rdx_wl_residual: out = h + drop(delta) over n elements.  rdx_wl_dropout_bwd: out = drop(g) in bf16.
  * rdx_wl_gelu: mode 0 out = gelu(u) (erf form); mode 1 out = dy * gelu'(u).
@@ -385,7 +387,7 @@ int rdx_dropout_mask(const int64_t* seed_dev, int salt, float p_drop, uint8_t* k
  * rdx_wl_lora_pack: for every layer l, wext[l] [3E, ldw] bf16 columns E..E+2r <- scale * lora_B
  *   (q rows 0..E-1, v rows 2E..3E-1); bq, bv, wext are DEVICE arrays of nl pointers. */
 int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float eps, const float* wg,
-                   const float* bg, const float* gconst, const float* lora_aq, const float* lora_av, int r,
+                   const float* bg, const float* gconst, const void* lora_aq, const void* lora_av, int r,
                    const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean,
                    float* rstd, int64_t M, int E, void* stream);
 int rdx_wl_add_ln_fwd(const float* h, const void* delta, const int64_t* seed_dev, int salt, float p, float* h2,
@@ -401,14 +403,14 @@ int rdx_wl_ln_bwd(const void* dx, int64_t ldd, const float* h, const float* mean
                   void* ddrop, int64_t M, int E, void* stream);
 int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
                    const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
-                   const float* gconst, const float* lora_aq, const float* lora_av, int r,
+                   const float* gconst, const void* lora_aq, const void* lora_av, int r,
                    const int64_t* seed_dev, int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
                    void* stream);
 /* rdx_wl_res_ln1_fwd: rdx_wl_ln1_fwd of h = h2 + drop(delta) (the residual of the previous layer, computed here
  *   and written to hout): one pass instead of rdx_wl_residual then rdx_wl_ln1_fwd. */
 int rdx_wl_res_ln1_fwd(const float* h2, const void* delta, int salt_res, float p_res, float* hout,
                        const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
-                       const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                       const float* gconst, const void* lora_aq, const void* lora_av, int r, const int64_t* seed_dev,
                        int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean,
                        float* rstd, int64_t M, int E, void* stream);
 /* rdx_wl_ln1_bwd_ex: rdx_wl_ln1_bwd plus (state_grad, state_weight non-null) dh += state_weight[0] * state_grad,
@@ -417,7 +419,7 @@ int rdx_wl_res_ln1_fwd(const float* h2, const void* delta, int salt_res, float p
  *   layer's hidden dropout (salt_prev, p_prev): that layer's rdx_wl_dropout_bwd, fused. */
 int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
                       const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
-                      const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                      const float* gconst, const void* lora_aq, const void* lora_av, int r, const int64_t* seed_dev,
                       int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd,
                       const float* state_grad, const float* state_weight, int salt_prev, float p_prev,
                       void* ddrop_prev, int64_t M, int E, void* stream);

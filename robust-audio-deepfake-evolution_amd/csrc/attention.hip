@@ -208,14 +208,12 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
   const int T = a.T, H = a.H, nt = (T + AT_TILE - 1) / AT_TILE, tp = nt * AT_TILE;
   const int head = blockIdx.y, b = blockIdx.z;
   const int64_t col0 = (int64_t)head * AT_DH;
+  // images sized for AT_MAXNT tiles whatever T (the host allocates at_fwd_lds): every staged chunk has a slot, so the
+  // stores below are unconditional and the compiler keeps all the loads ahead of the first wait
   char* Ks = at_lds;
-  char* Vs = at_lds + nt * AT_TILE_BYTES;
-  float* tab = reinterpret_cast<float*>(at_lds + 2 * nt * AT_TILE_BYTES);
-  float* mrg = tab + 2 * tp;                  // [AT_WAVES][64][AT_MERGE_STRIDE]
-  stage_image(Ks, a.k, a.ldk, b, T, col0, nt, at_fwd_threads<kSplit>());
-  stage_image(Vs, a.v, a.ldv, b, T, col0, nt, at_fwd_threads<kSplit>());
-  stage_rel(tab, a.rel, head, T, tp);
-  __syncthreads();
+  char* Vs = at_lds + AT_MAXNT * AT_TILE_BYTES;
+  float* tab = reinterpret_cast<float*>(at_lds + 2 * AT_MAXNT * AT_TILE_BYTES);
+  float* mrg = tab + 2 * AT_MAXNT * AT_TILE;  // [AT_WAVES][64][AT_MERGE_STRIDE]
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
   const int qw = w % AT_WAVES, half = w / AT_WAVES;
   const int qb = blockIdx.x * AT_WAVES + qw;
@@ -225,14 +223,66 @@ __global__ __launch_bounds__(at_fwd_threads<kSplit>()) void attn_fwd_kernel(Attn
   const int qi = qb * AT_TILE + r;
   const bool qvalid = active && qi < T;
   const int qc = qvalid ? qi : T - 1;
+  // Every global load of the workgroup in flight at once before the first wait: the K / V images (PER 16-byte
+  // chunks of each per thread, from row-clamped addresses, zeroed past T), the relative-bias row, this lane's Q
+  // fragments and gate. A staging loop that stored each chunk as it arrived waited out one load round trip per
+  // iteration (7 at T = 201 with 512 threads, 14 with 256).
+  constexpr int NTHR = at_fwd_threads<kSplit>();
+  constexpr int PER = AT_MAXNT * AT_TILE * 8 / NTHR;
+  hx8 kc[PER], vc[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = threadIdx.x + j * NTHR, row = i >> 3, ch = i & 7;
+    const int64_t o = (int64_t)b * T + (row < T ? row : T - 1);
+    kc[j] = *reinterpret_cast<const hx8*>(a.k + o * a.ldk + col0 + 8 * ch);
+    vc[j] = *reinterpret_cast<const hx8*>(a.v + o * a.ldv + col0 + 8 * ch);
+  }
+  constexpr int TPER = (2 * AT_MAXNT * AT_TILE + NTHR - 1) / NTHR;
+  float tv[TPER];
+  {
+    const int pad = tp - T;
+#pragma unroll
+    for (int j = 0; j < TPER; ++j) {
+      const int i = threadIdx.x + j * NTHR, d = i - pad - (T - 1);
+      const int dc = d > -T ? (d < T ? d : T - 1) : 1 - T;
+      tv[j] = a.rel[(int64_t)head * (2 * T - 1) + dc + T - 1];
+      tv[j] = (d > -T && d < T) ? tv[j] : 0.f;
+    }
+  }
+  hx8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const hx8*>(a.q + ((int64_t)b * T + qc) * a.ldq + col0 + 16 * s + 8 * hh);
+  const float graw = a.gate[((int64_t)b * T + qc) * H + head];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = threadIdx.x + j * NTHR, row = i >> 3, ch = i & 7;
+    hx8 kv = kc[j], vv = vc[j];
+    const bool z = row >= T;   // rows past T read as zeros
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      kv[e] = z ? (hel)0.f : kv[e];
+      vv[e] = z ? (hel)0.f : vv[e];
+    }
+    *reinterpret_cast<hx8*>(Ks + img_off(row, ch)) = kv;
+    *reinterpret_cast<hx8*>(Vs + img_off(row, ch)) = vv;
+  }
+#pragma unroll
+  for (int j = 0; j < TPER; ++j) {
+    const int i = threadIdx.x + j * NTHR;
+    if (TPER * NTHR == 2 * AT_MAXNT * AT_TILE || i < 2 * AT_MAXNT * AT_TILE) tab[i] = tv[j];
+  }
+  __syncthreads();
   float m = -INFINITY, l = 0.f;
   f32x16 oacc[2] = {zero16(), zero16()};
   const int64_t bh = (int64_t)b * H + head;
   if (active) {
-    hx8 qf[4];
+    if (!qvalid) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = load8(a.q + ((int64_t)b * T + qc) * a.ldq + col0 + 16 * s + 8 * hh, qvalid);
-    const float g2 = a.gate[((int64_t)b * T + qc) * H + head] * kLog2e;   // base-2 domain: exp2 of log2e-scaled scores
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[s][e] = (hel)0.f;
+    }
+    const float g2 = graw * kLog2e;   // base-2 domain: exp2 of log2e-scaled scores
     const float scale2 = a.scale * kLog2e;
     const uint64_t seed = kDrop ? attn_seed(a.seed_dev, a.salt) : 0;
     const DropKey32 k32 = drop_key32(seed);
@@ -1011,7 +1061,7 @@ extern "C" int rdx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t l
   const AttnArgs a = make_args(q, ldq, k, ldk, v, ldv, gate, rel_bias, seed_dev, salt, p_drop, scale, B, T, H);
   const int nt = (T + AT_TILE - 1) / AT_TILE;
   const dim3 grid((nt + AT_WAVES - 1) / AT_WAVES, H, B);
-  const size_t lds = 2 * (size_t)nt * AT_TILE_BYTES + rel_bytes(T);
+  const size_t lds = 2 * (size_t)AT_MAXNT * AT_TILE_BYTES + 2 * AT_MAXNT * AT_TILE * sizeof(float);   // see the kernel
   hipStream_t st = as_stream(stream);
   hst* ob = (hst*)o;
   // key-split kernel while the unsplit grid is at most 2 workgroups per CU (one wave per SIMD each)

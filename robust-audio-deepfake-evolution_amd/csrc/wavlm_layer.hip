@@ -173,8 +173,8 @@ struct Ln1Args {
   const float* beta;
   float eps;
   GateW g;
-  const float* Aq;  // [r, E] lora_A (q), null without LoRA
-  const float* Av;  // [r, E] lora_A (v)
+  const hst* Aq;    // [r, E] lora_A (q) in the 16-bit storage type (autocast's cast), null without LoRA
+  const hst* Av;    // [r, E] lora_A (v)
   Drop dq, dv;      // LoRA dropouts (q, v)
   hst* x1;  // [M, ldx]: LN1 output in [0, E), LoRA down-projection in [E, E + 2r)
   int64_t ldx;
@@ -190,24 +190,23 @@ struct Ln1Args {
   float* hout;
 };
 
-// LoRA-A of both adapters staged once per workgroup of WL_LN1_ROWS row-waves (4): [2r][E] bf16 (the cast autocast
-// applies to lora_A's weight), 32 KB. A row-wave reading the fp32 A from L2 itself moved 64 KB per token row
-// and left these kernels L2-bound (26 us of the 47 us forward at B = 32).
+// LoRA-A of both adapters staged once per workgroup of WL_LN1_ROWS row-waves (4): [2r][E] 16-bit (the cast autocast
+// applies to lora_A's weight, made once per pass by the caller), 32 KB copied with 16-byte loads. A row-wave reading
+// the fp32 A from L2 itself moved 64 KB per token row and left these kernels L2-bound (26 us of the 47 us forward
+// at B = 32); staging it from fp32 with the conversion here still read 64 KB per workgroup.
 #ifndef WL_LN1_ROWS_DEF
 #define WL_LN1_ROWS_DEF 4   // measured: 4 rows beat 8 and 2 at both pass sizes (tools/bench_wl.py)
 #endif
 constexpr int WL_LN1_ROWS = WL_LN1_ROWS_DEF;
 constexpr int WL_LN1_THREADS = WL_LN1_ROWS * RDX_WAVE;
 
-__device__ __forceinline__ void stage_lora_a(hst* sA, const float* Aq, const float* Av) {
-  // WL_R2 * WL_E floats over WL_LN1_THREADS threads, 4 float4 per pass
-  constexpr int kN = WL_R2 * WL_E / 4;
+__device__ __forceinline__ void stage_lora_a(hst* sA, const hst* Aq, const hst* Av) {
+  // WL_R2 * WL_E 16-bit values over WL_LN1_THREADS threads, 8 per 16-byte load
+  constexpr int kN = WL_R2 * WL_E / 8;
   for (int i = threadIdx.x; i < kN; i += WL_LN1_THREADS) {
-    const int k = (4 * i) / WL_E, e = (4 * i) % WL_E;
-    const float* src = k < WL_R2 / 2 ? Aq + (int64_t)k * WL_E + e : Av + (int64_t)(k - WL_R2 / 2) * WL_E + e;
-    const float4 t = *reinterpret_cast<const float4*>(src);
-    const uint32_t w0 = hbits(t.x) | (hbits(t.y) << 16), w1 = hbits(t.z) | (hbits(t.w) << 16);
-    *reinterpret_cast<uint2*>(sA + 4 * i) = make_uint2(w0, w1);
+    const int k = (8 * i) / WL_E, e = (8 * i) % WL_E;
+    const hst* src = k < WL_R2 / 2 ? Aq + (int64_t)k * WL_E + e : Av + (int64_t)(k - WL_R2 / 2) * WL_E + e;
+    *reinterpret_cast<uint4*>(sA + 8 * i) = *reinterpret_cast<const uint4*>(src);
   }
 }
 // 16 consecutive bf16 of an LDS row as fp32
@@ -473,8 +472,8 @@ struct Ln1BwdArgs {
   const float* gamma;
   const float* beta;
   GateW g;
-  const float* Aq;  // [r, E] or null
-  const float* Av;
+  const hst* Aq;    // [r, E] 16-bit or null
+  const hst* Av;
   Drop dq, dv;
   const float* dres;  // [M, E]
   float* dh;
@@ -762,14 +761,16 @@ static int ln1_fwd_launch(const Ln1Args& a, bool lora, void* stream) {
 extern "C" {
 
 int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
-                   const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                   const float* gconst, const void* lora_aq, const void* lora_av, int r, const int64_t* seed_dev,
                    int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean, float* rstd, int64_t M, int E,
                    void* stream) {
   RDX_REQUIRE(h && gamma && beta && wg && bg && gconst && x1 && gate && mean && rstd && M > 0);
   const bool lora = lora_aq != nullptr;
   RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
+  RDX_REQUIRE(!lora || ((((uintptr_t)lora_aq | (uintptr_t)lora_av) & 15) == 0));
   RDX_REQUIRE(ldx % 8 == 0);
-  Ln1Args a{h, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
+  Ln1Args a{h, gamma, beta, eps, GateW{wg, bg, gconst}, reinterpret_cast<const hst*>(lora_aq),
+            reinterpret_cast<const hst*>(lora_av), mk_drop(seed_dev, salt_q, p_lora),
             mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<hst*>(x1), ldx, gate, mean, rstd, M,
             nullptr, nullptr, mk_drop(nullptr, 0, 0.f), nullptr};
   return ln1_fwd_launch(a, lora, stream);
@@ -777,14 +778,16 @@ int rdx_wl_ln1_fwd(const float* h, const float* gamma, const float* beta, float 
 
 int rdx_wl_res_ln1_fwd(const float* h2, const void* delta, int salt_res, float p_res, float* hout,
                        const float* gamma, const float* beta, float eps, const float* wg, const float* bg,
-                       const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                       const float* gconst, const void* lora_aq, const void* lora_av, int r, const int64_t* seed_dev,
                        int salt_q, int salt_v, float p_lora, void* x1, int64_t ldx, float* gate, float* mean,
                        float* rstd, int64_t M, int E, void* stream) {
   RDX_REQUIRE(h2 && delta && hout && gamma && beta && wg && bg && gconst && x1 && gate && mean && rstd && M > 0);
   const bool lora = lora_aq != nullptr;
   RDX_REQUIRE(E == WL_E && (!lora || (2 * r == WL_R2 && lora_av)) && ldx >= E + (lora ? 2 * r : 0));
+  RDX_REQUIRE(!lora || ((((uintptr_t)lora_aq | (uintptr_t)lora_av) & 15) == 0));
   RDX_REQUIRE(ldx % 8 == 0);
-  Ln1Args a{nullptr, gamma, beta, eps, GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora),
+  Ln1Args a{nullptr, gamma, beta, eps, GateW{wg, bg, gconst}, reinterpret_cast<const hst*>(lora_aq),
+            reinterpret_cast<const hst*>(lora_av), mk_drop(seed_dev, salt_q, p_lora),
             mk_drop(seed_dev, salt_v, p_lora), reinterpret_cast<hst*>(x1), ldx, gate, mean, rstd, M,
             h2, reinterpret_cast<const hst*>(delta), mk_drop(seed_dev, salt_res, p_res), hout};
   return ln1_fwd_launch(a, lora, stream);
@@ -846,7 +849,7 @@ int rdx_wl_ln_bwd(const void* dx, int64_t ldd, const float* h, const float* mean
 
 int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
                       const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
-                      const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                      const float* gconst, const void* lora_aq, const void* lora_av, int r, const int64_t* seed_dev,
                       int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd,
                       const float* state_grad, const float* state_weight, int salt_prev, float p_prev,
                       void* ddrop_prev, int64_t M, int E, void* stream) {
@@ -854,8 +857,10 @@ int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const fl
   RDX_REQUIRE((state_grad == nullptr) == (state_weight == nullptr));
   const bool lora = lora_aq != nullptr;
   RDX_REQUIRE(E == WL_E && ldx % 8 == 0 && (!lora || (2 * r == WL_R2 && lora_av && ldx >= E + 2 * r)));
+  RDX_REQUIRE(!lora || ((((uintptr_t)lora_aq | (uintptr_t)lora_av) & 15) == 0));
   Ln1BwdArgs a{reinterpret_cast<const hst*>(dx1), ldx, dgate, h, mean, rstd, gamma, beta,
-               GateW{wg, bg, gconst}, lora_aq, lora_av, mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
+               GateW{wg, bg, gconst}, reinterpret_cast<const hst*>(lora_aq), reinterpret_cast<const hst*>(lora_av),
+               mk_drop(seed_dev, salt_q, p_lora), mk_drop(seed_dev, salt_v, p_lora),
                dres, dh, reinterpret_cast<hst*>(xd), M, state_grad, state_weight,
                mk_drop(seed_dev, salt_prev, p_prev), reinterpret_cast<hst*>(ddrop_prev)};
   if (lora)
@@ -868,7 +873,7 @@ int rdx_wl_ln1_bwd_ex(const void* dx1, int64_t ldx, const float* dgate, const fl
 
 int rdx_wl_ln1_bwd(const void* dx1, int64_t ldx, const float* dgate, const float* h, const float* mean,
                    const float* rstd, const float* gamma, const float* beta, const float* wg, const float* bg,
-                   const float* gconst, const float* lora_aq, const float* lora_av, int r, const int64_t* seed_dev,
+                   const float* gconst, const void* lora_aq, const void* lora_av, int r, const int64_t* seed_dev,
                    int salt_q, int salt_v, float p_lora, const float* dres, float* dh, void* xd, int64_t M, int E,
                    void* stream) {
   return rdx_wl_ln1_bwd_ex(dx1, ldx, dgate, h, mean, rstd, gamma, beta, wg, bg, gconst, lora_aq, lora_av, r, seed_dev,

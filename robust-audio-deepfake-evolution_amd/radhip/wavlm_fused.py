@@ -24,8 +24,8 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check
-from .ops import (HALF, _L, _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, half_dtype, layer_gemm,
-                  rel_bias_table, wgemm_policy)
+from .ops import (HALF, _L, _p, _stream, _timed, attn_bwd_launch, attn_keep_mask, cast_many, half_dtype,
+                  layer_gemm, rel_bias_table, wgemm_policy)
 
 E_FUSED = 1024
 
@@ -192,6 +192,7 @@ class WavLMLayerFn(torch.autograd.Function):
         gate = torch.empty(M, H, device=dev, dtype=torch.float32)
         mean1 = torch.empty(M, device=dev, dtype=torch.float32)
         rstd1 = torch.empty_like(mean1)
+        a16 = cache.a16.view(2, 8, E) if lora else None    # the pass's 16-bit lora_A (FusedEncoderRunner.prepare)
         pend = chain.pending_res if chain is not None else None
         if pend is not None and pend[0] == hf.data_ptr():
             # the previous layer's residual, computed here into its output (= this layer's input) tensor
@@ -199,13 +200,13 @@ class WavLMLayerFn(torch.autograd.Function):
             _, h2p, fop, salt_res, p_res = pend
             check(L.rdx_wl_res_ln1_fwd(_p(h2p), _p(fop), salt_res, float(p_res), _p(hf), _p(ln1.weight),
                                            _p(ln1.bias), float(ln1.eps), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
-                                           _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3,
+                                           _p(a16[0]) if lora else None, _p(a16[1]) if lora else None, 8, sdp, salt + 3,
                                            salt + 4, float(p_lora), _p(x1), ldx, _p(gate), _p(mean1), _p(rstd1), M,
                                            E, st), "wl_res_ln1_fwd")
         else:
             check(L.rdx_wl_ln1_fwd(_p(hf), _p(ln1.weight), _p(ln1.bias), float(ln1.eps), _p(cache.wg),
-                                       _p(cache.bg), _p(cache.gconst), _p(aq) if lora else None,
-                                       _p(av) if lora else None, 8, sdp, salt + 3, salt + 4, float(p_lora), _p(x1),
+                                       _p(cache.bg), _p(cache.gconst), _p(a16[0]) if lora else None,
+                                       _p(a16[1]) if lora else None, 8, sdp, salt + 3, salt + 4, float(p_lora), _p(x1),
                                        ldx, _p(gate), _p(mean1), _p(rstd1), M, E, st), "wl_ln1_fwd")
         pol = _gemm("qkv", M, 3 * E, ldx)
         if pol is not None:
@@ -269,6 +270,7 @@ class WavLMLayerFn(torch.autograd.Function):
         sdp = _p(zseed) if has_seed else None
         salt = SALT_BASE + 8 * index
         ldx = x1.shape[1]
+        a16 = cache.a16.view(2, 8, E) if lora else None
         g = dout.contiguous().view(M, E).float()
         hd = x1.dtype
         L = _L(hd)
@@ -324,8 +326,9 @@ class WavLMLayerFn(torch.autograd.Function):
             ddp = _p(ddrop)
         check(L.rdx_wl_ln1_bwd_ex(_p(dx1), ldx, _p(dgate), _p(hf), _p(mean1), _p(rstd1), _p(ln1.weight),
                                       _p(ln1.bias), _p(cache.wg), _p(cache.bg), _p(cache.gconst),
-                                      _p(aq) if lora else None, _p(av) if lora else None, 8, sdp, salt + 3, salt + 4,
-                                      p_lora, _p(dh2), _p(dh), None, sgp, swp, salt - 8 + 2, p_hidden, ddp, M, E, st),
+                                      _p(a16[0]) if lora else None, _p(a16[1]) if lora else None, 8, sdp, salt + 3,
+                                      salt + 4, p_lora, _p(dh2), _p(dh), None, sgp, swp, salt - 8 + 2, p_hidden, ddp, M,
+                                      E, st),
               "wl_ln1_bwd")
         if ddp is not None:
             chain.dfo[index - 1] = (dh.data_ptr(), ddrop)
@@ -377,8 +380,16 @@ class FusedEncoderRunner:
             self.tab = torch.tensor([[t.data_ptr() for t in bq], [t.data_ptr() for t in bv],
                                      [c.wext.data_ptr() for c in self.caches]], dtype=torch.int64).to(device)
             self.pack_key = key
-        lp0 = loras[0][0]
+        # lora_A of every layer in the 16-bit dtype (autocast's cast of the fp32 weight), one launch per pass: the LN1
+        # kernels stage it per workgroup with 16-byte loads instead of reading and converting 64 KB of fp32 each
         n = len(self.caches)
+        if getattr(self, "a16", None) is None or self.a16.dtype != hd or self.a16.device != device:
+            self.a16 = torch.empty(n, 16, E_FUSED, device=device, dtype=hd)
+            for i, cache in enumerate(self.caches):
+                cache.a16 = self.a16[i]
+        srcs = [lp[i].lora_A[lp[i].adapter].weight.detach() for lp in loras for i in (0, 1)]
+        cast_many(srcs, [self.a16[l, 8 * i:8 * (i + 1)] for l in range(n) for i in (0, 1)])
+        lp0 = loras[0][0]
         check(_L(hd).rdx_wl_lora_pack(n, self.tab[0].data_ptr(), self.tab[1].data_ptr(), self.tab[2].data_ptr(),
                                      self.caches[0].wext.shape[1], 8, float(lp0.scaling[lp0.adapter]), E_FUSED,
                                      _stream(self.tab)), "wl_lora_pack")

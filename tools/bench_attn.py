@@ -17,10 +17,11 @@ from radhip.ops import GatedAttention  # noqa: E402
 def main():
     B, T, H = int(os.environ.get("B", "8")), 201, 16
     P = float(os.environ.get("P", "0.1"))
+    dt = torch.float16 if os.environ.get("DT") == "fp16" else torch.bfloat16    # fp16: libradhip_f16.so
     E = H * 64
     dev = "cuda"
     torch.manual_seed(0)
-    qkv = torch.randn(B, T, 3 * E, device=dev, dtype=torch.bfloat16)
+    qkv = torch.randn(B, T, 3 * E, device=dev, dtype=dt)
     q, k, v = qkv[..., :E], qkv[..., E:2 * E], qkv[..., 2 * E:]
     q, k, v = (t.detach().requires_grad_(True) for t in (q, k, v))
     gate = torch.rand(B, T, H, device=dev) + 1.0
@@ -28,7 +29,7 @@ def main():
     i = torch.arange(T, device=dev)
     pb = tab[:, i[None, :] - i[:, None] + T - 1].contiguous()
     seed = torch.tensor([7], dtype=torch.int64, device=dev)
-    do = torch.randn(B, T, E, device=dev, dtype=torch.bfloat16)
+    do = torch.randn(B, T, E, device=dev, dtype=dt)
     for _ in range(3):
         o = GatedAttention.apply(q, k, v, gate, pb, seed, P, 0)
         o.backward(do)

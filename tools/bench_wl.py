@@ -42,7 +42,8 @@ def main():
         h = torch.randn(M, E, device=dev)
         gm, bt = torch.rand(E, device=dev) + 0.5, torch.randn(E, device=dev) * 0.1
         wg, bg, gc = torch.randn(8, 64, device=dev) * 0.1, torch.randn(8, device=dev) * 0.1, torch.rand(H, device=dev)
-        aq, av = torch.randn(r, E, device=dev) * 0.05, torch.randn(r, E, device=dev) * 0.05
+        aq, av = ((torch.randn(r, E, device=dev) * 0.05).to(torch.bfloat16),
+                  (torch.randn(r, E, device=dev) * 0.05).to(torch.bfloat16))   # 16-bit lora_A (the kernels' input)
         seed = torch.tensor([1234], dtype=torch.int64, device=dev)
         x1 = torch.empty(M, E + 16, device=dev, dtype=torch.bfloat16)
         gate = torch.empty(M, H, device=dev)
