@@ -141,14 +141,6 @@ struct GateW {
   const float* gconst;  // [H] gru_rel_pos_const
 };
 
-// gru_rel_pos_linear's [8, 64] weight staged once per workgroup (2 KB): every row-wave reads its 16 x 8 weights
-// from LDS instead of 512 B per lane from L2 (32 KB per token row), issued before the barrier so that the
-// staging overlaps the row's own HBM loads
-__device__ __forceinline__ void stage_gate_w(float* swg, const float* wg, int nthreads) {
-  for (int i = threadIdx.x; i < 8 * 64 / 4; i += nthreads)
-    reinterpret_cast<float4*>(swg)[i] = reinterpret_cast<const float4*>(wg)[i];
-}
-
 // gate pre-activations z[8] of this lane's head (4 lanes per head, 16 dims per lane); wg in LDS or global
 __device__ __forceinline__ void gate_z(const GateW& g, const float* wgp, const float* x, int lane, float* z) {
   const int part = lane & 3;
@@ -200,13 +192,50 @@ struct Ln1Args {
 constexpr int WL_LN1_ROWS = WL_LN1_ROWS_DEF;
 constexpr int WL_LN1_THREADS = WL_LN1_ROWS * RDX_WAVE;
 
-__device__ __forceinline__ void stage_lora_a(hst* sA, const hst* Aq, const hst* Av) {
-  // WL_R2 * WL_E 16-bit values over WL_LN1_THREADS threads, 8 per 16-byte load
-  constexpr int kN = WL_R2 * WL_E / 8;
-  for (int i = threadIdx.x; i < kN; i += WL_LN1_THREADS) {
-    const int k = (8 * i) / WL_E, e = (8 * i) % WL_E;
-    const hst* src = k < WL_R2 / 2 ? Aq + (int64_t)k * WL_E + e : Av + (int64_t)(k - WL_R2 / 2) * WL_E + e;
-    *reinterpret_cast<uint4*>(sA + 8 * i) = *reinterpret_cast<const uint4*>(src);
+// WL_R2 * WL_E 16-bit values over WL_LN1_THREADS threads, 8 per 16-byte load, every load issued before the first
+// store: a loop that stored each chunk as it arrived waited out one L2 round trip per chunk (8 per thread), which
+// was most of the LoRA kernels' extra time over the LoRA-free variant
+// The staging of a LN1 workgroup, gate weights (2 KB fp32) and LoRA-A (32 KB 16-bit), straight from global memory
+// into LDS by buffer_load ... lds (16 bytes per lane, lane-linear: one wave-instruction fills 1 KB), issued before the
+// rows' own loads and retired by the waitcnt ahead of the barrier: every load of the prologue in flight at once and
+// no registers. (A loop that stored each chunk as it arrived waited out one L2 round trip per chunk, 8 per thread:
+// most of the LoRA kernels' extra time over the LoRA-free variant; staging through registers loads-first kept the
+// round trips but the compiler sank the loads back to their stores under the row kernels' register pressure.)
+typedef __attribute__((ext_vector_type(4))) int wl_i32x4;
+__device__ void wl_load_lds(wl_i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds, int size, int voffset,
+                            int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+__device__ __forceinline__ wl_i32x4 wl_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  wl_i32x4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)(uint32_t)(a >> 32);
+  r.z = (int)bytes;
+  r.w = 0x00020000;  // raw buffer, range-checked
+  return r;
+}
+constexpr int WL_A_INSTR = WL_R2 * WL_E * 2 / 1024 / (WL_LN1_THREADS / 64);   // LoRA-A instructions per wave (8)
+static_assert(WL_A_INSTR * 1024 * (WL_LN1_THREADS / 64) == WL_R2 * WL_E * 2, "whole 1 KB instructions per wave");
+template <bool kLora>
+__device__ __forceinline__ void stage_dma(float* swg, hst* sA, const float* wg, const hst* Aq, const hst* Av) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  constexpr int NW = WL_LN1_THREADS / 64;
+  if (wv == 0) {
+    const wl_i32x4 rg = wl_rsrc(wg, 8 * 64 * 4);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      wl_load_lds(rg, (__attribute__((address_space(3))) uint32_t*)(reinterpret_cast<char*>(swg) + 1024 * q), 16,
+                  1024 * q + 16 * lane, 0, 0, 0);
+  }
+  if (kLora) {
+    const wl_i32x4 rq = wl_rsrc(Aq, WL_R2 / 2 * WL_E * 2), rv = wl_rsrc(Av, WL_R2 / 2 * WL_E * 2);
+#pragma unroll
+    for (int j = 0; j < WL_A_INSTR; ++j) {
+      const int q = wv + NW * j;                       // 1 KB instruction q of the [2r][E] image
+      constexpr int half = WL_R2 / 2 * WL_E * 2 / 1024; // instructions per adapter (16)
+      wl_load_lds(j < WL_A_INSTR / 2 ? rq : rv,         // q < half exactly when j < WL_A_INSTR / 2 (compile time)
+                  (__attribute__((address_space(3))) uint32_t*)(reinterpret_cast<char*>(sA) + 1024 * q), 16,
+                  1024 * (q % half) + 16 * lane, 0, 0, 0);
+    }
   }
 }
 // 16 consecutive bf16 of an LDS row as fp32
@@ -223,15 +252,15 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
   float v[WL_VPL], gm[WL_VPL], bt[WL_VPL], dl[WL_VPL];
   Bf16x16 dlr;
   const uint64_t sr = (a.h2 && a.dres.thr) ? attn_seed(a.dres.seed_dev, a.dres.salt) : 0;  // with the row loads
-  // every global load of the row first (one HBM round trip), the affine parameters with them
+  // every global load first (one round trip): the workgroup's staging, the row, the affine parameters
+  stage_dma<kLora>(swg, sA, a.g.wg, a.Aq, a.Av);
   if (live) {
     load16(a.h2 ? a.h2 + m * WL_E + e0 : a.h + m * WL_E + e0, v);
     if (a.h2) dlr = load16_bf_raw(a.delta + m * WL_E + e0);
     load16(a.gamma + e0, gm);
     load16(a.beta + e0, bt);
   }
-  stage_gate_w(swg, a.g.wg, WL_LN1_THREADS);
-  if (kLora) stage_lora_a(sA, a.Aq, a.Av);
+  __builtin_amdgcn_s_waitcnt(0);   // the staging DMA (and the row) landed
   __syncthreads();
   if (live) {
     if (a.h2) {
@@ -502,6 +531,7 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a
   float mean = 0.f, rstd = 0.f, dg = 0.f;
   Bf16x16 dxr;
   const uint64_t sp = (a.ddrop && a.dprev.thr) ? attn_seed(a.dprev.seed_dev, a.dprev.salt) : 0;
+  stage_dma<kLora>(swg, sA, a.g.wg, a.Aq, a.Av);
   if (live) {
     load16(a.h + m * WL_E + e0, x);
     dxr = load16_bf_raw(a.dx1 + m * a.ldx + e0);
@@ -513,8 +543,7 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a
     rstd = a.rstd[m];
     dg = a.dgate[m * (WL_E / 64) + head];
   }
-  stage_gate_w(swg, a.g.wg, WL_LN1_THREADS);
-  if (kLora) stage_lora_a(sA, a.Aq, a.Av);
+  __builtin_amdgcn_s_waitcnt(0);   // the staging DMA (and the row) landed
   __syncthreads();
   if (!live) return;  // after the only barrier
   unpack16_bf(dxr, dx);
