@@ -701,6 +701,11 @@ int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void* c, void* d
 int rdx_sconv_wgrad_nblk(int N, int Ho, int W);
 int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* part, int N, int H, int W, int ci, int co,
                     int kh, int ph, void* stream);
+/* rdx_sconv_wprep_many: for n <= 32 fp32 convolution weights src[k] [co][ci][kh][3] (kh 1 or 2), both 16-bit operand
+ *   layouts in one launch: wf[k] [kh*3][co][ci] (rdx_sconv_fwd's w) and wd[k] [kh*3][ci][co] of the kernel flipped in
+ *   both axes (the input gradient's w). src / wf / wd are host arrays of device pointers. */
+int rdx_sconv_wprep_many(int n, const float* const* src, void* const* wf, void* const* wd, const int* co,
+                         const int* ci, const int* kh, void* stream);
 
 #ifdef __cplusplus
 }

@@ -612,6 +612,54 @@ extern "C" int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void*
   return sconv_fwd_launch<32, 32, 2, true>(a, as_stream(stream));
 }
 
+// Both 16-bit operand layouts of up to SC_WP_MAX convolution weights [co][ci][kh][3] (fp32) in one launch: wf
+// [kh*3][co][ci] (forward, tap-major) and wd [kh*3][ci][co] of the kernel flipped in both axes (input gradient).
+// The per-window preparation of the SincNet stack's weights (radhip/window.py) was four torch launches per weight
+// (cast, permute-copy, flip, permute-copy).
+constexpr int SC_WP_MAX = 32;
+struct WPrepTable {
+  const float* src[SC_WP_MAX];
+  hst* wf[SC_WP_MAX];
+  hst* wd[SC_WP_MAX];
+  int co[SC_WP_MAX], ci[SC_WP_MAX], kh[SC_WP_MAX];
+};
+__global__ __launch_bounds__(256) void sconv_wprep_many_kernel(WPrepTable t) {
+  const int k = blockIdx.y;
+  const int co = t.co[k], ci = t.ci[k], kh = t.kh[k];
+  const int n = co * ci * kh * 3;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int kw = i % 3, r = i / 3, h = r % kh, r2 = r / kh, c = r2 % ci, o = r2 / ci;   // src [o][c][h][kw]
+    const hst v = f2h(t.src[k][i]);
+    t.wf[k][((int64_t)(h * 3 + kw) * co + o) * ci + c] = v;
+    t.wd[k][((int64_t)((kh - 1 - h) * 3 + (2 - kw)) * ci + c) * co + o] = v;
+  }
+}
+
+extern "C" int rdx_sconv_wprep_many(int n, const float* const* src, void* const* wf, void* const* wd, const int* co,
+                                    const int* ci, const int* kh, void* stream) {
+  RDX_REQUIRE(n >= 0 && (n == 0 || (src && wf && wd && co && ci && kh)));
+  if (n > SC_WP_MAX) return RDX_EUNSUPPORTED;
+  if (n == 0) return RDX_OK;
+  WPrepTable t{};
+  int mx = 1;
+  for (int k = 0; k < n; ++k) {
+    RDX_REQUIRE(src[k] && wf[k] && wd[k] && co[k] > 0 && ci[k] > 0 && (kh[k] == 1 || kh[k] == 2));
+    t.src[k] = src[k];
+    t.wf[k] = reinterpret_cast<hst*>(wf[k]);
+    t.wd[k] = reinterpret_cast<hst*>(wd[k]);
+    t.co[k] = co[k];
+    t.ci[k] = ci[k];
+    t.kh[k] = kh[k];
+    const int e = co[k] * ci[k] * kh[k] * 3;
+    mx = e > mx ? e : mx;
+  }
+  const int bx = (mx + 255) / 256;
+  hipLaunchKernelGGL(sconv_wprep_many_kernel, dim3((unsigned)(bx < 128 ? bx : 128), (unsigned)n), dim3(256), 0,
+                     as_stream(stream), t);
+  RDX_LAUNCH_CHECK();
+  return RDX_OK;
+}
+
 // row chunks of the weight-gradient units: about 4 rows each, at least 2048 units where the shape allows
 static int sc_wgrad_nz(int N, int Ho, int W) {
   const int64_t su = (int64_t)N * ((W + SC_P - 1) / SC_P);

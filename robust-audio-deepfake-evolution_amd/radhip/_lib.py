@@ -151,6 +151,7 @@ SIGNATURES = {
     "rdx_sconv_fwd_res": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_sconv_wgrad_nblk": (c_int, [c_int, c_int, c_int]),
     "rdx_sconv_wgrad": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "rdx_sconv_wprep_many": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp, c_i64,
                              c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_attn_keep_mask_words": (c_i64, [c_int, c_int, c_int]),

@@ -830,6 +830,32 @@ def _sconv_w_prep(weight, hd):
     return wf, wd
 
 
+def sconv_prep_many(weights, hd):
+    """Fill SCONV_WCACHE with both 16-bit layouts of every weight (sconv_weight_ok, fp32 contiguous, on the GPU) in
+    one launch per 32 weights (rdx_sconv_wprep_many): the window's SincNet stack prepared at once instead of four
+    torch launches per weight on first use (_sconv_w_prep's layouts). `weights` are the parameters themselves (the
+    cache is keyed by them); only their data is read."""
+    cache = SCONV_WCACHE
+    ws = [w for w in weights if w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and sconv_weight_ok(w)]
+    if cache is None or not ws:
+        return
+    for i in range(0, len(ws), 32):
+        g = ws[i:i + 32]
+        wf, wd = [], []
+        for w in g:
+            co, ci, kh, kw = w.shape
+            wf.append(torch.empty(kh * kw, co, ci, device=w.device, dtype=hd))
+            wd.append(torch.empty(kh * kw, ci, co, device=w.device, dtype=hd))
+        n = len(g)
+        ints = lambda vals: (ctypes.c_int * n)(*vals)
+        check(_L(hd).rdx_sconv_wprep_many(n, ptr_array([w.data_ptr() for w in g]), ptr_array([t.data_ptr() for t in wf]),
+                                          ptr_array([t.data_ptr() for t in wd]), ints([w.shape[0] for w in g]),
+                                          ints([w.shape[1] for w in g]), ints([w.shape[2] for w in g]),
+                                          _stream(g[0])), "sconv_wprep_many")
+        for w, a, b in zip(g, wf, wd):
+            cache[(id(w), hd)] = (w, a, b)
+
+
 def _sconv_run(x, w_tap, ci, co, kh, ph, y2=None, bn=None, res=None):
     """x: 16-bit NHWC (bf16 or fp16: the output's dtype and the library); res: an [N, co, Ho, W] channels_last
     tensor of x's dtype added in the epilogue (y = r(r(conv) + res), r = rounding to that dtype)."""

@@ -127,6 +127,7 @@ class WindowStep:
         self._lin_src = [p for mod in m.modules() if isinstance(mod, SideLinear)
                          for p in (mod.weight, mod.bias) if p is not None and p.dtype == torch.float32]
         self._lin_dst = None
+        self._sconv_w = None
         self.chain_captured = False
         self.feats = None
         self._host = None
@@ -246,10 +247,22 @@ class WindowStep:
         for p, c in zip(self._lin_src, self._lin_dst):
             self._wcache[("lin", id(p), c.dtype)] = (p, c)
 
+    def _precast_sconv(self):
+        """Both 16-bit layouts of every SincNet stack convolution weight into the window's cache in one launch
+        (ops.sconv_prep_many); the convolutions' first use then finds them."""
+        dt = self.tr.amp_dtype
+        if dt not in ops.HALF or not hasattr(self.tr.model, "sinc_stream") or os.environ.get("RADHIP_SCONV_PREP") == "0":
+            return
+        if self._sconv_w is None:
+            self._sconv_w = [mod.weight for mod in self.tr.model.sinc_stream.modules()
+                             if isinstance(mod, torch.nn.Conv2d) and mod.weight.dim() == 4 and mod.weight.shape[-1] == 3]
+        ops.sconv_prep_many(self._sconv_w, dt)    # the parameters themselves: the cache is keyed by them
+
     def _clean_pass(self):
         self._wcache = {}                  # weight layouts prepared by this pass, reused by the window's others
         ops.SCONV_WCACHE = self._wcache
         self._precast_linears()
+        self._precast_sconv()
         self._pass_grads(self._clean_pass_body)
 
     def _sinc_adv_forward(self):
