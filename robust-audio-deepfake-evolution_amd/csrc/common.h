@@ -55,6 +55,11 @@ __device__ __forceinline__ rdx_f32x16 mfma32x32x16(hx8 a, hx8 b, rdx_f32x16 c) {
 __device__ __forceinline__ rdx_f32x4 mfma16x16x32(hx8 a, hx8 b, rdx_f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
+// c + a.lo * b.lo + a.hi * b.hi of two packed 16-bit pairs, fp32 accumulate (v_dot2c_f32_f16)
+__device__ __forceinline__ float hdot2(uint32_t a, uint32_t b, float c) {
+  typedef __attribute__((ext_vector_type(2))) _Float16 rdx_h2;
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(rdx_h2, a), __builtin_bit_cast(rdx_h2, b), c, false);
+}
 #else
 __device__ __forceinline__ float h2f(hst x) { return __bfloat162float(x); }
 __device__ __forceinline__ hst f2h(float x) { return __float2bfloat16(x); }
@@ -66,6 +71,11 @@ __device__ __forceinline__ rdx_f32x16 mfma32x32x16(hx8 a, hx8 b, rdx_f32x16 c) {
 }
 __device__ __forceinline__ rdx_f32x4 mfma16x16x32(hx8 a, hx8 b, rdx_f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// c + a.lo * b.lo + a.hi * b.hi of two packed 16-bit pairs, fp32 accumulate (v_dot2c_f32_bf16)
+__device__ __forceinline__ float hdot2(uint32_t a, uint32_t b, float c) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 rdx_b2;
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(rdx_b2, a), __builtin_bit_cast(rdx_b2, b), c, false);
 }
 #endif
 __device__ __forceinline__ float hround(float x) { return h2f(f2h(x)); }

@@ -238,8 +238,6 @@ __device__ __forceinline__ void stage_dma(float* swg, hst* sA, const float* wg, 
     }
   }
 }
-// 16 consecutive bf16 of an LDS row as fp32
-__device__ __forceinline__ void lds16_bf(const hst* p, float* v) { load16_bf(p, v); }
 
 template <bool kLora>
 __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
@@ -293,22 +291,26 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_fwd_kernel(Ln1Args a) {
     if (!live) return;
     const uint64_t sq = a.dq.thr ? attn_seed(a.dq.seed_dev, a.dq.salt) : 0;
     const uint64_t sv = a.dv.thr ? attn_seed(a.dv.seed_dev, a.dv.salt) : 0;
-    float mq[WL_VPL], mv[WL_VPL];
+    // each adapter's dropped row in the 16-bit type (the reference's dropout output: lora_A's input under autocast),
+    // packed in pairs, and the down-projection as packed dot products (v_dot2c_f32_*: 8 per adapter row instead of
+    // 16 unpacks + 16 FMAs; the per-row VALU work of these 2r dot products was the LoRA kernels' extra time)
+    uint32_t mq[WL_VPL / 2], mv[WL_VPL / 2];
 #pragma unroll
-    for (int i = 0; i < WL_VPL; ++i) {
-      const uint64_t idx = (uint64_t)m * WL_E + e0 + i;
-      mq[i] = v[i] * drop_scale(a.dq, sq, idx);
-      mv[i] = v[i] * drop_scale(a.dv, sv, idx);
+    for (int j = 0; j < WL_VPL / 2; ++j) {
+      const uint64_t idx = (uint64_t)m * WL_E + e0 + 2 * j;
+      mq[j] = hpack2(v[2 * j] * drop_scale(a.dq, sq, idx), v[2 * j + 1] * drop_scale(a.dq, sq, idx + 1));
+      mv[j] = hpack2(v[2 * j] * drop_scale(a.dv, sv, idx), v[2 * j + 1] * drop_scale(a.dv, sv, idx + 1));
     }
     float acc[WL_R2];
 #pragma unroll
     for (int k = 0; k < WL_R2; ++k) {
-      const float* x = k < WL_R2 / 2 ? mq : mv;
-      float w[WL_VPL];
-      lds16_bf(sA + k * WL_E + e0, w);
+      const uint32_t* x = k < WL_R2 / 2 ? mq : mv;
+      const uint4* wp = reinterpret_cast<const uint4*>(sA + k * WL_E + e0);
+      const uint4 w0 = wp[0], w1 = wp[1];
+      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < WL_VPL; ++i) s = fmaf(w[i], x[i], s);
+      for (int j = 0; j < WL_VPL / 2; ++j) s = hdot2(w[j], x[j], s);
       acc[k] = s;
     }
     float tot = wave_sum16(acc, lane);
@@ -583,21 +585,33 @@ __global__ __launch_bounds__(WL_LN1_THREADS) void wl_ln1_bwd_kernel(Ln1BwdArgs a
         store16_bf(a.xd + (which * a.M + m) * WL_E + e0, xm);
       }
     }
-    // the 2r down-projection gradients of this row: one 32-byte broadcast read
-    float da[WL_R2];
-    load16_bf(a.dx1 + m * a.ldx + WL_E, da);
+    // the 2r down-projection gradients of this row, packed in k pairs (one 32-byte broadcast read); the term
+    // sum_k A[k][e] da[k] of each element e as packed dot products over k pairs: the two A rows k, k + 1 read as
+    // before (32 contiguous bytes per lane, conflict-free), their 16-bit halves regrouped per element
+    const uint4 dap[2] = {*reinterpret_cast<const uint4*>(a.dx1 + m * a.ldx + WL_E),
+                          *reinterpret_cast<const uint4*>(a.dx1 + m * a.ldx + WL_E + 8)};
 #pragma unroll
     for (int which = 0; which < 2; ++which) {
       float acc[WL_VPL];
 #pragma unroll
       for (int i = 0; i < WL_VPL; ++i) acc[i] = 0.f;
-#pragma unroll 1
-      for (int k = 0; k < WL_R2 / 2; ++k) {
-        float w[WL_VPL];
-        lds16_bf(sA + (which * (WL_R2 / 2) + k) * WL_E + e0, w);
-        const float d = da[which * (WL_R2 / 2) + k];
+      const uint32_t dk[4] = {dap[which].x, dap[which].y, dap[which].z, dap[which].w};
 #pragma unroll
-        for (int i = 0; i < WL_VPL; ++i) acc[i] = fmaf(w[i], d, acc[i]);
+      for (int kp = 0; kp < WL_R2 / 4; ++kp) {
+        const int k = which * (WL_R2 / 2) + 2 * kp;
+        const uint4* ra = reinterpret_cast<const uint4*>(sA + k * WL_E + e0);
+        const uint4* rb = reinterpret_cast<const uint4*>(sA + (k + 1) * WL_E + e0);
+        const uint4 a0 = ra[0], a1 = ra[1], b0 = rb[0], b1 = rb[1];
+        const uint32_t wa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t wb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int j = 0; j < WL_VPL / 2; ++j) {
+          // v_perm_b32 (selector bytes 0-3: the second operand's bytes, 4-7: the first's)
+          const uint32_t ev = __builtin_amdgcn_perm(wb[j], wa[j], 0x05040100u);   // (A[k][2j], A[k + 1][2j])
+          const uint32_t od = __builtin_amdgcn_perm(wb[j], wa[j], 0x07060302u);   // (A[k][2j + 1], A[k + 1][2j + 1])
+          acc[2 * j] = hdot2(ev, dk[kp], acc[2 * j]);
+          acc[2 * j + 1] = hdot2(od, dk[kp], acc[2 * j + 1]);
+        }
       }
       const Drop& dd = which ? a.dv : a.dq;
       const uint64_t sd = which ? sv : sq;
