@@ -701,6 +701,33 @@ int rdx_sconv_dgrad_bnselu(const void* dy, const void* w, const void* c, void* d
 int rdx_sconv_wgrad_nblk(int N, int Ho, int W);
 int rdx_sconv_wgrad(const void* x, const void* dy, float* dw, float* part, int N, int H, int W, int ci, int co,
                     int kh, int ph, void* stream);
+/* ---- The detector head's squeeze-excitation (src/models/DualStreamSEMamba.py:492-531) under autocast, csrc/head.hip.
+ * rdx_se_fwd: x [B, T, C] 16-bit (C % 8 == 0, C <= 256, 16-byte aligned), w1 [R, C], w2 [C, R] 16-bit (R <= 16):
+ *   m = mean_t x, h = relu(m w1^T), s = sigmoid(h w2^T) (each rounded to 16 bits as autocast leaves them; saved to
+ *   m [B, C], h [B, R], s [B, C]) and y = x * s [B, T, C].
+ * rdx_se_bwd: from dy [B, T, C] and the saved tensors: dx [B, T, C] (both branches' gradients added in 16 bits) and
+ *   the fc weight gradients ADDED in fp32 into dw1 [R, C] and dw2 [C, R] (per-utterance partial rows in part,
+ *   rdx_se_bwd_part_floats(B, C, R) floats, summed in utterance order). */
+int rdx_se_fwd(const void* x, const void* w1, const void* w2, void* y, void* m, void* h, void* s, int B, int T, int C,
+               int R, void* stream);
+int64_t rdx_se_bwd_part_floats(int B, int C, int R);
+int rdx_se_bwd(const void* dy, const void* x, const void* w1, const void* w2, const void* m, const void* h, const void* s,
+               void* dx, float* part, float* dw1, float* dw2, int B, int T, int C, int R, void* stream);
+/* rdx_attn_pool_fwd: the head's attention pooling under autocast (src/models/DualStreamSEMamba.py:700-770):
+ *   z = round(f w^T + bias) (f [B, T, C] 16-bit, w [C], bias [1] 16-bit or NULL), a = softmax_t(z) fp32 (saved to
+ *   a [B, T]), feat [B, C] = round(round(a)^T f). T <= 1024, C <= 1024.
+ * rdx_attn_pool_bwd: from dfeat [B, C]: df [B, T, C] (the weighted sum's and the scores' gradients added in 16 bits)
+ *   and dw [C] / db [1] (db may be NULL) ADDED in fp32 (part: B * (C + 1) floats of per-utterance partials). */
+int rdx_attn_pool_fwd(const void* f, const void* w, const void* bias, void* feat, float* a, int B, int T, int C,
+                      void* stream);
+int rdx_attn_pool_bwd(const void* f, const void* w, const float* a, const void* dfeat, void* df, float* part, float* dw,
+                      float* db, int B, int T, int C, void* stream);
+/* rdx_upcat_fwd: DualStreamFusion's alignment + concat (src/models/DualStreamSEMamba.py:537-637): out [B, T1, 2C] =
+ *   [fw [B, T1, C] | fs [B, T2, C] at F.interpolate's 'nearest' index min(floor(t * (T2 / T1)), T2 - 1)], 16-bit,
+ *   C % 8 == 0, 16-byte aligned.
+ * rdx_upcat_bwd: dfs [B, T2, C] = the nearest upsample's backward of dout[..., C:2C] (fp32 sums, rounded once). */
+int rdx_upcat_fwd(const void* fw, const void* fs, void* out, int B, int T1, int T2, int C, void* stream);
+int rdx_upcat_bwd(const void* dout, void* dfs, int B, int T1, int T2, int C, void* stream);
 /* rdx_sconv_wprep_many: for n <= 32 fp32 convolution weights src[k] [co][ci][kh][3] (kh 1 or 2), both 16-bit operand
  *   layouts in one launch: wf[k] [kh*3][co][ci] (rdx_sconv_fwd's w) and wd[k] [kh*3][ci][co] of the kernel flipped in
  *   both axes (the input gradient's w). src / wf / wd are host arrays of device pointers. */

@@ -19,11 +19,16 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
+from radhip.head import attn_pool, pool_eligible, se_eligible, se_layer, upcat, upcat_eligible
 from radhip.linear import RowLayerNorm, SideLinear, ffn_residual
 from radhip.mamba import Mamba
 from radhip.ops import layer_weighted_sum
 from radhip.sinc import CONV, Residual_block, SincNetEncoder  # noqa: F401  (re-exported like the reference)
 from radhip.wavlm import PeftWrapped, WavLMConfigLite, WavLMEncoderModel
+
+_SE_FUSED = os.environ.get("RADHIP_SE_FUSED", "1") != "0"    # 0: the module path (A/B)
+_POOL_FUSED = os.environ.get("RADHIP_POOL_FUSED", "1") != "0"   # 0: the module path (A/B)
+_UPCAT_FUSED = os.environ.get("RADHIP_UPCAT_FUSED", "1") != "0"  # 0: the module path (A/B)
 
 _LOCAL_WAVLM = [
     os.environ.get("RADHIP_WAVLM_DIR", ""),
@@ -149,6 +154,9 @@ class SELayer(nn.Module):
                                 SideLinear(channel // reduction, channel, bias=False), nn.Sigmoid())
 
     def forward(self, x: Tensor) -> Tensor:
+        w1, w2 = self.fc[0].weight, self.fc[2].weight
+        if _SE_FUSED and se_eligible(x, w1, w2):
+            return se_layer(x, w1, w2)       # radhip/head.py: one launch forward, two backward
         b, t, c = x.size()
         y = self.avg_pool(x.permute(0, 2, 1)).view(b, c)
         return x * self.fc(y).view(b, 1, c)
@@ -173,6 +181,8 @@ class DualStreamFusion(nn.Module):
         f_w = self.wavlm_proj(self.ln_wavlm(f_wavlm))
         f_s = self.sinc_proj(self.ln_sinc(f_sinc))
         T1 = f_w.size(1)
+        if _UPCAT_FUSED and upcat_eligible(f_w, f_s):       # radhip/head.py: one gather each way
+            return self.dropout(self.norm(self.se_layer(self.fusion_proj(upcat(f_w, f_s)))))
         if f_s.size(1) != T1:
             mode = "nearest" if T1 / f_s.size(1) > 4.0 else "linear"
             kw = {} if mode == "nearest" else {"align_corners": False}
@@ -248,7 +258,10 @@ class Model(nn.Module):
         for layer in self.backbone_layers:
             f = layer(f)
         f = self.norm_f(f)
-        attn = F.softmax(self.attention_pool(f), dim=1)                      # [B, T, 1]
-        features = torch.matmul(attn.transpose(1, 2), f).squeeze(1)          # [B, emb]
+        if _POOL_FUSED and pool_eligible(f, self.attention_pool):
+            features = attn_pool(f, self.attention_pool.weight, self.attention_pool.bias)   # radhip/head.py
+        else:
+            attn = F.softmax(self.attention_pool(f), dim=1)                  # [B, T, 1]
+            features = torch.matmul(attn.transpose(1, 2), f).squeeze(1)      # [B, emb]
         features = self.dropout(features)
         return features, self.classifier(features)

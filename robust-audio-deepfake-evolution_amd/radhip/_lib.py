@@ -152,6 +152,13 @@ SIGNATURES = {
     "rdx_sconv_wgrad_nblk": (c_int, [c_int, c_int, c_int]),
     "rdx_sconv_wgrad": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_sconv_wprep_many": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rdx_se_fwd": (c_int, [c_vp] * 7 + [c_int] * 4 + [c_vp]),
+    "rdx_se_bwd_part_floats": (c_i64, [c_int, c_int, c_int]),
+    "rdx_se_bwd": (c_int, [c_vp] * 11 + [c_int] * 4 + [c_vp]),
+    "rdx_attn_pool_fwd": (c_int, [c_vp] * 5 + [c_int] * 3 + [c_vp]),
+    "rdx_attn_pool_bwd": (c_int, [c_vp] * 8 + [c_int] * 3 + [c_vp]),
+    "rdx_upcat_fwd": (c_int, [c_vp] * 3 + [c_int] * 4 + [c_vp]),
+    "rdx_upcat_bwd": (c_int, [c_vp] * 2 + [c_int] * 4 + [c_vp]),
     "rdx_attn_fwd": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_f32, c_f32, c_vp, c_i64,
                              c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "rdx_attn_keep_mask_words": (c_i64, [c_int, c_int, c_int]),
