@@ -16,7 +16,7 @@ from collections import defaultdict
 
 def categorize(name):
     n = name
-    if n.startswith("rdx::") or "rdx::" in n[:40]:
+    if n.startswith("rdx::") or "rdx::" in n[:40] or n.startswith("b0x_"):   # b0x_bwd_kernel: csrc/b0fused.hip
         return "radhip (hand-written HIP)"
     if n.startswith("Cijk_") or "gemm" in n.lower() and "conv" not in n.lower():
         return "GEMM (hipBLASLt/rocBLAS)"
@@ -74,6 +74,8 @@ def main():
     busy = 0
     for s, e, n in win:
         short = re.sub(r"\(.*", "", n)[:100]
+        if "at::native::" in n and len(short) < 40:   # a templated name cut at its first parenthesis
+            short = n[:160]
         per[short][0] += 1
         per[short][1] += e - s
         cat[categorize(n)] += e - s
@@ -101,7 +103,11 @@ def main():
         print(f"{1e-6 * t / m:9.3f} {c / m:8.1f} {1e-3 * t / c:10.2f}  {k}")
     print("# radhip kernels")
     for k, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1]):
-        if "rdx::" in k:
+        if categorize(k) == "radhip (hand-written HIP)":
+            print(f"{1e-6 * t / m:9.3f} {c / m:8.1f} {1e-3 * t / c:10.2f}  {k}")
+    print("# other kernels (torch / hipBLASLt / runtime)")
+    for k, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+        if categorize(k) != "radhip (hand-written HIP)":
             print(f"{1e-6 * t / m:9.3f} {c / m:8.1f} {1e-3 * t / c:10.2f}  {k}")
 
 
