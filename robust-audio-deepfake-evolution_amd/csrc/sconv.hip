@@ -28,6 +28,7 @@
 namespace rdx {
 
 typedef __attribute__((ext_vector_type(16))) float sf32x16;
+typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
 
 constexpr int SC_T = 256;        // threads
 constexpr int SC_P = 128;        // output positions per strip
@@ -69,16 +70,28 @@ struct SConvArgs {
 // Input rows cycle through KH + 1 LDS slots: input row (ho - ph + kh) of output row ho lives in slot
 // (ho + kh) % (KH + 1), and the row the next output row adds is loaded into registers while the current
 // row's MFMAs run, then written to the slot the current row no longer needs (one barrier per row).
+constexpr uint32_t SC_OOB = 0x80000000u;   // a buffer offset past every range (the host keeps ranges below it)
+
+// raw buffer resource over `bytes` bytes at p (range-checked: an offset past it loads 0, a store there is dropped)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// input row hi of the utterance behind rs (positions p0 - 1 .. p0 + 128, zero outside the image) into registers:
+// one unconditional buffer load per 16-byte item (an item outside the image gets an offset past the range and
+// loads 0). Branch-free, so the compiler tracks the loads exactly and does not wait on them, or on the stores
+// around them, before they are used.
 template <int CI>
-__device__ __forceinline__ void sc_load_row(uint4* regs, const hst* x, int n, int hi, int H, int W, int p0) {
+__device__ __forceinline__ void sc_load_row(uint4* regs, __amdgpu_buffer_rsrc_t rs, int hi, int H, int W, int p0) {
   constexpr int XCH = CI / 8, NV = (SC_PW * XCH + SC_T - 1) / SC_T;
+  const bool rok = hi >= 0 && hi < H;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int i = threadIdx.x + SC_T * j;
     const int ch = i % XCH, pp = i / XCH, wi = p0 - 1 + pp;
-    regs[j] = make_uint4(0, 0, 0, 0);
-    if (pp < SC_PW && hi >= 0 && hi < H && wi >= 0 && wi < W)
-      regs[j] = *reinterpret_cast<const uint4*>(x + (((int64_t)n * H + hi) * W + wi) * CI + ch * 8);
+    const bool ok = rok && pp < SC_PW && wi >= 0 && wi < W;
+    const uint32_t off = ok ? (uint32_t)(((hi * W + wi) * CI + ch * 8) * 2) : SC_OOB;
+    regs[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
   }
 }
 template <int CI>
@@ -105,17 +118,26 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   // the epilogue's per-channel BN parameters (up to 5 x CO fp32) in LDS: read per output element, they were
   // global loads ordered behind the previous group's stores (y may alias bn / c for the compiler)
   float* sbn = reinterpret_cast<float*>(xs + NSLOT * SLOT);
-  const hst* __restrict__ cpre_src = a.c;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n = blockIdx.y, p0 = blockIdx.x * SC_P;
   const int ho0 = blockIdx.z * a.rows_per, ho1 = min(a.Ho, ho0 + a.rows_per);
+  // buffer resources over this utterance's input and output images (the host keeps each below 2 GiB)
+  const int64_t ibytes = (int64_t)a.H * a.W * CI * 2, obytes = (int64_t)a.Ho * a.W * CO * 2;
+  const int64_t obase_n = (int64_t)n * a.Ho * a.W * CO;
+  const __amdgpu_buffer_rsrc_t rx = sc_rsrc(a.x + (int64_t)n * a.H * a.W * CI, ibytes);
+  const __amdgpu_buffer_rsrc_t ry = sc_rsrc(a.y + obase_n, obytes);
+  const __amdgpu_buffer_rsrc_t ry2 = sc_rsrc(a.y2 ? a.y2 + obase_n : a.y + obase_n, obytes);
+  const __amdgpu_buffer_rsrc_t rc = sc_rsrc(kBnBwd ? a.c + obase_n : a.y + obase_n, obytes);
+  const __amdgpu_buffer_rsrc_t rres = sc_rsrc(a.res ? a.res + obase_n : a.y + obase_n, obytes);
   {  // weights: every load issued before the first LDS store (one round trip, not one per chunk)
     constexpr int NWV = (KH * 3 * CO * XCH + SC_T - 1) / SC_T;
+    const __amdgpu_buffer_rsrc_t rw = sc_rsrc(a.w, (int64_t)KH * 3 * CO * CI * 2);
     uint4 wr[NWV];
 #pragma unroll
-    for (int j = 0; j < NWV; ++j) {
+    for (int j = 0; j < NWV; ++j) {   // unconditional (past the end: an offset out of range), so wr stays in VGPRs
       const int i = tid + SC_T * j;
-      if (i < KH * 3 * CO * XCH) wr[j] = *reinterpret_cast<const uint4*>(a.w + (int64_t)(i / XCH) * CI + (i % XCH) * 8);
+      const uint32_t off = i < KH * 3 * CO * XCH ? (uint32_t)(((i / XCH) * CI + (i % XCH) * 8) * 2) : SC_OOB;
+      wr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0));
     }
 #pragma unroll
     for (int j = 0; j < NWV; ++j) {
@@ -128,13 +150,14 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
   uint4 pre[NV];
 #pragma unroll
   for (int kh = 0; kh < KH; ++kh) {
-    sc_load_row<CI>(pre, a.x, n, ho0 + kh - a.ph, a.H, a.W, p0);
+    sc_load_row<CI>(pre, rx, ho0 + kh - a.ph, a.H, a.W, p0);
     sc_store_row<CI>(xs + ((ho0 + kh) % NSLOT) * SLOT, pre);
   }
   __syncthreads();
   constexpr int NT = CO / 32;
   const int pw = wv * 32 + r;  // this lane's position within the strip (B operand row)
   const int p = p0 + pw;
+  const bool pv = p < a.W;
   // kBnBwd: per-lane sums [sum][t][g][e] over the rows this workgroup walks (channel t*32 + 8g + 4h + e)
   float bsum[kBnBwd ? 3 : 1][NT][4][4];
   if constexpr (kBnBwd) {
@@ -147,116 +170,118 @@ __global__ __launch_bounds__(SC_T) void sconv_fwd_kernel(SConvArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) bsum[q][t][g][e] = 0.f;
   }
+  // MFMA steps of a row: (kh, kw, 16-channel step s); their LDS operands are read PD steps ahead
+  constexpr int SPK = CI / 16, NSTEP = KH * 3 * SPK, PD = 4;
   for (int ho = ho0; ho < ho1; ++ho) {
     const bool more = ho + 1 < ho1;
-    if (more) sc_load_row<CI>(pre, a.x, n, ho - a.ph + KH, a.H, a.W, p0);
+    // the next input row (rows past the last one this workgroup needs load zeros: ho1 <= Ho keeps them in range
+    // or out of the image)
+    sc_load_row<CI>(pre, rx, more ? ho - a.ph + KH : -1, a.H, a.W, p0);
+    // this lane's output byte offset in the utterance (an offset past the range for a position past W: its loads
+    // read 0 and its stores are dropped)
+    const uint32_t orow = pv ? (uint32_t)(((ho * a.W + p) * CO + 4 * h) * 2) : SC_OOB;
     // kBnBwd: this row's saved pre-activations, loaded with the next input row (before the MFMAs), not one
-    // round trip per channel group in the epilogue
-    uint2 cpre[kBnBwd ? NT : 1][4];
-    if constexpr (kBnBwd) {
-      if (p < a.W) {
-        const int64_t obase = (((int64_t)n * a.Ho + ho) * a.W + p) * CO;
+    // round trip per channel group in the epilogue; !kBnBwd with a residual: this row's residual
+    uint2 cres[NT][4];
+    if (kBnBwd || a.res) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) cpre[t][g] = *reinterpret_cast<const uint2*>(cpre_src + obase + t * 32 + 8 * g + 4 * h);
-      }
-    }
-    // residual epilogue: this row's residual, loaded before the MFMAs as the saved pre-activations are
-    uint2 rres[kBnBwd ? 1 : NT][4];
-    if constexpr (!kBnBwd) {
-      if (a.res && p < a.W) {
-        const int64_t obase = (((int64_t)n * a.Ho + ho) * a.W + p) * CO;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) rres[t][g] = *reinterpret_cast<const uint2*>(a.res + obase + t * 32 + 8 * g + 4 * h);
-      }
+        for (int g = 0; g < 4; ++g)
+          cres[t][g] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                     kBnBwd ? rc : rres, orow + (t * 32 + 8 * g) * 2, 0, 0));
     }
     sf32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    const char* xk0 = xs + (ho % NSLOT) * SLOT;
+    const char* xk1 = xs + ((ho + 1) % NSLOT) * SLOT;
+    hx8 xq[NSTEP], wq[NSTEP][NT];
 #pragma unroll
-    for (int kh = 0; kh < KH; ++kh) {
-      const char* xk = xs + ((ho + kh) % NSLOT) * SLOT;
+    for (int q = 0; q < NSTEP + PD; ++q) {
+      if (q < NSTEP) {   // issue step q's operand reads
+        const int kh = q / (3 * SPK), kw = (q / SPK) % 3, s = q % SPK;
+        xq[q] = *reinterpret_cast<const hx8*>((kh ? xk1 : xk0) + sc_off<CI>(pw + kw, 2 * s + h));
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
+        for (int t = 0; t < NT; ++t)
+          wq[q][t] = *reinterpret_cast<const hx8*>(ws + sc_off<CI>((kh * 3 + kw) * CO + t * 32 + r, 2 * s + h));
+      }
+      if (q >= PD) {     // step q - PD on the MFMA (Y^T tile: rows co, columns positions)
 #pragma unroll
-        for (int s = 0; s < CI / 16; ++s) {
-          const hx8 xf = *reinterpret_cast<const hx8*>(xk + sc_off<CI>(pw + kw, 2 * s + h));
-#pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            const int rowc = (kh * 3 + kw) * CO + t * 32 + r;
-            const hx8 wf = *reinterpret_cast<const hx8*>(ws + sc_off<CI>(rowc, 2 * s + h));
-            acc[t] = sc_mfma(wf, xf, acc[t]);  // Y^T tile: rows co, columns positions
-          }
-        }
+        for (int t = 0; t < NT; ++t) acc[t] = sc_mfma(wq[q - PD][t], xq[q - PD], acc[t]);
+      }
+      // keep the reads PD steps ahead: the scheduler would otherwise pull each read back to its MFMA and expose
+      // the LDS latency at every step (one wave per SIMD at 64 x 64 channels: nothing else hides it)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue: lane owns position p, channels co = t*32 + 8g + 4h + e
-    if (p < a.W) {
-      const int64_t obase = (((int64_t)n * a.Ho + ho) * a.W + p) * CO;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int co = t * 32 + 8 * g + 4 * h;
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
-          if constexpr (kBnBwd) {
-            const uint2 cc = cpre[t][g];
-            const float cv[4] = {hlo(cc.x), hhi(cc.x),
-                                 hlo(cc.y), hhi(cc.y)};
-            const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
-            const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
-            const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
-            const float4 bb = *reinterpret_cast<const float4*>(sbn + 3 * CO + co);
-            const float4 is = *reinterpret_cast<const float4*>(sbn + 4 * CO + co);
-            const float pcb[4] = {cb.x, cb.y, cb.z, cb.w}, pmu[4] = {mu.x, mu.y, mu.z, mu.w};
-            const float psg[4] = {sg.x, sg.y, sg.z, sg.w}, pbb[4] = {bb.x, bb.y, bb.z, bb.w};
-            const float pis[4] = {is.x, is.y, is.z, is.w};
-            float dz[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {  // the arithmetic of bnselu_bwd_kernel
-              const float zc = (cv[e] + pcb[e]) - pmu[e];
-              const float xhat = zc * pis[e];
-              const float u = fmaf(zc, psg[e], pbb[e]);
-              const float sd = u > 0.f ? 1.0507009873554805f : 1.0507009873554805f * 1.6732632423543772f * __expf(u);
-              const float du = hround(v[e]) * sd;
-              dz[e] = du * psg[e];
-              bsum[0][t][g][e] += dz[e];
-              bsum[1][t][g][e] = fmaf(du, xhat, bsum[1][t][g][e]);
-              bsum[2][t][g][e] += du;
-            }
-            *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(dz[0], dz[1]), sc_pack2(dz[2], dz[3]));
-            continue;
-          }
-          if (a.res) {   // the sum autograd would form: the bf16 convolution output plus the residual gradient
-            const uint2 rr = rres[kBnBwd ? 0 : t][g];
-            v[0] = hround(v[0]) + hlo(rr.x);
-            v[1] = hround(v[1]) + hhi(rr.x);
-            v[2] = hround(v[2]) + hlo(rr.y);
-            v[3] = hround(v[3]) + hhi(rr.y);
-          }
-          *reinterpret_cast<uint2*>(a.y + obase + co) = make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]));
-          if (a.y2) {
-            const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
-            const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
-            const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
-            const float4 bb = *reinterpret_cast<const float4*>(sbn + 3 * CO + co);
-            const float pcb[4] = {cb.x, cb.y, cb.z, cb.w}, pmu[4] = {mu.x, mu.y, mu.z, mu.w};
-            const float psg[4] = {sg.x, sg.y, sg.z, sg.w}, pbb[4] = {bb.x, bb.y, bb.z, bb.w};
-            float u[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)  // the arithmetic of bnselu_fwd_kernel on the bf16 conv output
-              u[e] = sc_selu(fmaf((hround(v[e]) + pcb[e]) - pmu[e], psg[e], pbb[e]));
-            *reinterpret_cast<uint2*>(a.y2 + obase + co) = make_uint2(sc_pack2(u[0], u[1]), sc_pack2(u[2], u[3]));
-          }
-        }
-    }
+    // the next input row into the slot this row does not read (its last reader, row ho - 1, is behind the previous
+    // barrier), before the epilogue's stores
     if (more) sc_store_row<CI>(xs + ((ho + KH) % NSLOT) * SLOT, pre);
+    // epilogue: lane owns position p, channels co = t*32 + 8g + 4h + e
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int co = t * 32 + 8 * g + 4 * h;
+        const uint32_t off = orow + (t * 32 + 8 * g) * 2;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * g + e];
+        if constexpr (kBnBwd) {
+          const uint2 cc = cres[t][g];
+          const float cv[4] = {hlo(cc.x), hhi(cc.x), hlo(cc.y), hhi(cc.y)};
+          const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
+          const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
+          const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
+          const float4 bb = *reinterpret_cast<const float4*>(sbn + 3 * CO + co);
+          const float4 is = *reinterpret_cast<const float4*>(sbn + 4 * CO + co);
+          const float pcb[4] = {cb.x, cb.y, cb.z, cb.w}, pmu[4] = {mu.x, mu.y, mu.z, mu.w};
+          const float psg[4] = {sg.x, sg.y, sg.z, sg.w}, pbb[4] = {bb.x, bb.y, bb.z, bb.w};
+          const float pis[4] = {is.x, is.y, is.z, is.w};
+          float dz[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {  // the arithmetic of bnselu_bwd_kernel
+            const float zc = (cv[e] + pcb[e]) - pmu[e];
+            const float xhat = zc * pis[e];
+            const float u = fmaf(zc, psg[e], pbb[e]);
+            const float sd = u > 0.f ? 1.0507009873554805f : 1.0507009873554805f * 1.6732632423543772f * __expf(u);
+            const float du = hround(v[e]) * sd;
+            dz[e] = du * psg[e];
+            // a position past W has no gradient (its lane's sums skip it)
+            bsum[0][t][g][e] += pv ? dz[e] : 0.f;
+            bsum[1][t][g][e] = pv ? fmaf(du, xhat, bsum[1][t][g][e]) : bsum[1][t][g][e];
+            bsum[2][t][g][e] += pv ? du : 0.f;
+          }
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(v2u32, make_uint2(sc_pack2(dz[0], dz[1]), sc_pack2(dz[2], dz[3]))), ry, off, 0, 0);
+          continue;
+        }
+        if (a.res) {   // the sum autograd would form: the bf16 convolution output plus the residual gradient
+          const uint2 rr = cres[t][g];
+          v[0] = hround(v[0]) + hlo(rr.x);
+          v[1] = hround(v[1]) + hhi(rr.x);
+          v[2] = hround(v[2]) + hlo(rr.y);
+          v[3] = hround(v[3]) + hhi(rr.y);
+        }
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(v2u32, make_uint2(sc_pack2(v[0], v[1]), sc_pack2(v[2], v[3]))), ry, off, 0, 0);
+        if (a.y2) {
+          const float4 cb = *reinterpret_cast<const float4*>(sbn + co);
+          const float4 mu = *reinterpret_cast<const float4*>(sbn + CO + co);
+          const float4 sg = *reinterpret_cast<const float4*>(sbn + 2 * CO + co);
+          const float4 bb = *reinterpret_cast<const float4*>(sbn + 3 * CO + co);
+          const float pcb[4] = {cb.x, cb.y, cb.z, cb.w}, pmu[4] = {mu.x, mu.y, mu.z, mu.w};
+          const float psg[4] = {sg.x, sg.y, sg.z, sg.w}, pbb[4] = {bb.x, bb.y, bb.z, bb.w};
+          float u[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)  // the arithmetic of bnselu_fwd_kernel on the bf16 conv output
+            u[e] = sc_selu(fmaf((hround(v[e]) + pcb[e]) - pmu[e], psg[e], pbb[e]));
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(v2u32, make_uint2(sc_pack2(u[0], u[1]), sc_pack2(u[2], u[3]))), ry2, off, 0, 0);
+        }
+      }
     __syncthreads();
   }
   if constexpr (kBnBwd) {
@@ -478,6 +503,9 @@ __global__ void sconv_wgrad_reduce2_kernel(const float* __restrict__ part2, int6
 
 template <int CI, int CO, int KH, bool kBnBwd = false>
 static int sconv_fwd_launch(const SConvArgs& a, hipStream_t st) {
+  // the kernel's per-utterance buffer ranges and 32-bit offsets (the sentinel SC_OOB must lie past every range)
+  if ((int64_t)a.H * a.W * CI * 2 >= (int64_t)SC_OOB - 4096 || (int64_t)a.Ho * a.W * CO * 2 >= (int64_t)SC_OOB - 4096)
+    return RDX_EUNSUPPORTED;
   const size_t smem = (size_t)(KH + 1) * SC_PW * CI * 2 + (size_t)KH * 3 * CO * CI * 2 + 5 * CO * sizeof(float);
   const int strips = (a.W + SC_P - 1) / SC_P;
   // one round of resident workgroups (256 CUs x the workgroups the LDS image allows per CU: 4 at 32 x 32
