@@ -348,6 +348,7 @@ constexpr int BXB_PR = 6 * 16 * 16;                  // conv1 / frozen-BN record
 constexpr int BXB_LDS = 192 * 64 + 3 * BX_IMG + 2 * BX_IMG + 2 * BXB_DCR * 64 + 4 * BXB_XW * 4 + BXB_XS + BXB_WDX +
                         BXB_OB + BXB_PR;
 constexpr int BXB_BLOCKS = 512;
+constexpr int BXB_PD = 2;                            // phase B's dout1 MFMA operands read this many steps ahead
 static_assert(2 * BXB_LDS <= 160 * 1024, "two workgroups per CU");
 
 
@@ -593,17 +594,21 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
         // weight rows tap * 32 + r: 2048 bytes per tap; input rows pw + kw
         const int wo0 = bx_img(r, hh), wo1 = bx_img(r, 2 + hh);
+        // steps (kh, kw, s) in the same order, each step's two operand reads issued BXB_PD steps ahead of its MFMA
+        // (the scheduler would otherwise pull them back next to it and expose the LDS latency at every step)
+        {
+          constexpr int PD = BXB_PD;
+          hx8 xq[12], wq[12];
 #pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-          const char* dk = ds_slot(hp - 1 + kh);
-#pragma unroll
-          for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const hx8 xf = *reinterpret_cast<const hx8*>(dk + bx_img(pw + kw, 2 * s + hh));
-              const hx8 wf = *reinterpret_cast<const hx8*>(wsf + (kh * 3 + kw) * 2048 + (s ? wo1 : wo0));
-              acc = mfma32x32x16(wf, xf, acc);
+          for (int q = 0; q < 12 + PD; ++q) {
+            if (q < 12) {
+              const int kh = q / 6, kw = (q / 2) % 3, s = q & 1;
+              xq[q] = *reinterpret_cast<const hx8*>(ds_slot(hp - 1 + kh) + bx_img(pw + kw, 2 * s + hh));
+              wq[q] = *reinterpret_cast<const hx8*>(wsf + (kh * 3 + kw) * 2048 + (s ? wo1 : wo0));
             }
+            if (q >= PD) acc = mfma32x32x16(wq[q - PD], xq[q - PD], acc);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
         char* dcs = dcr + (hp & 1) * (BXB_DCR * 64);
 #pragma unroll
@@ -618,16 +623,28 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
         const char* oi1 = o1r + ((hp + 1) & 1) * BX_IMG;     // taps 4, 5: kh = 1
         const int2 offb0 = bx_tr_off(2 + kw0, lane), offb1 = bx_tr_off(3 + (wv >> 1), lane);
         const int s1 = 4 * (wv & 1);
-#pragma unroll 2
-        for (int s = 0; s < 8; ++s) {
-          hx8 av = bx_read_tr_at(dsi, off_ds, s);
-          if (s == 7 && tail_lane) {
-            av[6] = (hel)0.0f;
-            av[7] = (hel)0.0f;
+        // K steps s in order, their reads BXB_PD steps ahead (the taps-4/5 operand is read at every step and used
+        // at the wave's four)
+        constexpr int PD = BXB_PD;
+        hx8 aq[8], bq0[8], bq1[8];
+#pragma unroll
+        for (int q = 0; q < 8 + PD; ++q) {
+          if (q < 8) {
+            aq[q] = bx_read_tr_at(dsi, off_ds, q);
+            bq0[q] = bx_read_tr_at(oi0, offb0, q);
+            bq1[q] = bx_read_tr_at(oi1, offb1, q);
           }
-          acc2[0] = mfma32x32x16(av, bx_read_tr_at(oi0, offb0, s), acc2[0]);
-          if (s >= s1 && s < s1 + 4)
-            acc2[1] = mfma32x32x16(av, bx_read_tr_at(oi1, offb1, s), acc2[1]);
+          if (q >= PD) {
+            const int s = q - PD;
+            hx8 av = aq[s];
+            if (s == 7 && tail_lane) {
+              av[6] = (hel)0.0f;
+              av[7] = (hel)0.0f;
+            }
+            acc2[0] = mfma32x32x16(av, bq0[s], acc2[0]);
+            if (s >= s1 && s < s1 + 4) acc2[1] = mfma32x32x16(av, bq1[s], acc2[1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
       __syncthreads();
@@ -716,14 +733,18 @@ __global__ __launch_bounds__(BX_T, 2) void b0x_bwd_kernel(BxBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[i] = 0.f;
             const int kp = 32 * wv - 2 + r;
-#pragma unroll 2
-            for (int s = 0; s < 6; ++s) {
-              const int img = s >> 1;
-              const char* src = img == 0 ? dcA : (img == 1 ? dcB : dsP);
-              const hx8 bv =
-                  *reinterpret_cast<const hx8*>(src + bx_img(kp + (img == 2 ? 3 : 2), 2 * (s & 1) + hh));
-              const hx8 wa = *reinterpret_cast<const hx8*>(wdx + (r < 3 ? (s * 6 + hh * 3 + r) * 16 : 576));
-              o = mfma32x32x16(wa, bv, o);
+            constexpr int PD = BXB_PD;   // reads PD steps ahead, as in phase B
+            hx8 bq[6], wq[6];
+#pragma unroll
+            for (int q = 0; q < 6 + PD; ++q) {
+              if (q < 6) {
+                const int img = q >> 1;
+                const char* src = img == 0 ? dcA : (img == 1 ? dcB : dsP);
+                bq[q] = *reinterpret_cast<const hx8*>(src + bx_img(kp + (img == 2 ? 3 : 2), 2 * (q & 1) + hh));
+                wq[q] = *reinterpret_cast<const hx8*>(wdx + (r < 3 ? (q * 6 + hh * 3 + r) * 16 : 576));
+              }
+              if (q >= PD) o = mfma32x32x16(wq[q - PD], bq[q - PD], o);
+              __builtin_amdgcn_sched_barrier(0);
             }
             if (hh == 0) {   // D[m][n]: element i of lane n < 32 holds m = i for i < 3
               ob[kp + 2] = o[0];

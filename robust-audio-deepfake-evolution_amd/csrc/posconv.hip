@@ -186,16 +186,33 @@ __global__ __launch_bounds__(256, 2) void posconv2_kernel(const hst* __restrict_
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
   // tap kk from image buf: the B fragments [nt * 4 + s] = W[kk][nt * 32 + r][16 s + 8 hh .. + 7]
+  // every LDS read of the tap (8 B fragments, both M tiles' 4 A fragments; the second tile's rows stay inside the
+  // window) issued before its first MFMA, with a scheduling barrier so they are not pulled back one by one to
+  // their MFMAs: the MFMAs then wait on a decreasing count instead of a full LDS round trip each
   auto tap = [&](int kk, int buf) {
-    hx8 bf[8];
+    hx8 bf[8], af[2][4];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
         bf[nt * 4 + s2] =
             *reinterpret_cast<const hx8*>(wimg + buf * PC2_WIMG + (nt * 32 + r) * PC_LDW + 16 * s2 + 8 * hh);
-    if (one) pc_tap(acc[0], &win[r0 + r + kk][8 * hh], bf);
-    if (two) pc_tap(acc[1], &win[r0 + 32 + r + kk][8 * hh], bf);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        af[mt][s2] = *reinterpret_cast<const hx8*>(&win[r0 + 32 * mt + r + kk][8 * hh] + 16 * s2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      if (!(mt == 0 ? one : two)) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {   // pc_tap's order
+        acc[mt][0] = mfma32x32x16(af[mt][s2], bf[s2], acc[mt][0]);
+        acc[mt][1] = mfma32x32x16(af[mt][s2], bf[4 + s2], acc[mt][1]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
   };
   static_assert(PC_K % 2 == 0, "taps in pairs");
   for (int k = 0; k < PC_K; k += 2) {
