@@ -184,7 +184,7 @@ def shape_table(shape_rows, kernel, steps):
     bound, kind = KERNEL_BOUND.get(kernel, ("hbm", None))
     out = {}
     for k, r in shape_rows.items():
-        if not k.startswith(kernel + "["):
+        if not k.startswith(kernel + "[") or r["avg_ms"] <= 0:   # a shape with no timed launch (short runs)
             continue
         rate = r["avg_work"] / (r["avg_ms"] * 1e-3) / (1e12 if bound == "mfma" else 1e9)
         peak = PEAKS[kind] if bound == "mfma" else PEAKS["hbm"]

@@ -67,14 +67,42 @@ __device__ __forceinline__ void se_unpack(uint4 u, float* v) {
   }
 }
 
+// the utterance's [T, C] 16-bit rows into an LDS image (256 threads; every 16-byte load of a batch of 8 per thread
+// in flight before its LDS stores, from clamped addresses): the passes over the rows then read LDS, not one
+// dependent global round trip per row group or per row
+__device__ __forceinline__ void head_stage(char* img, const hst* fb, int T, int C) {
+  const int n = T * C / 8;
+  const uint4* src = reinterpret_cast<const uint4*>(fb);
+  for (int base = 0; base < n; base += 8 * 256) {
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * 256 + threadIdx.x;
+      v[j] = src[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * 256 + threadIdx.x;
+      if (i < n) reinterpret_cast<uint4*>(img)[i] = v[j];
+    }
+  }
+}
 __global__ __launch_bounds__(SE_T) void se_fwd_kernel(SeArgs a) {
   __shared__ float red[SE_T * SE_CH];
   __shared__ float sm[SE_CMAX], sh[SE_RMAX], ss[SE_CMAX];
+  extern __shared__ __attribute__((aligned(16))) char se_lds[];   // x image [T][C]
+  __shared__ hst sw1[SE_RMAX * SE_CMAX], sw2[SE_CMAX * SE_RMAX];
   const int b = blockIdx.x, T = a.T, C = a.C, R = a.R;
-  const hst* xb = a.x + (int64_t)b * T * C;
+  const uint4* ximg = reinterpret_cast<const uint4*>(se_lds);
+  head_stage(se_lds, a.x + (int64_t)b * T * C, T, C);
+  for (int i = threadIdx.x; i < R * C; i += SE_T) {
+    sw1[i] = a.w1[i];
+    sw2[i] = a.w2[i];
+  }
+  __syncthreads();
   se_colsum(red, sm, T, C, [&](int t, int q, float* acc) {
     float v[SE_CH];
-    se_unpack(*reinterpret_cast<const uint4*>(xb + (int64_t)t * C + q * SE_CH), v);
+    se_unpack(ximg[t * (C / SE_CH) + q], v);
 #pragma unroll
     for (int k = 0; k < SE_CH; ++k) acc[k] += v[k];
   });
@@ -85,19 +113,25 @@ __global__ __launch_bounds__(SE_T) void se_fwd_kernel(SeArgs a) {
     a.m[(int64_t)b * C + c] = f2h(mv);
   }
   __syncthreads();
-  if (threadIdx.x < R) {   // fc1 + relu
-    const int j = threadIdx.x;
+  {   // fc1 + relu: 16 lanes per output j (lane l takes c = l, l + 16, ...; the 16 partials added by a butterfly),
+      // weights read from the image staged with x
+    const int j = threadIdx.x >> 4, l = threadIdx.x & 15;
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(sm[c], h2f(a.w1[(int64_t)j * C + c]), acc);
-    const float hv = fmaxf(hround(acc), 0.f);
-    sh[j] = hv;
-    a.h[(int64_t)b * R + j] = f2h(hv);
+    if (j < R)
+      for (int c = l; c < C; c += 16) acc = fmaf(sm[c], h2f(sw1[j * C + c]), acc);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (j < R && l == 0) {
+      const float hv = fmaxf(hround(acc), 0.f);
+      sh[j] = hv;
+      a.h[(int64_t)b * R + j] = f2h(hv);
+    }
   }
   __syncthreads();
   if (threadIdx.x < C) {   // fc2 + sigmoid
     const int c = threadIdx.x;
     float acc = 0.f;
-    for (int j = 0; j < R; ++j) acc = fmaf(sh[j], h2f(a.w2[(int64_t)c * R + j]), acc);
+    for (int j = 0; j < R; ++j) acc = fmaf(sh[j], h2f(sw2[c * R + j]), acc);
     const float z = hround(acc);
     const float sv = hround(1.0f / (1.0f + __expf(-z)));
     ss[c] = sv;
@@ -110,7 +144,7 @@ __global__ __launch_bounds__(SE_T) void se_fwd_kernel(SeArgs a) {
   for (int i = threadIdx.x; i < T * nq; i += SE_T) {
     const int t = i / nq, q = i % nq;
     float v[SE_CH];
-    se_unpack(*reinterpret_cast<const uint4*>(xb + (int64_t)t * C + q * SE_CH), v);
+    se_unpack(ximg[i], v);
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = hpack2(v[2 * j] * ss[q * SE_CH + 2 * j], v[2 * j + 1] * ss[q * SE_CH + 2 * j + 1]);
@@ -134,42 +168,53 @@ struct SeBwdArgs {
 __global__ __launch_bounds__(SE_T) void se_bwd_kernel(SeBwdArgs a) {
   __shared__ float red[SE_T * SE_CH];
   __shared__ float sds[SE_CMAX], sdz[SE_CMAX], sdh[SE_RMAX], sdm[SE_CMAX], ssv[SE_CMAX];
+  extern __shared__ __attribute__((aligned(16))) char se_lds[];   // dy image [T][C], then x image [T][C]
   const int b = blockIdx.x, T = a.T, C = a.C, R = a.R;
-  const hst* dyb = a.dy + (int64_t)b * T * C;
-  const hst* xb = a.x + (int64_t)b * T * C;
+  const uint4* dimg = reinterpret_cast<const uint4*>(se_lds);
+  const uint4* ximg = reinterpret_cast<const uint4*>(se_lds + T * C * 2);
+  __shared__ hst sw1[SE_RMAX * SE_CMAX], sw2[SE_CMAX * SE_RMAX];
+  __shared__ float shv[SE_RMAX], smv[SE_CMAX];
+  head_stage(se_lds, a.dy + (int64_t)b * T * C, T, C);
+  head_stage(se_lds + T * C * 2, a.x + (int64_t)b * T * C, T, C);
+  for (int i = threadIdx.x; i < R * C; i += SE_T) {
+    sw1[i] = a.w1[i];
+    sw2[i] = a.w2[i];
+  }
+  if (threadIdx.x < R) shv[threadIdx.x] = h2f(a.h[(int64_t)b * R + threadIdx.x]);
+  if (threadIdx.x < C) smv[threadIdx.x] = h2f(a.m[(int64_t)b * C + threadIdx.x]);
+  __syncthreads();
   // ds = sum_t round(dy * x)
   se_colsum(red, sds, T, C, [&](int t, int q, float* acc) {
     float d[SE_CH], v[SE_CH];
-    se_unpack(*reinterpret_cast<const uint4*>(dyb + (int64_t)t * C + q * SE_CH), d);
-    se_unpack(*reinterpret_cast<const uint4*>(xb + (int64_t)t * C + q * SE_CH), v);
+    se_unpack(dimg[t * (C / SE_CH) + q], d);
+    se_unpack(ximg[t * (C / SE_CH) + q], v);
 #pragma unroll
     for (int k = 0; k < SE_CH; ++k) acc[k] += hround(d[k] * v[k]);
   });
   float* prow = a.part + (int64_t)b * (2 * R * C);
-  if (threadIdx.x < C) {   // sigmoid backward; dW2 [C, R] row c = dz[c] h
+  if (threadIdx.x < C) {   // sigmoid backward
     const int c = threadIdx.x;
     const float sv = h2f(a.s[(int64_t)b * C + c]);
     ssv[c] = sv;
-    const float dz = hround(hround(sds[c]) * (sv * (1.0f - sv)));
-    sdz[c] = dz;
-    for (int j = 0; j < R; ++j) prow[R * C + c * R + j] = dz * h2f(a.h[(int64_t)b * R + j]);
+    sdz[c] = hround(hround(sds[c]) * (sv * (1.0f - sv)));
   }
   __syncthreads();
-  if (threadIdx.x < R) {   // fc2's input gradient, relu'
-    const int j = threadIdx.x;
+  for (int i = threadIdx.x; i < C * R; i += SE_T) prow[R * C + i] = sdz[i / R] * shv[i % R];   // dW2 [C, R] = dz h^T
+  {   // fc2's input gradient, relu': 16 lanes per j, as the forward's fc1
+    const int j = threadIdx.x >> 4, l = threadIdx.x & 15;
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(sdz[c], h2f(a.w2[(int64_t)c * R + j]), acc);
-    sdh[j] = h2f(a.h[(int64_t)b * R + j]) > 0.f ? hround(acc) : 0.f;
+    if (j < R)
+      for (int c = l; c < C; c += 16) acc = fmaf(sdz[c], h2f(sw2[c * R + j]), acc);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (j < R && l == 0) sdh[j] = shv[j] > 0.f ? hround(acc) : 0.f;
   }
   __syncthreads();
-  if (threadIdx.x < C) {   // fc1's input gradient; dW1 [R, C] column c = dh m[c]; the mean's backward
+  for (int i = threadIdx.x; i < R * C; i += SE_T) prow[i] = sdh[i / C] * smv[i % C];   // dW1 [R, C] = dh m^T
+  if (threadIdx.x < C) {   // fc1's input gradient; the mean's backward
     const int c = threadIdx.x;
     float acc = 0.f;
-    const float mv = h2f(a.m[(int64_t)b * C + c]);
-    for (int j = 0; j < R; ++j) {
-      acc = fmaf(sdh[j], h2f(a.w1[(int64_t)j * C + c]), acc);
-      prow[j * C + c] = sdh[j] * mv;
-    }
+    for (int j = 0; j < R; ++j) acc = fmaf(sdh[j], h2f(sw1[j * C + c]), acc);
     sdm[c] = hround(hround(acc) / (float)T);
   }
   __syncthreads();
@@ -178,7 +223,7 @@ __global__ __launch_bounds__(SE_T) void se_bwd_kernel(SeBwdArgs a) {
   for (int i = threadIdx.x; i < T * nq; i += SE_T) {
     const int t = i / nq, q = i % nq;
     float d[SE_CH];
-    se_unpack(*reinterpret_cast<const uint4*>(dyb + (int64_t)t * C + q * SE_CH), d);
+    se_unpack(dimg[i], d);
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -195,7 +240,8 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n1 + n2) return;
   float sum = 0.f;
-  for (int b = 0; b < B; ++b) sum += part[(int64_t)b * (n1 + n2) + i];
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) sum += part[(int64_t)b * (n1 + n2) + i];   // in order; 8 loads in flight
   if (i < n1) g1[i] += sum;
   else g2[i - n1] += sum;
 }
@@ -244,18 +290,68 @@ __device__ __forceinline__ float ap_block_max(float v, float* red) {
   return s;
 }
 
+// f [T, C] of the utterance staged in LDS once (every 16-byte load of a batch in flight before its stores), then
+// read from there by the score pass (a thread per row) and the weighted sum (a thread per (8-channel chunk, row
+// group), the groups' partial sums added in group order): the global reads were one dependent round trip per row
+// and per step of a per-channel loop over T.
+constexpr int AP_LDS_MAX = 128 * 1024;   // f image bytes
+static_assert(AP_LDS_MAX + 2 * 1024 * 4 + 2 * 1024 * 4 + 8 * 256 * 4 + 64 <= 160 * 1024, "LDS budget");
+// sum over t of wt(t) * f[t, chunk q] for this thread's (chunk, row group), the groups' partials through `red`
+// ([G][C] floats) added in group order into out[c] (thread c < C)
+template <class Wt>
+__device__ __forceinline__ void ap_colsum(const char* img, float* red, float* out, int T, int C, Wt wt) {
+  const int nq = C / 8, G = AP_T / nq;
+  const int q = threadIdx.x % nq, g = threadIdx.x / nq;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (g < G)
+    for (int t = g; t < T; t += G) {
+      float v[8];
+      se_unpack(reinterpret_cast<const uint4*>(img)[t * nq + q], v);
+      const float wv = wt(t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = fmaf(wv, v[k], acc[k]);
+    }
+  __syncthreads();
+  if (g < G)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[g * C + 8 * q + k] = acc[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += AP_T) {
+    float sum = 0.f;
+    for (int gg = 0; gg < G; ++gg) sum += red[gg * C + c];
+    out[c] = sum;
+  }
+  __syncthreads();
+}
+// dynamic LDS: f image [T][C] 16-bit | per-row floats x 2 [AP_TMAX] | per-channel floats x 2 [1024] | the row
+// groups' partials [G][C] (G C = 8 G nq <= 8 AP_T floats) | block-reduction scratch
+__host__ __device__ constexpr int ap_lds_bytes(int T, int C) {
+  return T * C * 2 + 2 * AP_TMAX * 4 + 2 * 1024 * 4 + 8 * AP_T * 4 + 64;
+}
+
 __global__ __launch_bounds__(AP_T) void attn_pool_fwd_kernel(ApArgs a) {
-  __shared__ float sz[AP_TMAX], red[AP_T / 64];
+  extern __shared__ __attribute__((aligned(16))) char ap_lds[];
   const int b = blockIdx.x, T = a.T, C = a.C;
-  const hst* fb = a.f + (int64_t)b * T * C;
+  char* img = ap_lds;
+  float* sz = reinterpret_cast<float*>(ap_lds + T * C * 2);
+  float* sw = sz + 2 * AP_TMAX;
+  float* sout = sw + 1024;
+  float* red2 = sout + 1024;
+  float* red = red2 + 8 * AP_T;
+  head_stage(img, a.f + (int64_t)b * T * C, T, C);
+  for (int c = threadIdx.x; c < C; c += AP_T) sw[c] = h2f(a.w[c]);
   const float bias = a.bias ? h2f(a.bias[0]) : 0.f;
-  // scores: one wave per row, lanes over channels
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int t = w; t < T; t += AP_T / 64) {
+  __syncthreads();
+  const int nq = C / 8;
+  for (int t = threadIdx.x; t < T; t += AP_T) {   // scores: a thread per row
     float acc = 0.f;
-    for (int c = lane; c < C; c += 64) acc = fmaf(h2f(fb[(int64_t)t * C + c]), h2f(a.w[c]), acc);
-    acc = wave_sum(acc);
-    if (lane == 0) sz[t] = hround(acc + bias);
+    for (int q = 0; q < nq; ++q) {
+      float v[8];
+      se_unpack(reinterpret_cast<const uint4*>(img)[t * nq + q], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = fmaf(v[k], sw[8 * q + k], acc);
+    }
+    sz[t] = hround(acc + bias);
   }
   __syncthreads();
   float mx = -INFINITY;
@@ -276,11 +372,8 @@ __global__ __launch_bounds__(AP_T) void attn_pool_fwd_kernel(ApArgs a) {
     sz[t] = hround(av);
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += AP_T) {
-    float acc = 0.f;
-    for (int t = 0; t < T; ++t) acc = fmaf(sz[t], h2f(fb[(int64_t)t * C + c]), acc);
-    a.feat[(int64_t)b * C + c] = f2h(acc);
-  }
+  ap_colsum(img, red2, sout, T, C, [&](int t) { return sz[t]; });
+  for (int c = threadIdx.x; c < C; c += AP_T) a.feat[(int64_t)b * C + c] = f2h(sout[c]);
 }
 
 struct ApBwdArgs {
@@ -294,43 +387,62 @@ struct ApBwdArgs {
 };
 
 __global__ __launch_bounds__(AP_T) void attn_pool_bwd_kernel(ApBwdArgs a) {
-  __shared__ float sa[AP_TMAX], sdz[AP_TMAX], sdf[1024], red[AP_T / 64];
-  const int b = blockIdx.x, T = a.T, C = a.C;
-  const hst* fb = a.f + (int64_t)b * T * C;
-  for (int c = threadIdx.x; c < C; c += AP_T) sdf[c] = h2f(a.dfeat[(int64_t)b * C + c]);
+  extern __shared__ __attribute__((aligned(16))) char ap_lds[];
+  const int b = blockIdx.x, T = a.T, C = a.C, nq = C / 8;
+  char* img = ap_lds;
+  float* sa = reinterpret_cast<float*>(ap_lds + T * C * 2);
+  float* sdz = sa + AP_TMAX;
+  float* sdf = sdz + AP_TMAX;
+  float* sw = sdf + 1024;
+  float* red2 = sw + 1024;
+  float* red = red2 + 8 * AP_T;
+  head_stage(img, a.f + (int64_t)b * T * C, T, C);
+  for (int c = threadIdx.x; c < C; c += AP_T) {
+    sdf[c] = h2f(a.dfeat[(int64_t)b * C + c]);
+    sw[c] = h2f(a.w[c]);
+  }
   for (int t = threadIdx.x; t < T; t += AP_T) sa[t] = a.a[(int64_t)b * T + t];
   __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int t = w; t < T; t += AP_T / 64) {   // da = round(f dfeat)
+  for (int t = threadIdx.x; t < T; t += AP_T) {   // da = round(f dfeat): a thread per row
     float acc = 0.f;
-    for (int c = lane; c < C; c += 64) acc = fmaf(h2f(fb[(int64_t)t * C + c]), sdf[c], acc);
-    acc = wave_sum(acc);
-    if (lane == 0) sdz[t] = hround(acc);
+    for (int q = 0; q < nq; ++q) {
+      float v[8];
+      se_unpack(reinterpret_cast<const uint4*>(img)[t * nq + q], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = fmaf(v[k], sdf[8 * q + k], acc);
+    }
+    sdz[t] = hround(acc);
   }
   __syncthreads();
   float dot = 0.f;
   for (int t = threadIdx.x; t < T; t += AP_T) dot = fmaf(sa[t], sdz[t], dot);
   dot = ap_block_sum(dot, red);
   __syncthreads();
-  for (int t = threadIdx.x; t < T; t += AP_T) sdz[t] = hround(sa[t] * (sdz[t] - dot));
+  float dbs = 0.f;
+  for (int t = threadIdx.x; t < T; t += AP_T) {
+    const float dz = hround(sa[t] * (sdz[t] - dot));
+    sdz[t] = dz;
+    dbs += dz;
+  }
+  dbs = ap_block_sum(dbs, red);
   __syncthreads();
-  // df = round(round(a16 dfeat) + round(dz w)); dw = sum_t dz f, db = sum_t dz
-  float* prow = a.part + (int64_t)b * (C + 1);
-  for (int c = threadIdx.x; c < C; c += AP_T) {
-    const float wc = h2f(a.w[c]), dc = sdf[c];
-    float acc = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const float fv = h2f(fb[(int64_t)t * C + c]);
-      acc = fmaf(sdz[t], fv, acc);
-      a.df[((int64_t)b * T + t) * C + c] = f2h(hround(hround(sa[t]) * dc) + hround(sdz[t] * wc));
+  // df = round(round(a16 dfeat) + round(dz w)): 16-byte chunks, every (row, chunk) in parallel
+  hst* dfb = a.df + (int64_t)b * T * C;
+  for (int i = threadIdx.x; i < T * nq; i += AP_T) {
+    const int t = i / nq, q = i - t * nq;
+    const float a16 = hround(sa[t]), dz = sdz[t];
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 8 * q + 2 * k;
+      o[k] = hpack2(hround(a16 * sdf[c]) + hround(dz * sw[c]), hround(a16 * sdf[c + 1]) + hround(dz * sw[c + 1]));
     }
-    prow[c] = acc;
+    reinterpret_cast<uint4*>(dfb)[i] = make_uint4(o[0], o[1], o[2], o[3]);
   }
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) s += sdz[t];
-    prow[C] = s;
-  }
+  // dw = sum_t dz f (row groups added in group order), db = sum_t dz
+  float* prow = a.part + (int64_t)b * (C + 1);
+  ap_colsum(img, red2, prow, T, C, [&](int t) { return sdz[t]; });
+  if (threadIdx.x == 0) prow[C] = dbs;
 }
 
 __global__ __launch_bounds__(256) void ap_wgrad_kernel(const float* __restrict__ part, int B, int C,
@@ -338,7 +450,8 @@ __global__ __launch_bounds__(256) void ap_wgrad_kernel(const float* __restrict__
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i > C) return;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += part[(int64_t)b * (C + 1) + i];
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) s += part[(int64_t)b * (C + 1) + i];   // in order; 8 loads in flight
   if (i < C) dw[i] += s;
   else if (db) db[0] += s;
 }
@@ -393,8 +506,23 @@ __global__ __launch_bounds__(256) void upcat_bwd_kernel(const hst* __restrict__ 
 
 using namespace rdx;
 
+constexpr int SE_IMG_MAX = 64 * 1024;   // bytes of one [T][C] image (the backward stages two)
 static bool se_shape_ok(int B, int T, int C, int R) {
-  return B > 0 && T > 0 && C > 0 && C % SE_CH == 0 && C <= SE_CMAX && R > 0 && R <= SE_RMAX && C / SE_CH <= 32;
+  return B > 0 && T > 0 && C > 0 && C % SE_CH == 0 && C <= SE_CMAX && R > 0 && R <= SE_RMAX && C / SE_CH <= 32 &&
+         (int64_t)T * C * 2 <= SE_IMG_MAX;
+}
+static int se_set_lds() {
+  static bool done = false;
+  if (!done) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&se_fwd_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, SE_IMG_MAX);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&se_bwd_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * SE_IMG_MAX);
+    if (e != hipSuccess) return (int)e;
+    done = true;
+  }
+  return RDX_OK;
 }
 
 extern "C" int rdx_se_fwd(const void* x, const void* w1, const void* w2, void* y, void* m, void* h, void* s, int B,
@@ -402,7 +530,8 @@ extern "C" int rdx_se_fwd(const void* x, const void* w1, const void* w2, void* y
   RDX_REQUIRE(x && w1 && w2 && y && m && h && s && se_shape_ok(B, T, C, R));
   RDX_REQUIRE((((uintptr_t)x | (uintptr_t)y) & 15) == 0);
   SeArgs a{(const hst*)x, (const hst*)w1, (const hst*)w2, (hst*)y, (hst*)m, (hst*)h, (hst*)s, B, T, C, R};
-  hipLaunchKernelGGL(se_fwd_kernel, dim3((unsigned)B), dim3(SE_T), 0, as_stream(stream), a);
+  if (const int e = se_set_lds()) return e;
+  hipLaunchKernelGGL(se_fwd_kernel, dim3((unsigned)B), dim3(SE_T), T * C * 2, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
@@ -416,7 +545,8 @@ extern "C" int rdx_se_bwd(const void* dy, const void* x, const void* w1, const v
   RDX_REQUIRE((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dx) & 15) == 0);
   SeBwdArgs a{(const hst*)dy, (const hst*)x, (const hst*)w1, (const hst*)w2, (const hst*)m, (const hst*)h,
               (const hst*)s, (hst*)dx, part, B, T, C, R};
-  hipLaunchKernelGGL(se_bwd_kernel, dim3((unsigned)B), dim3(SE_T), 0, as_stream(stream), a);
+  if (const int e = se_set_lds()) return e;
+  hipLaunchKernelGGL(se_bwd_kernel, dim3((unsigned)B), dim3(SE_T), 2 * T * C * 2, as_stream(stream), a);
   RDX_LAUNCH_CHECK();
   const int n = 2 * R * C;
   hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), part, B,
@@ -425,20 +555,41 @@ extern "C" int rdx_se_bwd(const void* dy, const void* x, const void* w1, const v
   return RDX_OK;
 }
 
+static bool ap_shape_ok(int B, int T, int C) {
+  return B > 0 && T > 0 && T <= AP_TMAX && C > 0 && C <= 1024 && C % 8 == 0 && (int64_t)T * C * 2 <= AP_LDS_MAX;
+}
+static int ap_set_lds() {
+  static bool done = false;
+  if (!done) {
+    for (const void* fn : {reinterpret_cast<const void*>(&attn_pool_fwd_kernel),
+                           reinterpret_cast<const void*>(&attn_pool_bwd_kernel)}) {
+      // the largest image (AP_LDS_MAX) with the fixed parts: 152 KB
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               ap_lds_bytes(1, AP_LDS_MAX / 2));
+      if (e != hipSuccess) return (int)e;
+    }
+    done = true;
+  }
+  return RDX_OK;
+}
+
 extern "C" int rdx_attn_pool_fwd(const void* f, const void* w, const void* bias, void* feat, float* a, int B, int T,
                                  int C, void* stream) {
-  RDX_REQUIRE(f && w && feat && a && B > 0 && T > 0 && T <= AP_TMAX && C > 0 && C <= 1024);
+  RDX_REQUIRE(f && w && feat && a && ap_shape_ok(B, T, C) && ((uintptr_t)f & 15) == 0);
+  if (const int e = ap_set_lds()) return e;
   ApArgs g{(const hst*)f, (const hst*)w, (const hst*)bias, (hst*)feat, a, B, T, C};
-  hipLaunchKernelGGL(attn_pool_fwd_kernel, dim3((unsigned)B), dim3(AP_T), 0, as_stream(stream), g);
+  hipLaunchKernelGGL(attn_pool_fwd_kernel, dim3((unsigned)B), dim3(AP_T), ap_lds_bytes(T, C), as_stream(stream), g);
   RDX_LAUNCH_CHECK();
   return RDX_OK;
 }
 
 extern "C" int rdx_attn_pool_bwd(const void* f, const void* w, const float* a, const void* dfeat, void* df, float* part,
                                  float* dw, float* db, int B, int T, int C, void* stream) {
-  RDX_REQUIRE(f && w && a && dfeat && df && part && dw && B > 0 && T > 0 && T <= AP_TMAX && C > 0 && C <= 1024);
+  RDX_REQUIRE(f && w && a && dfeat && df && part && dw && ap_shape_ok(B, T, C));
+  RDX_REQUIRE((((uintptr_t)f | (uintptr_t)df) & 15) == 0);
+  if (const int e = ap_set_lds()) return e;
   ApBwdArgs g{(const hst*)f, (const hst*)w, a, (const hst*)dfeat, (hst*)df, part, B, T, C};
-  hipLaunchKernelGGL(attn_pool_bwd_kernel, dim3((unsigned)B), dim3(AP_T), 0, as_stream(stream), g);
+  hipLaunchKernelGGL(attn_pool_bwd_kernel, dim3((unsigned)B), dim3(AP_T), ap_lds_bytes(T, C), as_stream(stream), g);
   RDX_LAUNCH_CHECK();
   hipLaunchKernelGGL(ap_wgrad_kernel, dim3((unsigned)((C + 1 + 255) / 256)), dim3(256), 0, as_stream(stream), part, B,
                      C, dw, db);

@@ -36,6 +36,7 @@ def se_eligible(x, w1, w2):
     C = x.shape[-1]
     R = w1.shape[0]
     return (C % 8 == 0 and C <= 256 and 0 < R <= 16 and tuple(w1.shape) == (R, C) and tuple(w2.shape) == (C, R)
+            and x.shape[1] * C * 2 <= 64 * 1024     # one utterance's rows fit the kernels' LDS image
             and x.dtype == torch.get_autocast_dtype("cuda"))   # the module path's output dtype then is x's
 
 
@@ -43,6 +44,8 @@ class SEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, w2, dt):
         xc = x.to(dt).contiguous()
+        if xc.data_ptr() % 16:
+            xc = xc.clone()
         w1c, w2c = _cast(w1, dt).contiguous(), _cast(w2, dt).contiguous()
         B, T, C = xc.shape
         R = w1.shape[0]
@@ -65,6 +68,8 @@ class SEFn(torch.autograd.Function):
         R = w1c.shape[0]
         dt = xc.dtype
         dyc = dy.to(dt).contiguous()
+        if dyc.data_ptr() % 16:
+            dyc = dyc.clone()
         dx = torch.empty_like(xc)
         part = torch.empty(int(_lib.lib().rdx_se_bwd_part_floats(B, C, R)), device=xc.device, dtype=torch.float32)
         need = ctx.needs_input_grad
@@ -90,13 +95,16 @@ def pool_eligible(f, lin):
     """The fused attention pooling: CUDA, 16-bit autocast, f [B, T, C] in that dtype, a 1-output linear."""
     return (f.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") in ops.HALF
             and f.dim() == 3 and f.dtype == torch.get_autocast_dtype("cuda") and lin.weight.shape[0] == 1
-            and f.shape[1] <= 1024 and f.shape[2] <= 1024)
+            and f.shape[1] <= 1024 and f.shape[2] <= 1024 and f.shape[2] % 8 == 0
+            and f.shape[1] * f.shape[2] * 2 <= 128 * 1024)   # one utterance's rows fit the kernels' LDS image
 
 
 class AttnPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f, w, bias, dt):
         fc = f.contiguous()
+        if fc.data_ptr() % 16:
+            fc = fc.clone()
         wc = _cast(w, dt).reshape(-1).contiguous()
         bc = _cast(bias, dt).reshape(-1).contiguous() if bias is not None else None
         B, T, C = fc.shape
