@@ -68,12 +68,21 @@ __global__ __launch_bounds__(LWS_THREADS) void lws_fwd_kernel(PtrTable hs, int n
   const int64_t nv = n / 4;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int l = 0; l < nl; ++l) {
-      float h[4];
-      Vec4<T>::load(reinterpret_cast<const T*>(hs.p[l]), v * 4, h);
-      const float p = s_p[l];
+    // 8 layers' loads in flight, then their FMAs in layer order (one round trip per layer before); a layer past nl
+    // re-reads the last one and is not added
+    for (int l0 = 0; l0 < nl; l0 += 8) {
+      float h[8][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = fmaf(p, h[j], acc[j]);
+      for (int k = 0; k < 8; ++k)
+        Vec4<T>::load(reinterpret_cast<const T*>(hs.p[l0 + k < nl ? l0 + k : nl - 1]), v * 4, h[k]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (l0 + k < nl) {
+          const float p = s_p[l0 + k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = fmaf(p, h[k][j], acc[j]);
+        }
+      }
     }
     Vec4<T>::store(out, v * 4, acc);
   }
@@ -96,27 +105,50 @@ __global__ __launch_bounds__(LWS_THREADS) void lws_bwd_kernel(PtrTable hs, MutPt
   softmax_into(w, nl, s_p);
   const int64_t nv = n / 4;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int l = 0; l < nl; ++l) {
-    const T* h = reinterpret_cast<const T*>(hs.p[l]);
-    T* dh = reinterpret_cast<T*>(dhs.p[l]);
-    const float p = s_p[l];
-    float dot = 0.f;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-      float gv[4], hv[4], o[4];
-      Vec4<T>::load(g, v * 4, gv);
-      Vec4<T>::load(h, v * 4, hv);
+  // v outer, layers inner in batches of 8 (g loaded once per v, 8 layers' h loads in flight before their dots and
+  // dh stores); each layer's dot still sums this thread's v in the grid-stride order, as one loop per layer did
+  float dot[LWS_MAXL];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { dot = fmaf(gv[j], hv[j], dot); o[j] = p * gv[j]; }
-      if (dh) Vec4<T>::store(dh, v * 4, o);
+  for (int l = 0; l < LWS_MAXL; ++l) dot[l] = 0.f;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    float gv[4];
+    Vec4<T>::load(g, v * 4, gv);
+#pragma unroll
+    for (int l0 = 0; l0 < LWS_MAXL; l0 += 8) {
+      if (l0 >= nl) continue;   // (continue, not break: the loop stays fully unrolled, dot[] in registers)
+      float hv[8][4];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        Vec4<T>::load(reinterpret_cast<const T*>(hs.p[l0 + k < nl ? l0 + k : nl - 1]), v * 4, hv[k]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (l0 + k < nl) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dot[l0 + k] = fmaf(gv[j], hv[k][j], dot[l0 + k]);
+          T* dh = reinterpret_cast<T*>(dhs.p[l0 + k]);
+          if (dh) {
+            const float p = s_p[l0 + k];
+            const float o[4] = {p * gv[0], p * gv[1], p * gv[2], p * gv[3]};
+            Vec4<T>::store(dh, v * 4, o);
+          }
+        }
+      }
     }
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-      int64_t i = (n & ~(int64_t)3) + threadIdx.x;
-      float gg = ld(g, i);
-      dot = fmaf(gg, ld(h, i), dot);
-      if (dh) st(dh, i, p * gg);
+  }
+#pragma unroll
+  for (int l = 0; l < LWS_MAXL; ++l) {
+    if (l >= nl) continue;
+    float d = dot[l];
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {   // tail (n % 4)
+      const T* h = reinterpret_cast<const T*>(hs.p[l]);
+      T* dh = reinterpret_cast<T*>(dhs.p[l]);
+      const int64_t i = (n & ~(int64_t)3) + threadIdx.x;
+      const float gg = ld(g, i);
+      d = fmaf(gg, ld(h, i), d);
+      if (dh) st(dh, i, s_p[l] * gg);
     }
-    dot = wave_sum(dot);
-    if (lane == 0) s_red[wid][l] = dot;
+    d = wave_sum(d);
+    if (lane == 0) s_red[wid][l] = d;
   }
   __syncthreads();
   if (threadIdx.x < nl) {
