@@ -134,9 +134,29 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// Sum over the 64 lanes, the same value in every lane, on the VALU's lane-crossing paths instead of LDS permutes
+// (six dependent ds_bpermute round trips were the latency floor of every one-wave-per-row reduction): xor 1 and
+// xor 2 by DPP quad_perm, the quads of each 8-lane half by row_half_mirror (quads 0 <-> 1), the halves of a row by
+// row_mirror (quads 0 <-> 3, 1 <-> 2), then rows by permlane16_swap and halves of the wave by permlane32_swap.
+// Every step adds a lane's value to its mirror's, whose value is the same sum in the other order, so all lanes hold
+// the bit-identical total. Call with the whole wave active (DPP reads of switched-off lanes return 0).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += dpp_f32<0xB1>(v);    // quad_perm [1, 0, 3, 2]: xor 1
+  v += dpp_f32<0x4E>(v);    // quad_perm [2, 3, 0, 1]: xor 2
+  v += dpp_f32<0x141>(v);   // row_half_mirror
+  v += dpp_f32<0x140>(v);   // row_mirror
+  {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(p[0]) + __uint_as_float(p[1]);    // rows 0 + 1, 2 + 3
+  }
+  {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(p[0]) + __uint_as_float(p[1]);    // lanes 0-31 + 32-63
+  }
   return v;
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
